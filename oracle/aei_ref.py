@@ -1,0 +1,253 @@
+"""ORACLE — CPU restatement of GHOST's AEI_Net forward (test infrastructure only).
+
+This module is the *checker* for the MI355X product path in ``ghost_amd``.  It is
+imported only by ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg; the product never imports, links or calls it, and there is
+no CPU fallback in the product that routes through here.
+
+It is a from-scratch restatement, written with ``torch.nn.functional`` ops on CPU
+(fp32 by default, fp64 on request), of the reference algorithm:
+
+* ``conv4x4``            -> /root/reference/network/AEI_Net.py:19-24
+* ``deconv4x4``          -> /root/reference/network/AEI_Net.py:27-41
+* ``MLAttrEncoder``      -> /root/reference/network/AEI_Net.py:44-95
+* ``AADGenerator``       -> /root/reference/network/AEI_Net.py:98-139
+* ``AEI_Net``            -> /root/reference/network/AEI_Net.py:143-159
+* ``AADLayer.forward``   -> /root/reference/network/AADLayer.py:20-38
+* ``AddBlocksSequential``-> /root/reference/network/AADLayer.py:40-50
+* ``AAD_ResBlk``         -> /root/reference/network/AADLayer.py:53-80
+* ``faceshifter_batch`` post-processing -> /root/reference/utils/inference/faceshifter_run.py:19-22
+* ``transform_target_to_torch``        -> /root/reference/utils/inference/core.py:13-26
+
+Parity status: PINNED.  ``tests/test_oracle_golden.py`` checks this restatement
+against golden vectors produced by running the reference ``network.AEI_Net``
+itself (``tests/golden/make_golden.py``, committed with its outputs).
+
+Parameters are a flat ``{state_dict key: tensor}`` mapping with exactly the
+reference's key names and torch layouts (Conv2d [Cout,Cin,kh,kw], ConvTranspose2d
+[Cin,Cout,kh,kw], Linear [out,in]).
+"""
+from __future__ import annotations
+
+import zlib
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+BN_EPS = 1e-5          # nn.BatchNorm2d default (AEI_Net.py:22,31)
+IN_EPS = 1e-5          # nn.InstanceNorm2d default (AADLayer.py:16)
+LRELU = 0.1            # AEI_Net.py:23,32
+
+# ----------------------------------------------------------------------------
+# architecture tables (AEI_Net.py:48-69, :101-118)
+# ----------------------------------------------------------------------------
+ENC_DOWN = [(3, 32), (32, 64), (64, 128), (128, 256), (256, 512), (512, 1024), (1024, 1024)]
+ENC_UP = {
+    "unet": [(1024, 1024), (2048, 512), (1024, 256), (512, 128), (256, 64), (128, 32)],
+    "linknet": [(1024, 1024), (1024, 512), (512, 256), (256, 128), (128, 64), (64, 32)],
+}
+# (cin, cout, c_attr) per AADBlk1..8
+GEN_BLOCKS = {
+    "unet": [(1024, 1024, 1024), (1024, 1024, 2048), (1024, 1024, 1024), (1024, 512, 512),
+             (512, 256, 256), (256, 128, 128), (128, 64, 64), (64, 3, 64)],
+    "linknet": [(1024, 1024, 1024), (1024, 1024, 1024), (1024, 1024, 512), (1024, 512, 256),
+                (512, 256, 128), (256, 128, 64), (128, 64, 32), (64, 3, 32)],
+}
+
+
+def param_specs(backbone: str = "unet", num_blocks: int = 2, c_id: int = 512) -> List[Tuple[str, Tuple[int, ...], str]]:
+    """Ordered (key, shape, kind) list matching the reference ``state_dict``.
+
+    kind in {conv, convT, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, lin_w, bias}.
+    """
+    if backbone not in GEN_BLOCKS:
+        raise ValueError(f"backbone {backbone!r} not supported by the oracle")
+    specs: List[Tuple[str, Tuple[int, ...], str]] = []
+
+    def bn(prefix: str, c: int) -> None:
+        specs.extend([(f"{prefix}.weight", (c,), "bn_w"), (f"{prefix}.bias", (c,), "bn_b"),
+                      (f"{prefix}.running_mean", (c,), "bn_rm"), (f"{prefix}.running_var", (c,), "bn_rv"),
+                      (f"{prefix}.num_batches_tracked", (), "bn_nbt")])
+
+    for i, (ci, co) in enumerate(ENC_DOWN, 1):
+        specs.append((f"encoder.conv{i}.0.weight", (co, ci, 4, 4), "conv"))
+        bn(f"encoder.conv{i}.1", co)
+    for i, (ci, co) in enumerate(ENC_UP[backbone], 1):
+        specs.append((f"encoder.deconv{i}.deconv.weight", (ci, co, 4, 4), "convT"))
+        bn(f"encoder.deconv{i}.bn", co)
+    specs.append(("generator.up1.weight", (c_id, 1024, 2, 2), "convT"))
+    specs.append(("generator.up1.bias", (1024,), "bias"))
+
+    def aad(prefix: str, c_x: int, c_attr: int) -> None:
+        specs.extend([(f"{prefix}.conv1.weight", (c_x, c_attr, 1, 1), "conv"), (f"{prefix}.conv1.bias", (c_x,), "bias"),
+                      (f"{prefix}.conv2.weight", (c_x, c_attr, 1, 1), "conv"), (f"{prefix}.conv2.bias", (c_x,), "bias"),
+                      (f"{prefix}.fc1.weight", (c_x, c_id), "lin_w"), (f"{prefix}.fc1.bias", (c_x,), "bias"),
+                      (f"{prefix}.fc2.weight", (c_x, c_id), "lin_w"), (f"{prefix}.fc2.bias", (c_x,), "bias"),
+                      (f"{prefix}.conv_h.weight", (1, c_x, 1, 1), "conv"), (f"{prefix}.conv_h.bias", (1,), "bias")])
+
+    for k, (cin, cout, ca) in enumerate(GEN_BLOCKS[backbone], 1):
+        p = f"generator.AADBlk{k}"
+        for i in range(num_blocks):
+            out = cin if i < num_blocks - 1 else cout
+            aad(f"{p}.add_blocks.{3 * i}", cin, ca)
+            specs.append((f"{p}.add_blocks.{3 * i + 2}.weight", (out, cin, 3, 3), "conv"))
+        if cin != cout:
+            aad(f"{p}.last_add_block.0", cin, ca)
+            specs.append((f"{p}.last_add_block.2.weight", (cout, cin, 3, 3), "conv"))
+    return specs
+
+
+def make_weights(specs, dtype=torch.float32) -> Dict[str, torch.Tensor]:
+    """Deterministic key-hashed weight recipe.
+
+    Every float key seeds ``np.random.Generator(PCG64(crc32(key)))``:
+    conv/convT ~ N(0, sqrt(2/(fan_in+fan_out))); linear weights and biases ~ N(0, 0.02);
+    BN gamma ~ U(0.5,1.5), beta ~ N(0,0.1), running_mean ~ N(0,0.1), running_var ~ U(0.5,1.5).
+    """
+    out: Dict[str, torch.Tensor] = {}
+    for key, shape, kind in specs:
+        if kind == "bn_nbt":
+            out[key] = torch.zeros((), dtype=torch.int64)
+            continue
+        g = np.random.Generator(np.random.PCG64(zlib.crc32(key.encode())))
+        if kind in ("conv", "convT"):
+            rf = int(np.prod(shape[2:]))
+            std = float(np.sqrt(2.0 / ((shape[0] + shape[1]) * rf)))
+            a = g.normal(0.0, std, size=shape)
+        elif kind in ("lin_w", "bias"):
+            a = g.normal(0.0, 0.02, size=shape)
+        elif kind == "bn_w" or kind == "bn_rv":
+            a = g.uniform(0.5, 1.5, size=shape)
+        elif kind in ("bn_b", "bn_rm"):
+            a = g.normal(0.0, 0.1, size=shape)
+        else:  # pragma: no cover
+            raise ValueError(kind)
+        out[key] = torch.from_numpy(np.asarray(a, dtype=np.float32)).to(dtype)
+    return out
+
+
+def make_inputs(batch: int, seed: int = 7, c_id: int = 512):
+    """Xt ~ U(-1,1) [B,3,256,256], z_id ~ N(0,1) [B,c_id] from PCG64(seed)."""
+    g = np.random.Generator(np.random.PCG64(seed))
+    xt = g.uniform(-1.0, 1.0, size=(batch, 3, 256, 256)).astype(np.float32)
+    z = g.normal(0.0, 1.0, size=(batch, c_id)).astype(np.float32)
+    return torch.from_numpy(xt), torch.from_numpy(z)
+
+
+def make_u8_crops(batch: int, seed: int = 0) -> np.ndarray:
+    """Synthetic aligned-face crops: uint8 BGR NHWC [B,256,256,3] ~ U{0..255}."""
+    g = np.random.Generator(np.random.PCG64(seed))
+    return g.integers(0, 256, size=(batch, 256, 256, 3), dtype=np.uint8)
+
+
+# ----------------------------------------------------------------------------
+# ops
+# ----------------------------------------------------------------------------
+def _bn_eval(x, p, prefix):
+    # eval-mode BatchNorm with running statistics (AEI_Net.py:22,31)
+    return F.batch_norm(x, p[f"{prefix}.running_mean"].to(x.dtype), p[f"{prefix}.running_var"].to(x.dtype),
+                        p[f"{prefix}.weight"].to(x.dtype), p[f"{prefix}.bias"].to(x.dtype), False, 0.0, BN_EPS)
+
+
+def conv4x4_block(x, p, i):
+    """Conv4x4/s2/p1 (no bias) -> BN(eval) -> LeakyReLU(0.1)   (AEI_Net.py:19-24)."""
+    y = F.conv2d(x, p[f"encoder.conv{i}.0.weight"].to(x.dtype), None, stride=2, padding=1)
+    return F.leaky_relu(_bn_eval(y, p, f"encoder.conv{i}.1"), LRELU)
+
+
+def deconv4x4_block(x, skip, p, i, backbone):
+    """ConvT4x4/s2/p1 -> BN -> LReLU -> cat((x,skip),1) | x+skip   (AEI_Net.py:27-41)."""
+    y = F.conv_transpose2d(x, p[f"encoder.deconv{i}.deconv.weight"].to(x.dtype), None, stride=2, padding=1)
+    y = F.leaky_relu(_bn_eval(y, p, f"encoder.deconv{i}.bn"), LRELU)
+    return y + skip if backbone == "linknet" else torch.cat((y, skip), dim=1)
+
+
+def up2x(x):
+    """Bilinear x2, align_corners=True (AEI_Net.py:94,125-137)."""
+    return F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=True)
+
+
+def encoder(xt, p, backbone="unet"):
+    """MLAttrEncoder.forward (AEI_Net.py:72-95) -> 8-tuple z_attr1..z_attr8."""
+    feats = []
+    x = xt
+    for i in range(1, 8):
+        x = conv4x4_block(x, p, i)
+        feats.append(x)
+    z = [feats[6]]
+    for i in range(1, 7):
+        z.append(deconv4x4_block(z[-1], feats[6 - i], p, i, backbone))
+    z.append(up2x(z[-1]))
+    return tuple(z)
+
+
+def aad_layer(h_in, z_attr, z_id, p, prefix):
+    """AADLayer.forward (AADLayer.py:20-38): IN, gamma/beta from attr (1x1) and id (Linear), sigmoid mask blend."""
+    dt = h_in.dtype
+    h = F.instance_norm(h_in, eps=IN_EPS)
+    ga = F.conv2d(z_attr, p[f"{prefix}.conv1.weight"].to(dt), p[f"{prefix}.conv1.bias"].to(dt))
+    ba = F.conv2d(z_attr, p[f"{prefix}.conv2.weight"].to(dt), p[f"{prefix}.conv2.bias"].to(dt))
+    gi = F.linear(z_id, p[f"{prefix}.fc1.weight"].to(dt), p[f"{prefix}.fc1.bias"].to(dt))
+    bi = F.linear(z_id, p[f"{prefix}.fc2.weight"].to(dt), p[f"{prefix}.fc2.bias"].to(dt))
+    c_x = h.shape[1]
+    A = ga * h + ba
+    I = gi.reshape(h.shape[0], c_x, 1, 1) * h + bi.reshape(h.shape[0], c_x, 1, 1)
+    M = torch.sigmoid(F.conv2d(h, p[f"{prefix}.conv_h.weight"].to(dt), p[f"{prefix}.conv_h.bias"].to(dt)))
+    return (1 - M) * A + M * I
+
+
+def _add_seq(h, z_attr, z_id, p, prefix, n_layers):
+    # AddBlocksSequential (AADLayer.py:40-50): every AADLayer sees the same z_attr / z_id
+    x = h
+    for i in range(n_layers):
+        x = aad_layer(x, z_attr, z_id, p, f"{prefix}.{3 * i}")
+        x = F.relu(x)
+        x = F.conv2d(x, p[f"{prefix}.{3 * i + 2}.weight"].to(x.dtype), None, padding=1)
+    return x
+
+
+def aad_resblk(h, z_attr, z_id, p, k, cin, cout, num_blocks):
+    """AAD_ResBlk.forward (AADLayer.py:74-80): x = add_blocks(h); h' = last_add_block(h) if cin != cout; x + h'."""
+    prefix = f"generator.AADBlk{k}"
+    x = _add_seq(h, z_attr, z_id, p, f"{prefix}.add_blocks", num_blocks)
+    if cin != cout:
+        h = _add_seq(h, z_attr, z_id, p, f"{prefix}.last_add_block", 1)
+    return x + h
+
+
+def generator(z_attr, z_id, p, backbone="unet", num_blocks=2):
+    """AADGenerator.forward (AEI_Net.py:122-139)."""
+    dt = z_attr[0].dtype
+    z_id = z_id.to(dt).reshape(z_id.shape[0], -1)
+    m = F.conv_transpose2d(z_id.reshape(z_id.shape[0], -1, 1, 1), p["generator.up1.weight"].to(dt),
+                           p["generator.up1.bias"].to(dt))
+    for k, (cin, cout, _ca) in enumerate(GEN_BLOCKS[backbone], 1):
+        y = aad_resblk(m, z_attr[k - 1], z_id, p, k, cin, cout, num_blocks)
+        m = up2x(y) if k < 8 else y
+    return torch.tanh(m)
+
+
+@torch.no_grad()
+def aei_forward(p, xt, z_id, backbone="unet", num_blocks=2, dtype=torch.float32):
+    """AEI_Net.forward (AEI_Net.py:153-156) -> (Y, attr)."""
+    xt = xt.to(dtype)
+    attr = encoder(xt, p, backbone)
+    return generator(attr, z_id, p, backbone, num_blocks), attr
+
+
+# ----------------------------------------------------------------------------
+# pipeline arithmetic on either side of the generator
+# ----------------------------------------------------------------------------
+def transform_target(crops_u8_bgr: np.ndarray) -> torch.Tensor:
+    """transform_target_to_torch(half=False) (core.py:13-26): BGR->RGB, /255, (x-0.5)/0.5, NHWC->NCHW view."""
+    t = torch.from_numpy(crops_u8_bgr.copy())[:, :, :, [2, 1, 0]] / 255.0
+    t = (t - 0.5) / 0.5
+    return t.permute(0, 3, 1, 2)
+
+
+def y_to_u8_bgr(y: torch.Tensor) -> np.ndarray:
+    """faceshifter_batch post-processing (faceshifter_run.py:20-22): ((Y*0.5+0.5)*255)[..., BGR] -> uint8 (trunc)."""
+    t = (y.permute(0, 2, 3, 1) * 0.5 + 0.5) * 255
+    return t[:, :, :, [2, 1, 0]].type(torch.uint8).numpy()

@@ -1,0 +1,71 @@
+"""Pin the oracle (oracle/aei_ref.py) to golden vectors produced by the reference itself
+(tests/golden/make_golden.py runs /root/reference/network/AEI_Net.py on CPU fp32)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import aei_ref
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+CASES = ["aei_unet2_b2", "aei_linknet3_b2", "aei_unet1_b1", "aei_unet3_b1"]
+
+
+def _load(name):
+    return np.load(os.path.join(GOLD, name + ".npz"))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_forward_matches_reference(name):
+    g = _load(name)
+    backbone, nb, B = str(g["backbone"]), int(g["num_blocks"]), int(g["batch"])
+    p = aei_ref.make_weights(aei_ref.param_specs(backbone, nb))
+    xt, z = aei_ref.make_inputs(B, int(g["seed"]))
+    y, attr = aei_ref.aei_forward(p, xt, z, backbone, nb)
+    # same ATen ops on the same CPU: agreement far below the 1e-3 product gate
+    assert float((y - torch.from_numpy(g["Y"])).abs().max()) < 1e-5
+    for i, a in enumerate(attr, 1):
+        assert tuple(a.shape) == tuple(g[f"attr{i}_shape"])
+        flat = a.reshape(-1).double()
+        np.testing.assert_allclose(flat[g[f"attr{i}_idx"]].float().numpy(), g[f"attr{i}_sample"], atol=1e-5, rtol=1e-5)
+        np.testing.assert_allclose(float(flat.abs().sum()), float(g[f"attr{i}_abssum"]), rtol=1e-5)
+
+
+@pytest.mark.parametrize("name", ["aei_unet2_b2", "aei_linknet3_b2"])
+def test_oracle_u8_pipeline_matches_reference(name):
+    g = _load(name)
+    backbone, nb, B = str(g["backbone"]), int(g["num_blocks"]), int(g["batch"])
+    p = aei_ref.make_weights(aei_ref.param_specs(backbone, nb))
+    _, z = aei_ref.make_inputs(B, int(g["seed"]))
+    target = aei_ref.transform_target(aei_ref.make_u8_crops(B, int(g["crops_seed"])))
+    y, _ = aei_ref.aei_forward(p, target, torch.cat([z[:1]] * B), backbone, nb)
+    assert float((y - torch.from_numpy(g["Ypipe"])).abs().max()) < 1e-5
+    u8 = aei_ref.y_to_u8_bgr(y)
+    diff = np.abs(u8.astype(np.int16) - g["U8"].astype(np.int16))
+    assert diff.max() <= 1 and (diff > 0).mean() < 1e-3
+
+
+def test_oracle_aad_layer_cases():
+    g = _load("aad_layer_cases")
+    for i, (c_x, c_a, n) in enumerate(g["cases"].tolist()):
+        specs = []
+        for k, shp, kind in [("conv1.weight", (c_x, c_a, 1, 1), "conv"), ("conv1.bias", (c_x,), "bias"),
+                             ("conv2.weight", (c_x, c_a, 1, 1), "conv"), ("conv2.bias", (c_x,), "bias"),
+                             ("fc1.weight", (c_x, 512), "lin_w"), ("fc1.bias", (c_x,), "bias"),
+                             ("fc2.weight", (c_x, 512), "lin_w"), ("fc2.bias", (c_x,), "bias"),
+                             ("conv_h.weight", (1, c_x, 1, 1), "conv"), ("conv_h.bias", (1,), "bias")]:
+            specs.append((f"case{i}.{k}", shp, kind))
+        p = aei_ref.make_weights(specs)
+        rg = np.random.Generator(np.random.PCG64(100 + i))
+        h = torch.from_numpy(rg.normal(0.5, 2.0, size=(2, c_x, n, n)).astype(np.float32))
+        za = torch.from_numpy(rg.normal(0, 1, size=(2, c_a, n, n)).astype(np.float32))
+        zi = torch.from_numpy(rg.normal(0, 1, size=(2, 512)).astype(np.float32))
+        out = aei_ref.aad_layer(h, za, zi, p, f"case{i}")
+        assert float((out - torch.from_numpy(g[f"case{i}_out"])).abs().max()) < 1e-5, (c_x, c_a, n)
+
+
+def test_param_specs_counts():
+    # 311 keys for unet/2, 399 for linknet/3
+    assert len(aei_ref.param_specs("unet", 2)) == 311
+    assert len(aei_ref.param_specs("linknet", 3)) == 399
