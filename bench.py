@@ -1,0 +1,170 @@
+"""Benchmark: swapped 256x256 frames/s of GHOST's swap forward on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W --batch 64 --backbone unet --num-blocks 2]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (driver's multi-GPU form)
+
+One step = one faceshifter_batch of B synthetic aligned-face crops per GPU, device-resident:
+uint8 BGR crops -> normalise -> AEI_Net (encoder + AAD generator, bf16) -> tanh -> uint8 BGR,
+then (N > 1) an RCCL all-gather of every rank's swapped crops (frame order = rank order).
+Weak scaling: B frames per GPU; value = N*B*K / max-over-ranks wall time of the K timed steps.
+
+Besides the JSON line's throughput, it reports
+* roofline: the AAD-layer GEMM (fused IN-normalise / gamma-beta / sigmoid-mask blend) at the
+  256x256 stage, HBM-bound: algorithmic bytes |h_in|+|z_attr|+|out| per launch / its average
+  launch time (HIP events around each launch on the launch stream, inside the timed region);
+* cpu_baseline: the CPU restatement (oracle/aei_ref.py, fp32, same ATen op sequence as the
+  reference) on this host's cores over a bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA spec
+AAD_BYTES_PER_FRAME = {"unet": 135.58e6, "linknet": 156.02e6}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="frames per GPU per step")
+    ap.add_argument("--backbone", default="unet")
+    ap.add_argument("--num-blocks", type=int, default=2)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
+    return ap.parse_args()
+
+
+def cpu_baseline(backbone, nb, seconds):
+    """Oracle (CPU fp32 restatement) frames/s on this host, bounded sample."""
+    from oracle import aei_ref
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    p = aei_ref.make_weights(aei_ref.param_specs(backbone, nb))
+    bs = 4
+    xt, z = aei_ref.make_inputs(bs, seed=3)
+    aei_ref.aei_forward(p, xt[:1], z[:1], backbone, nb)       # warm-up
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        aei_ref.aei_forward(p, xt, z, backbone, nb)
+        frames += bs
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(frames / el, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} frames of {backbone}/{nb} fp32 in batches of {bs} (oracle/aei_ref.py), {el:.1f}s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from ghost_amd.network import AEI_Net
+    from oracle.aei_ref import make_weights, param_specs   # deterministic synthetic weights (no checkpoint offline)
+
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    G = AEI_Net(a.backbone, num_blocks=a.num_blocks, c_id=512, compute_dtype=dt).eval()
+    G.load_state_dict(make_weights(param_specs(a.backbone, a.num_blocks)))
+    G = G.to(dev)
+
+    B = a.batch
+    rng = np.random.Generator(np.random.PCG64(1000 + rank))
+    crops = torch.from_numpy(rng.integers(0, 256, size=(B, 256, 256, 3), dtype=np.uint8)).to(dev)
+    z = torch.from_numpy(np.random.Generator(np.random.PCG64(1)).normal(size=(1, 512)).astype(np.float32)).to(dev)
+    out = torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev)
+    gathered = torch.empty(world * B, 256, 256, 3, dtype=torch.uint8, device=dev) if world > 1 else None
+
+    def step():
+        G.swap_u8(crops, z, out=out)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    prof = not a.no_profile
+    if prof:
+        G.profile(0b1111111)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    classes = {}
+    if prof:
+        names = ["aad_gemm_all", "aad_gemm_256", "conv3x3_all", "conv3x3_256", "in_stats_mask", "encoder", "upsample"]
+        for i, n in enumerate(names):
+            classes[n] = G.profile_read(i)
+        G.profile(0)
+
+    if rank == 0:
+        frames = world * B * a.steps
+        value = frames / el
+        res = {
+            "metric": "swapped frames/sec at 256x256 bf16 (AEI_Net unet/2 swap forward, device-resident u8 crops)",
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": a.dtype if a.dtype == "fp32" else "bf16", "data": "synthetic",
+            "config": {"workload": f"batch={B} synthetic 256x256 aligned faces per GPU, AEI_Net {a.backbone} "
+                                   f"num_blocks={a.num_blocks}, faceshifter_batch (u8 in -> u8 out)"
+                                   + (", RCCL all-gather of swapped crops" if world > 1 else ""),
+                       "global_batch": world * B, "per_gpu_batch": B, "backbone": a.backbone,
+                       "num_blocks": a.num_blocks, "parallelism": f"dp{world}"},
+        }
+        if prof and classes["aad_gemm_256"]["launches"]:
+            c = classes["aad_gemm_256"]
+            per_launch_bytes = c["bytes"] / c["launches"]
+            per_launch_s = c["ms"] / c["launches"] / 1e3
+            ach = per_launch_bytes / per_launch_s / 1e9
+            res["roofline"] = {"kernel": "AAD fused GEMM (IN-normalise + gamma/beta + sigmoid-mask blend), 256x256 stage",
+                               "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                               "bytes_per_launch": per_launch_bytes, "avg_launch_us": round(per_launch_s * 1e6, 2)}
+            cc = classes["conv3x3_all"]
+            if cc["launches"]:
+                tf = cc["flops"] / (cc["ms"] / 1e3) / 1e12
+                res["roofline_conv3x3"] = {"bound": "mfma", "achieved": round(tf, 1), "peak": BF16_PEAK_TFLOPS,
+                                           "unit": "TFLOP/s", "frac": round(tf / BF16_PEAK_TFLOPS, 4)}
+            aad = classes["aad_gemm_all"]
+            res["aad_decoder_gbs"] = round(aad["bytes"] / (aad["ms"] / 1e3) / 1e9, 1) if aad["ms"] else None
+            res["kernel_ms_per_step"] = {k: round(v["ms"] / a.steps, 3) for k, v in classes.items()}
+        if world == 1 and a.cpu_seconds > 0:
+            res["cpu_baseline"] = cpu_baseline(a.backbone, a.num_blocks, a.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,754 @@
+// ghost_amd — native runtime for the AEI_Net forward (C ABI in include/ghost_amd.h).
+//
+// The handle holds the layer plan of AEI_Net(backbone, num_blocks, c_id)
+// (network/AEI_Net.py:143-159, network/AADLayer.py) and pointers to weights that the
+// host packed once (ghost_amd/network/pack.py).  A forward is a fixed sequence of
+// launches on one stream; all intermediate tensors are carved from the caller's
+// workspace by a bump allocator, whose size is found by a dry run of the same plan.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/ghost_amd.h"
+#include "conv_igemm.h"
+#include "ghost_common.h"
+#include "ops.h"
+
+using namespace ghost;
+
+static thread_local std::string g_err;
+static int fail(int rc, const std::string& msg) {
+  g_err = msg;
+  return rc == 0 ? GHOST_EINVAL : rc;
+}
+
+extern "C" const char* ghost_version(void) { return "ghost_amd 0.1 (gfx950)"; }
+extern "C" const char* ghost_last_error(void) { return g_err.c_str(); }
+
+namespace {
+
+constexpr float kBnLrelu = 0.1f;  // LeakyReLU(0.1) (AEI_Net.py:23,32)
+
+const int kEncDown[7][2] = {{3, 32}, {32, 64}, {64, 128}, {128, 256}, {256, 512}, {512, 1024}, {1024, 1024}};
+const int kEncUpUnet[6][2] = {{1024, 1024}, {2048, 512}, {1024, 256}, {512, 128}, {256, 64}, {128, 32}};
+const int kEncUpLink[6][2] = {{1024, 1024}, {1024, 512}, {512, 256}, {256, 128}, {128, 64}, {64, 32}};
+// (cin, cout, c_attr) for AADBlk1..8 (AEI_Net.py:102-118)
+const int kGenUnet[8][3] = {{1024, 1024, 1024}, {1024, 1024, 2048}, {1024, 1024, 1024}, {1024, 512, 512},
+                            {512, 256, 256},    {256, 128, 128},    {128, 64, 64},      {64, 3, 64}};
+const int kGenLink[8][3] = {{1024, 1024, 1024}, {1024, 1024, 1024}, {1024, 1024, 512}, {1024, 512, 256},
+                            {512, 256, 128},    {256, 128, 64},     {128, 64, 32},     {64, 3, 32}};
+
+inline int rup(int v, int m) { return (v + m - 1) / m * m; }
+
+struct ProfClass {
+  double ms = 0, bytes = 0, flops = 0;
+  int64_t launches = 0;
+};
+
+}  // namespace
+
+struct ghost_aei {
+  bool linknet = false;
+  int nb = 2, c_id = 512, dt = GHOST_F32, esz = 4;
+  std::map<std::string, const void*> slots;   // name -> device pointer (nullptr = unbound)
+  int id_total = 0;                            // sum over AAD layers of 2*c_x
+  // profiling
+  int prof_mask = 0;
+  std::vector<hipEvent_t> ev;
+  struct Pending { int cls; int e0, e1; double bytes, flops; };
+  std::vector<Pending> pend;
+  int ev_used = 0;
+  ProfClass prof[8];
+
+  typedef int Pair[2];
+  typedef int Triple[3];
+  const Pair* up() const { return linknet ? kEncUpLink : kEncUpUnet; }
+  const Triple* gen() const { return linknet ? kGenLink : kGenUnet; }
+  void attr_geom(int k, int& C, int& H) const {  // k = 1..8
+    static const int hs[8] = {2, 4, 8, 16, 32, 64, 128, 256};
+    H = hs[k - 1];
+    if (k == 1) C = 1024;
+    else if (k == 8) C = linknet ? 32 : 64;
+    else C = linknet ? up()[k - 2][1] : up()[k - 2][1] * 2;
+  }
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// execution context: dry run (sizing) or real run (launches)
+// ---------------------------------------------------------------------------
+struct Ctx {
+  ghost_aei* h;
+  bool dry;
+  char* base;
+  size_t off = 0, cap = 0;
+  size_t scratch_need = 0;  // max split-K / IN-stats partial bytes
+  char* scratch = nullptr;
+  size_t scratch_cap = 0;
+  hipStream_t s;
+  int rc = 0;
+  std::string where;
+
+  void* alloc(size_t bytes) {
+    off = (off + 255) & ~size_t(255);
+    void* p = dry ? reinterpret_cast<void*>(uintptr_t(0x10000000) + off) : base + off;
+    off += bytes;
+    return p;
+  }
+  bool ok() const { return rc == 0; }
+  void check(int r, const char* what) {
+    if (r != 0 && rc == 0) {
+      rc = r;
+      where = what;
+    }
+  }
+  const void* W(const std::string& name) {
+    if (dry) return reinterpret_cast<const void*>(uintptr_t(0x1000));  // sizing needs no weights
+    auto it = h->slots.find(name);
+    if (it == h->slots.end() || !it->second) {
+      if (rc == 0) {
+        rc = GHOST_ENOTREADY;
+        where = "unbound weight slot " + name;
+      }
+      return nullptr;
+    }
+    return it->second;
+  }
+  // profiling brackets
+  int prof_begin(int cls) {
+    if (dry || !(h->prof_mask & (1 << cls))) return -1;
+    if (h->ev_used + 2 > (int)h->ev.size()) {
+      for (int i = 0; i < 64; ++i) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return -1;
+        h->ev.push_back(e);
+      }
+    }
+    int e0 = h->ev_used;
+    h->ev_used += 2;
+    (void)hipEventRecord(h->ev[e0], s);
+    return e0;
+  }
+  void prof_end(int cls, int e0, double bytes, double flops) {
+    if (e0 < 0) return;
+    (void)hipEventRecord(h->ev[e0 + 1], s);
+    h->pend.push_back({cls, e0, e0 + 1, bytes, flops});
+  }
+};
+
+// one conv launch (or its workspace accounting in the dry run)
+void run_conv(Ctx& c, ConvDesc& d, int cls_all, int cls_big, double flops) {
+  if (!c.ok()) return;
+  if (c.dry) {
+    size_t need = conv_workspace_bytes(d);
+    if (need > c.scratch_need) c.scratch_need = need;
+    return;
+  }
+  const bool big = d.Hi == 256 || d.Hi * (d.kind == CONV_T4S2 ? 2 : 1) == 256;
+  int e_all = c.prof_begin(cls_all);
+  int e_big = (big && cls_big >= 0) ? c.prof_begin(cls_big) : -1;
+  c.check(conv_launch(d, c.scratch, c.scratch_cap, c.s), "conv_launch");
+  double bytes = 0;
+  if (d.epi == EPI_AAD) {
+    // algorithmic AAD bytes: |h_in| + |z_attr| + |out|
+    const double P = (double)d.B * d.Hi * d.Wi;
+    bytes = P * (2.0 * d.C_aad + d.Cin) * (double)c.h->esz;
+  }
+  if (e_big >= 0) c.prof_end(cls_big, e_big, bytes, flops);
+  if (e_all >= 0) c.prof_end(cls_all, e_all, bytes, flops);
+}
+
+void run_stats(Ctx& c, const void* x, int ldx, int B, int HW, int C, float* stat) {
+  if (!c.ok()) return;
+  if (c.dry) {
+    size_t need = in_stats_workspace_bytes(B, HW, C);
+    if (need > c.scratch_need) c.scratch_need = need;
+    return;
+  }
+  int e = c.prof_begin(4);
+  c.check(in_stats(c.h->dt, x, ldx, B, HW, C, stat, c.scratch, c.scratch_cap, c.s), "in_stats");
+  c.prof_end(4, e, (double)B * HW * C * c.h->esz, 0);
+}
+
+void run_mask(Ctx& c, const void* x, int ldx, int B, int HW, int C, const float* stat, const float* wh,
+              const float* bh, float* mask) {
+  if (!c.ok() || c.dry) return;
+  int e = c.prof_begin(4);
+  c.check(aad_mask(c.h->dt, x, ldx, B, HW, C, stat, wh, bh, mask, c.s), "aad_mask");
+  c.prof_end(4, e, (double)B * HW * C * c.h->esz, 0);
+}
+
+void run_up(Ctx& c, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C) {
+  if (!c.ok() || c.dry) return;
+  int e = c.prof_begin(6);
+  c.check(upsample2x(c.h->dt, x, ldx, y, ldy, B, H, W, C, c.s), "upsample2x");
+  c.prof_end(6, e, (double)B * H * W * C * 5 * c.h->esz, 0);
+}
+
+// ---------------------------------------------------------------------------
+// encoder (MLAttrEncoder.forward, AEI_Net.py:72-95)
+// ---------------------------------------------------------------------------
+struct Buf {
+  void* p;
+  int ld;
+};
+
+void encoder(Ctx& c, const void* xin, int B, void* const attr[8]) {
+  ghost_aei* h = c.h;
+  const int es = h->esz;
+  // where feat_1..feat_6 live: unet -> inside z_attr_{8-j} after the deconv channels
+  Buf feat[7];
+  int Hs = 256;
+  for (int j = 1; j <= 6; ++j) {
+    const int co = kEncDown[j - 1][1];
+    if (!h->linknet) {
+      int C, H;
+      h->attr_geom(8 - j, C, H);
+      const int off = h->up()[6 - j][1];  // deconv_{7-j} output channels come first
+      feat[j] = {(char*)attr[8 - j - 1] + (size_t)off * es, C};
+    } else {
+      const int H = 256 >> j;
+      feat[j] = {c.alloc((size_t)B * H * H * co * es), co};
+    }
+  }
+  // down path: conv_i = Conv4x4/s2/p1 -> BN -> LReLU(0.1)
+  Buf in{const_cast<void*>(xin), 3};
+  for (int i = 1; i <= 7; ++i) {
+    const int ci = kEncDown[i - 1][0], co = kEncDown[i - 1][1];
+    Buf out = i <= 6 ? feat[i] : Buf{attr[0], 1024};
+    ConvDesc d;
+    d.ti = d.to = h->dt;
+    d.x = in.p; d.B = B; d.Hi = Hs; d.Wi = Hs; d.Cin = ci; d.ldx = in.ld;
+    d.w = c.W("enc.conv" + std::to_string(i) + ".w");
+    d.N = co; d.Npad = rup(co, 128); d.Kpad = rup(16 * ci, 32);
+    d.kind = CONV_FWD; d.kh = d.kw = 4; d.stride = 2; d.pad = 1;
+    d.y = out.p; d.ldy = out.ld;
+    d.scale = (const float*)c.W("enc.conv" + std::to_string(i) + ".scale");
+    d.shift = (const float*)c.W("enc.conv" + std::to_string(i) + ".shift");
+    d.slope = kBnLrelu;
+    const double Ho = Hs / 2;
+    run_conv(c, d, 5, -1, 2.0 * B * Ho * Ho * co * 16.0 * ci);
+    in = out;
+    Hs /= 2;
+  }
+  // up path: deconv_i = ConvT4x4/s2/p1 -> BN -> LReLU -> cat((x, skip)) | x + skip
+  for (int i = 1; i <= 6; ++i) {
+    int Cin, H, Cout, Ho;
+    h->attr_geom(i, Cin, H);
+    h->attr_geom(i + 1, Cout, Ho);
+    const int co = h->up()[i - 1][1];
+    ConvDesc d;
+    d.ti = d.to = h->dt;
+    d.x = attr[i - 1]; d.B = B; d.Hi = H; d.Wi = H; d.Cin = Cin; d.ldx = Cin;
+    d.w = c.W("enc.deconv" + std::to_string(i) + ".w");
+    d.N = co; d.Npad = rup(co, 128); d.Kpad = rup(4 * Cin, 32);
+    d.kind = CONV_T4S2;
+    d.y = attr[i]; d.ldy = Cout;
+    d.scale = (const float*)c.W("enc.deconv" + std::to_string(i) + ".scale");
+    d.shift = (const float*)c.W("enc.deconv" + std::to_string(i) + ".shift");
+    d.slope = kBnLrelu;
+    if (h->linknet) { d.res = feat[7 - i].p; d.ldres = feat[7 - i].ld; }
+    run_conv(c, d, 5, -1, 2.0 * B * Ho * Ho * co * 4.0 * Cin);
+  }
+  int C7, H7, C8, H8;
+  h->attr_geom(7, C7, H7);
+  h->attr_geom(8, C8, H8);
+  run_up(c, attr[6], C7, attr[7], C8, B, H7, H7, C7);
+}
+
+// ---------------------------------------------------------------------------
+// generator (AADGenerator.forward, AEI_Net.py:122-139)
+// ---------------------------------------------------------------------------
+struct GenShared {
+  const float* zid32;
+  float* idgb;
+};
+
+// one AADLayer (+ fused ReLU) -> out
+void aad(Ctx& c, const std::string& name, const void* hin, int ldh, const float* stat, const void* za, int lda,
+         int Ca, int B, int n, int C, int id_off, const float* idgb, void* out, int ldo) {
+  ghost_aei* h = c.h;
+  float* mask = (float*)c.alloc((size_t)B * n * n * sizeof(float));
+  run_mask(c, hin, ldh, B, n * n, C, stat, (const float*)c.W(name + ".wh"), (const float*)c.W(name + ".bh"), mask);
+  ConvDesc d;
+  d.ti = d.to = h->dt;
+  d.x = za; d.B = B; d.Hi = n; d.Wi = n; d.Cin = Ca; d.ldx = lda;
+  d.w = c.W(name + ".gbw");
+  d.N = 2 * C; d.Npad = rup(2 * C, 128); d.Kpad = rup(Ca, 32);
+  d.kind = CONV_FWD; d.kh = d.kw = 1; d.stride = 1; d.pad = 0;
+  d.y = out; d.ldy = ldo;
+  d.shift = (const float*)c.W(name + ".gbb");
+  d.slope = 0.0f;  // the ReLU that follows every AADLayer in AddBlocksSequential
+  d.epi = EPI_AAD;
+  d.hin = hin; d.ldh = ldh; d.stat = stat;
+  d.idgb = idgb ? idgb + id_off : nullptr; d.id_ld = h->id_total; d.mask = mask; d.C_aad = C;
+  run_conv(c, d, 0, 1, 2.0 * B * n * n * 2.0 * C * Ca);
+}
+
+void conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, int B, int n, int Cout, void* y,
+             int ldy, const void* res, int ldres, int tanh_out, uint8_t* u8) {
+  ConvDesc d;
+  d.ti = d.to = c.h->dt;
+  d.x = x; d.B = B; d.Hi = n; d.Wi = n; d.Cin = Cin; d.ldx = ldx;
+  d.w = c.W(wname);
+  d.N = Cout; d.Npad = rup(Cout, 128); d.Kpad = rup(9 * Cin, 32);
+  d.kind = CONV_FWD; d.kh = d.kw = 3; d.stride = 1; d.pad = 1;
+  d.y = y; d.ldy = ldy;
+  d.res = res; d.ldres = ldres;
+  d.tanh_out = tanh_out; d.u8 = u8;
+  run_conv(c, d, 2, 3, 2.0 * B * n * n * Cout * 9.0 * Cin);
+}
+
+void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, void* y_out, uint8_t* u8) {
+  ghost_aei* h = c.h;
+  const int es = h->esz;
+  const int nb = h->nb;
+  // identity projections of every AADLayer at once: idgb[b] = [gamma_id | beta_id] per layer (fc1/fc2)
+  float* idgb = (float*)c.alloc((size_t)B * h->id_total * sizeof(float));
+  {
+    ConvDesc d;
+    d.ti = d.to = GHOST_F32;
+    d.x = zid32; d.B = B; d.Hi = 1; d.Wi = 1; d.Cin = h->c_id; d.ldx = h->c_id;
+    d.w = c.W("gen.id.w");
+    d.N = h->id_total; d.Npad = rup(h->id_total, 128); d.Kpad = rup(h->c_id, 32);
+    d.y = idgb; d.ldy = h->id_total;
+    d.shift = (const float*)c.W("gen.id.shift");
+    run_conv(c, d, 7, -1, 2.0 * B * h->id_total * h->c_id);
+  }
+  // m1 = up1(z_id): ConvT k2 on a 1x1 input == GEMM to [B, 2, 2, 1024] (AEI_Net.py:101,123)
+  void* m = c.alloc((size_t)B * 4 * 1024 * es);
+  {
+    ConvDesc d;
+    d.ti = GHOST_F32; d.to = h->dt;
+    d.x = zid32; d.B = B; d.Hi = 1; d.Wi = 1; d.Cin = h->c_id; d.ldx = h->c_id;
+    d.w = c.W("gen.up1.w");
+    d.N = 4096; d.Npad = 4096; d.Kpad = rup(h->c_id, 32);
+    d.y = m; d.ldy = 4096;
+    d.shift = (const float*)c.W("gen.up1.shift");
+    run_conv(c, d, 7, -1, 2.0 * B * 4096 * h->c_id);
+  }
+  int id_off = 0;
+  for (int k = 1; k <= 8; ++k) {
+    const int cin = h->gen()[k - 1][0], cout = h->gen()[k - 1][1];
+    int Ca, n;
+    h->attr_geom(k, Ca, n);
+    const void* za = attr[k - 1];
+    const std::string blk = "gen.blk" + std::to_string(k);
+    const size_t P = (size_t)B * n * n;
+    float* stat_m = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
+    run_stats(c, m, cin, B, n * n, cin, stat_m);
+    const void* x = m;
+    const float* stat_x = stat_m;
+    const bool last_k = k == 8;
+    void* y = last_k ? y_out : c.alloc(P * cout * es);
+    const int ldy = cout;
+    for (int i = 0; i < nb; ++i) {
+      const bool last = i == nb - 1;
+      const std::string an = blk + ".aad" + std::to_string(i);
+      const std::string cn = blk + ".conv" + std::to_string(i);
+      if (!last) {
+        void* a = c.alloc(P * cin * es);
+        aad(c, an, x, cin, stat_x, za, Ca, Ca, B, n, cin, id_off, idgb, a, cin);
+        id_off += 2 * cin;
+        void* xn = c.alloc(P * cin * es);
+        conv3x3(c, cn, a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr);
+        float* st = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
+        run_stats(c, xn, cin, B, n * n, cin, st);
+        x = xn;
+        stat_x = st;
+      } else if (cin == cout) {
+        void* a = c.alloc(P * cin * es);
+        aad(c, an, x, cin, stat_x, za, Ca, Ca, B, n, cin, id_off, idgb, a, cin);
+        id_off += 2 * cin;
+        conv3x3(c, cn, a, cin, cin, B, n, cout, y, ldy, m, cin, last_k, last_k ? u8 : nullptr);
+      } else {
+        // x-branch and h'-branch share the output: conv(cat(a_x, a_h), [W_x | W_h]) = x + h'
+        void* cat = c.alloc(P * 2 * cin * es);
+        aad(c, an, x, cin, stat_x, za, Ca, Ca, B, n, cin, id_off, idgb, cat, 2 * cin);
+        id_off += 2 * cin;
+        aad(c, blk + ".aadlast", m, cin, stat_m, za, Ca, Ca, B, n, cin, id_off, idgb,
+            (char*)cat + (size_t)cin * es, 2 * cin);
+        conv3x3(c, cn, cat, 2 * cin, 2 * cin, B, n, cout, y, ldy, nullptr, 0, last_k, last_k ? u8 : nullptr);
+      }
+    }
+    if (cin != cout) id_off += 2 * cin;  // last_add_block's AADLayer
+    if (!last_k) {
+      void* mn = c.alloc((size_t)B * 4 * n * n * cout * es);
+      run_up(c, y, ldy, mn, cout, B, n, n, cout);
+      m = mn;
+    }
+  }
+}
+
+int check_handle(ghost_aei* h) {
+  if (!h) return fail(GHOST_EINVAL, "null handle");
+  for (auto& kv : h->slots)
+    if (!kv.second) return fail(GHOST_ENOTREADY, "unbound weight slot " + kv.first);
+  return 0;
+}
+
+void declare_slots(ghost_aei* h) {
+  auto add = [&](const std::string& s) { h->slots[s] = nullptr; };
+  for (int i = 1; i <= 7; ++i) {
+    add("enc.conv" + std::to_string(i) + ".w");
+    add("enc.conv" + std::to_string(i) + ".scale");
+    add("enc.conv" + std::to_string(i) + ".shift");
+  }
+  for (int i = 1; i <= 6; ++i) {
+    add("enc.deconv" + std::to_string(i) + ".w");
+    add("enc.deconv" + std::to_string(i) + ".scale");
+    add("enc.deconv" + std::to_string(i) + ".shift");
+  }
+  add("gen.up1.w"); add("gen.up1.shift"); add("gen.id.w"); add("gen.id.shift");
+  h->id_total = 0;
+  for (int k = 1; k <= 8; ++k) {
+    const int cin = h->gen()[k - 1][0], cout = h->gen()[k - 1][1];
+    const std::string blk = "gen.blk" + std::to_string(k);
+    for (int i = 0; i < h->nb; ++i) {
+      const std::string an = blk + ".aad" + std::to_string(i);
+      add(an + ".gbw"); add(an + ".gbb"); add(an + ".wh"); add(an + ".bh");
+      add(blk + ".conv" + std::to_string(i) + ".w");
+      h->id_total += 2 * cin;
+    }
+    if (cin != cout) {
+      const std::string an = blk + ".aadlast";
+      add(an + ".gbw"); add(an + ".gbb"); add(an + ".wh"); add(an + ".bh");
+      h->id_total += 2 * cin;
+    }
+  }
+}
+
+// shared driver for forward / get_attr / swap
+enum Mode { M_FORWARD, M_ATTR, M_SWAP };
+
+struct Io {
+  const void* xt = nullptr; int xt_dtype = 0; int64_t st[4] = {0, 0, 0, 0};
+  const uint8_t* crops = nullptr; int64_t crop_bs = 0;
+  const void* zid = nullptr; int zid_dtype = 0; int64_t zid_rs = 0;
+  void* y = nullptr; uint8_t* u8 = nullptr;
+  void* attr[8] = {nullptr};
+};
+
+void plan(Ctx& c, Mode mode, int B, Io io) {
+  ghost_aei* h = c.h;
+  const int es = h->esz;
+  void* attr[8];
+  for (int k = 1; k <= 8; ++k) {
+    int C, H;
+    h->attr_geom(k, C, H);
+    attr[k - 1] = (mode == M_SWAP) ? c.alloc((size_t)B * H * H * C * es) : io.attr[k - 1];
+  }
+  void* xin = c.alloc((size_t)B * 256 * 256 * 3 * es);
+  if (!c.dry && c.ok()) {
+    if (mode == M_SWAP)
+      c.check(crops_u8_to_input(io.crops, io.crop_bs, B, 256, 256, h->dt, xin, c.s), "crops_u8_to_input");
+    else
+      c.check(input_to_nhwc(io.xt_dtype, io.xt, io.st, B, 3, 256, 256, h->dt, xin, c.s), "input_to_nhwc");
+  }
+  encoder(c, xin, B, attr);
+  if (mode == M_ATTR) return;
+  float* zid32 = (float*)c.alloc((size_t)B * h->c_id * sizeof(float));
+  if (!c.dry && c.ok()) c.check(rows_to_f32(io.zid_dtype, io.zid, io.zid_rs, B, h->c_id, zid32, c.s), "rows_to_f32");
+  void* y = (mode == M_SWAP) ? c.alloc((size_t)B * 256 * 256 * 3 * es) : io.y;
+  generator(c, B, attr, zid32, y, io.u8);
+}
+
+int64_t plan_bytes(ghost_aei* h, Mode mode, int B) {
+  Ctx c{};
+  c.h = h; c.dry = true;
+  Io io;
+  uintptr_t fake = 0x20000000;
+  for (int k = 0; k < 8; ++k) io.attr[k] = (void*)(fake + k * 0x100000);
+  io.y = (void*)(fake + 0x1000000);
+  plan(c, mode, B, io);
+  if (!c.ok()) return (int64_t)c.rc;
+  return (int64_t)(((c.off + 255) & ~size_t(255)) + c.scratch_need + 256);
+}
+
+int run(ghost_aei* h, Mode mode, int B, const Io& io, void* ws, int64_t ws_bytes, void* stream) {
+  if (int rc = check_handle(h)) return rc;
+  if (B <= 0) return fail(GHOST_EINVAL, "batch must be positive");
+  Ctx dry{};
+  dry.h = h; dry.dry = true;
+  plan(dry, mode, B, io);
+  if (!dry.ok()) return fail(dry.rc, dry.where);
+  const size_t main_bytes = (dry.off + 255) & ~size_t(255);
+  const size_t need = main_bytes + dry.scratch_need + 256;
+  if (!ws || (size_t)ws_bytes < need)
+    return fail(GHOST_ENOWS, "workspace too small: need " + std::to_string(need) + " bytes");
+  Ctx c{};
+  c.h = h; c.dry = false;
+  c.base = (char*)(((uintptr_t)ws + 255) & ~uintptr_t(255));
+  c.cap = main_bytes;
+  c.scratch = c.base + main_bytes;
+  c.scratch_cap = dry.scratch_need;
+  c.s = (hipStream_t)stream;
+  plan(c, mode, B, io);
+  if (!c.ok()) return fail(c.rc, "forward failed at " + c.where + ": " + (c.rc > 0 ? hipGetErrorString((hipError_t)c.rc) : ""));
+  return 0;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI: handle
+// ---------------------------------------------------------------------------
+extern "C" int ghost_aei_create(const char* backbone, int num_blocks, int c_id, int dtype, ghost_aei** out) {
+  if (!out || !backbone) return fail(GHOST_EINVAL, "null argument");
+  std::string bb(backbone);
+  if (bb != "unet" && bb != "linknet") return fail(GHOST_EINVAL, "backbone must be 'unet' or 'linknet' (got " + bb + ")");
+  if (num_blocks < 1 || num_blocks > 8) return fail(GHOST_EINVAL, "num_blocks out of range");
+  if (c_id <= 0 || c_id % 32) return fail(GHOST_EINVAL, "c_id must be a positive multiple of 32");
+  if (dtype != GHOST_F32 && dtype != GHOST_BF16) return fail(GHOST_EINVAL, "dtype must be f32 or bf16");
+  ghost_aei* h = new ghost_aei();
+  h->linknet = bb == "linknet";
+  h->nb = num_blocks;
+  h->c_id = c_id;
+  h->dt = dtype;
+  h->esz = dtype == GHOST_F32 ? 4 : 2;
+  declare_slots(h);
+  *out = h;
+  return 0;
+}
+
+extern "C" void ghost_aei_destroy(ghost_aei* h) {
+  if (!h) return;
+  for (auto e : h->ev) (void)hipEventDestroy(e);
+  delete h;
+}
+
+extern "C" int ghost_aei_bind(ghost_aei* h, const char* name, const void* p, int64_t numel) {
+  if (!h || !name) return fail(GHOST_EINVAL, "null argument");
+  auto it = h->slots.find(name);
+  if (it == h->slots.end()) return fail(GHOST_EINVAL, std::string("unknown weight slot ") + name);
+  if (!p || numel <= 0) return fail(GHOST_EINVAL, std::string("null/empty tensor for slot ") + name);
+  if ((uintptr_t)p % 16) return fail(GHOST_EINVAL, std::string("slot not 16-byte aligned: ") + name);
+  it->second = p;
+  return 0;
+}
+
+extern "C" int ghost_aei_missing(ghost_aei* h) {
+  if (!h) return fail(GHOST_EINVAL, "null handle");
+  int n = 0;
+  std::string first;
+  for (auto& kv : h->slots)
+    if (!kv.second) {
+      if (!n) first = kv.first;
+      ++n;
+    }
+  if (n) g_err = "unbound weight slot " + first;
+  return n;
+}
+
+extern "C" int ghost_aei_attr_geometry(ghost_aei* h, int level, int* C, int* H, int* W) {
+  if (!h || level < 1 || level > 8 || !C || !H || !W) return fail(GHOST_EINVAL, "bad argument");
+  int c, hh;
+  h->attr_geom(level, c, hh);
+  *C = c; *H = hh; *W = hh;
+  return 0;
+}
+
+extern "C" int64_t ghost_aei_workspace_bytes(ghost_aei* h, int B) {
+  if (!h || B <= 0) return fail(GHOST_EINVAL, "bad argument");
+  return plan_bytes(h, M_FORWARD, B);
+}
+
+extern "C" int64_t ghost_aei_swap_workspace_bytes(ghost_aei* h, int B) {
+  if (!h || B <= 0) return fail(GHOST_EINVAL, "bad argument");
+  return plan_bytes(h, M_SWAP, B);
+}
+
+extern "C" int ghost_aei_forward(ghost_aei* h, const void* xt, int xt_dtype, const int64_t xt_strides[4], int B,
+                                 const void* z_id, int zid_dtype, int64_t zid_row_stride, void* y_nhwc,
+                                 uint8_t* y_u8_bgr, void* const attr_nhwc[8], void* ws, int64_t ws_bytes,
+                                 void* stream) {
+  if (!xt || !xt_strides || !z_id || !y_nhwc || !attr_nhwc) return fail(GHOST_EINVAL, "null argument");
+  Io io;
+  io.xt = xt; io.xt_dtype = xt_dtype;
+  for (int i = 0; i < 4; ++i) io.st[i] = xt_strides[i];
+  io.zid = z_id; io.zid_dtype = zid_dtype; io.zid_rs = zid_row_stride;
+  io.y = y_nhwc; io.u8 = y_u8_bgr;
+  for (int k = 0; k < 8; ++k) {
+    if (!attr_nhwc[k]) return fail(GHOST_EINVAL, "attr buffer missing");
+    io.attr[k] = attr_nhwc[k];
+  }
+  return run(h, M_FORWARD, B, io, ws, ws_bytes, stream);
+}
+
+extern "C" int ghost_aei_get_attr(ghost_aei* h, const void* xt, int xt_dtype, const int64_t xt_strides[4], int B,
+                                  void* const attr_nhwc[8], void* ws, int64_t ws_bytes, void* stream) {
+  if (!xt || !xt_strides || !attr_nhwc) return fail(GHOST_EINVAL, "null argument");
+  Io io;
+  io.xt = xt; io.xt_dtype = xt_dtype;
+  for (int i = 0; i < 4; ++i) io.st[i] = xt_strides[i];
+  for (int k = 0; k < 8; ++k) {
+    if (!attr_nhwc[k]) return fail(GHOST_EINVAL, "attr buffer missing");
+    io.attr[k] = attr_nhwc[k];
+  }
+  return run(h, M_ATTR, B, io, ws, ws_bytes, stream);
+}
+
+extern "C" int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_stride, int B,
+                                 const void* z_id, int zid_dtype, int64_t zid_row_stride, uint8_t* out_u8, void* ws,
+                                 int64_t ws_bytes, void* stream) {
+  if (!crops || !z_id || !out_u8) return fail(GHOST_EINVAL, "null argument");
+  Io io;
+  io.crops = crops; io.crop_bs = crop_batch_stride;
+  io.zid = z_id; io.zid_dtype = zid_dtype; io.zid_rs = zid_row_stride;
+  io.u8 = out_u8;
+  return run(h, M_SWAP, B, io, ws, ws_bytes, stream);
+}
+
+extern "C" int ghost_aei_profile(ghost_aei* h, int class_mask) {
+  if (!h) return fail(GHOST_EINVAL, "null handle");
+  h->prof_mask = class_mask;
+  h->pend.clear();
+  h->ev_used = 0;
+  for (auto& p : h->prof) p = ProfClass{};
+  return 0;
+}
+
+extern "C" int ghost_aei_profile_read(ghost_aei* h, int cls, double* ms, int64_t* launches, double* bytes,
+                                      double* flops) {
+  if (!h || cls < 0 || cls >= 8) return fail(GHOST_EINVAL, "bad argument");
+  // fold completed brackets into the class totals (caller synchronised the stream)
+  for (auto& p : h->pend) {
+    float t = 0.f;
+    hipError_t e = hipEventElapsedTime(&t, h->ev[p.e0], h->ev[p.e1]);
+    if (e != hipSuccess) return fail((int)e, "hipEventElapsedTime failed (stream not synchronised?)");
+    ProfClass& pc = h->prof[p.cls];
+    pc.ms += t;
+    pc.launches += 1;
+    pc.bytes += p.bytes;
+    pc.flops += p.flops;
+  }
+  h->pend.clear();
+  h->ev_used = 0;
+  if (ms) *ms = h->prof[cls].ms;
+  if (launches) *launches = h->prof[cls].launches;
+  if (bytes) *bytes = h->prof[cls].bytes;
+  if (flops) *flops = h->prof[cls].flops;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI: single operators
+// ---------------------------------------------------------------------------
+static int g_force_split = 0;
+extern "C" int ghost_set_split_k(int n) {
+  if (n < 0) return fail(GHOST_EINVAL, "split must be >= 0");
+  g_force_split = n;
+  return 0;
+}
+
+static int conv_op(ConvDesc& d, void* ws, int64_t ws_bytes, void* stream, const char* what) {
+  d.force_split = g_force_split;
+  const size_t need = conv_workspace_bytes(d);
+  if (need > 0 && (!ws || (size_t)ws_bytes < need))
+    return fail(GHOST_ENOWS, std::string(what) + ": workspace too small, need " + std::to_string(need));
+  int rc = conv_launch(d, ws, (size_t)ws_bytes, (hipStream_t)stream);
+  if (rc) return fail(rc, std::string(what) + " failed");
+  return 0;
+}
+
+extern "C" int ghost_conv2d_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx, const void* w_packed,
+                                 int Cout, int Npad, int Kpad, int kh, int kw, int stride, int pad, const float* scale,
+                                 const float* shift, float slope, const void* res, int ldres, int tanh_out, void* y,
+                                 int ldy, void* ws, int64_t ws_bytes, void* stream) {
+  ConvDesc d;
+  d.ti = d.to = dtype;
+  d.x = x; d.B = B; d.Hi = H; d.Wi = W; d.Cin = Cin; d.ldx = ldx;
+  d.w = w_packed; d.N = Cout; d.Npad = Npad; d.Kpad = Kpad;
+  d.kind = CONV_FWD; d.kh = kh; d.kw = kw; d.stride = stride; d.pad = pad;
+  d.scale = scale; d.shift = shift; d.slope = slope; d.res = res; d.ldres = ldres; d.tanh_out = tanh_out;
+  d.y = y; d.ldy = ldy;
+  return conv_op(d, ws, ws_bytes, stream, "ghost_conv2d_nhwc");
+}
+
+extern "C" int ghost_conv_transpose4x4s2_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx,
+                                              const void* w_packed, int Cout, int Npad, int Kpad, const float* scale,
+                                              const float* shift, float slope, const void* res, int ldres, void* y,
+                                              int ldy, void* ws, int64_t ws_bytes, void* stream) {
+  ConvDesc d;
+  d.ti = d.to = dtype;
+  d.x = x; d.B = B; d.Hi = H; d.Wi = W; d.Cin = Cin; d.ldx = ldx;
+  d.w = w_packed; d.N = Cout; d.Npad = Npad; d.Kpad = Kpad;
+  d.kind = CONV_T4S2;
+  d.scale = scale; d.shift = shift; d.slope = slope; d.res = res; d.ldres = ldres;
+  d.y = y; d.ldy = ldy;
+  return conv_op(d, ws, ws_bytes, stream, "ghost_conv_transpose4x4s2_nhwc");
+}
+
+extern "C" int ghost_linear_f32(const float* x, int B, int K, const float* w_packed, int N, int Npad, int Kpad,
+                                const float* bias, int out_dtype, void* y, int ldy, void* ws, int64_t ws_bytes,
+                                void* stream) {
+  ConvDesc d;
+  d.ti = GHOST_F32; d.to = out_dtype;
+  d.x = x; d.B = B; d.Hi = 1; d.Wi = 1; d.Cin = K; d.ldx = K;
+  d.w = w_packed; d.N = N; d.Npad = Npad; d.Kpad = Kpad;
+  d.shift = bias; d.y = y; d.ldy = ldy;
+  return conv_op(d, ws, ws_bytes, stream, "ghost_linear_f32");
+}
+
+extern "C" int ghost_instnorm_stats_nhwc(int dtype, const void* x, int B, int HW, int C, int ldx, float* stat, void* ws,
+                                         int64_t ws_bytes, void* stream) {
+  if ((size_t)ws_bytes < in_stats_workspace_bytes(B, HW, C)) return fail(GHOST_ENOWS, "in_stats: workspace too small");
+  int rc = in_stats(dtype, x, ldx, B, HW, C, stat, ws, (size_t)ws_bytes, (hipStream_t)stream);
+  return rc ? fail(rc, "in_stats failed") : 0;
+}
+
+extern "C" int ghost_aad_layer_nhwc(int dtype, const void* h_in, int ldh, const void* z_attr, int lda, int B, int H,
+                                    int W, int C, int Ca, const void* gbw_packed, int Npad, int Kpad, const float* gbb,
+                                    const float* wh, const float* bh, const float* idgb, int id_ld, float slope,
+                                    void* out, int ldo, void* ws, int64_t ws_bytes, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int HW = H * W;
+  // workspace: stat [B][C][2] | mask [B*HW] | scratch (max of IN partials and split-K partials)
+  const size_t stat_b = ((size_t)B * C * 2 * sizeof(float) + 255) & ~size_t(255);
+  const size_t mask_b = ((size_t)B * HW * sizeof(float) + 255) & ~size_t(255);
+  ConvDesc d;
+  d.ti = d.to = dtype;
+  d.x = z_attr; d.B = B; d.Hi = H; d.Wi = W; d.Cin = Ca; d.ldx = lda;
+  d.w = gbw_packed; d.N = 2 * C; d.Npad = Npad; d.Kpad = Kpad;
+  d.kind = CONV_FWD; d.kh = d.kw = 1;
+  d.y = out; d.ldy = ldo; d.shift = gbb; d.slope = slope; d.epi = EPI_AAD;
+  d.hin = h_in; d.ldh = ldh; d.idgb = idgb; d.id_ld = id_ld; d.C_aad = C;
+  size_t sc = conv_workspace_bytes(d);
+  const size_t st = in_stats_workspace_bytes(B, HW, C);
+  if (st > sc) sc = st;
+  char* base = (char*)(((uintptr_t)ws + 255) & ~uintptr_t(255));
+  if (!ws || (size_t)ws_bytes < stat_b + mask_b + sc + 256) return fail(GHOST_ENOWS, "aad_layer: workspace too small");
+  float* stat = (float*)base;
+  float* mask = (float*)(base + stat_b);
+  char* scratch = base + stat_b + mask_b;
+  int rc = in_stats(dtype, h_in, ldh, B, HW, C, stat, scratch, sc, s);
+  if (rc) return fail(rc, "aad_layer: in_stats failed");
+  rc = aad_mask(dtype, h_in, ldh, B, HW, C, stat, wh, bh, mask, s);
+  if (rc) return fail(rc, "aad_layer: mask failed");
+  d.stat = stat; d.mask = mask;
+  rc = conv_launch(d, scratch, sc, s);
+  if (rc) return fail(rc, "aad_layer: gemm failed");
+  return 0;
+}
+
+extern "C" int ghost_upsample2x_nhwc(int dtype, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C,
+                                     void* stream) {
+  int rc = upsample2x(dtype, x, ldx, y, ldy, B, H, W, C, (hipStream_t)stream);
+  return rc ? fail(rc, "upsample2x failed") : 0;
+}
+
+extern "C" int ghost_nhwc_to_nchw(int dtype, const void* x, int ldx, int B, int H, int W, int C, void* y, void* stream) {
+  int rc = nhwc_to_nchw(dtype, x, ldx, B, H, W, C, y, (hipStream_t)stream);
+  return rc ? fail(rc, "nhwc_to_nchw failed") : 0;
+}
+
+extern "C" int ghost_crops_to_input_nhwc(const uint8_t* crops, int64_t crop_batch_stride, int B, int H, int W, int dtype,
+                                         void* y, void* stream) {
+  int rc = crops_u8_to_input(crops, crop_batch_stride, B, H, W, dtype, y, (hipStream_t)stream);
+  return rc ? fail(rc, "crops_to_input failed") : 0;
+}

@@ -1,0 +1,469 @@
+// ghost_amd — implicit-GEMM convolution on CDNA4 matrix cores (gfx950).
+//
+// Tile: BM output pixels x BN output channels x BK=32 reduction, 256 threads = 4 waves
+// in a 2x2 arrangement, each wave owning (BM/2)x(BN/2) as 16x16 MFMA tiles.
+//   bf16: v_mfma_f32_16x16x32_bf16  (one instruction per 16x16x32 step)
+//   fp32: v_mfma_f32_16x16x4_f32    (exact fp32 products, fp32 accumulate — the 1e-3 parity path)
+// The A tile (pixels x (tap,cin)) is gathered from NHWC activations with zero padding
+// at the borders; when Cin % 32 == 0 a 32-deep K slice lies inside one tap, so every
+// row is one contiguous 64 B (bf16) / 128 B (fp32) run loaded as 16 B vectors.
+// Staging: global -> registers -> LDS, double-buffered, one barrier per K step.
+#include "conv_igemm.h"
+#include "ghost_common.h"
+
+namespace ghost {
+
+struct ConvArgs {
+  const void* x;
+  const void* w;
+  void* y;
+  const float* scale;
+  const float* shift;
+  const void* res;
+  const void* hin;
+  const float* stat;
+  const float* idgb;
+  const float* mask;
+  float* partial;
+  uint8_t* u8;
+  long wpar_stride;
+  int B, Hi, Wi, Cin, ldx;
+  int Ho, Wo, M;        // GEMM pixel grid (the sub-pixel grid for CONV_T4S2)
+  int N, Kpad, K, NT;   // NT = padded channel extent covered by tiles
+  int nNt;              // number of channel tiles
+  int ldy, ldres, ldh, id_ld, C_aad;
+  int stride, ntx, tbase, tsign;   // input coord = out*stride + tbase + tsign*tap  (per dim)
+  int deconv;           // 1: four parity phases in blockIdx.z, output pixel (2qy+py, 2qx+px)
+  int nsplit, kt_per_split;
+  float slope;
+  int tanh_out;
+};
+
+// ---------------------------------------------------------------------------
+// epilogues (shared by the GEMM kernel and the split-K reduction)
+// ---------------------------------------------------------------------------
+template <typename TO>
+GHOST_DEV float epi_std(const ConvArgs& a, float v, int n, long opix) {
+  if (a.scale) v *= a.scale[n];
+  if (a.shift) v += a.shift[n];
+  v = v > 0.f ? v : v * a.slope;
+  if (a.res) v += to_f(reinterpret_cast<const TO*>(a.res)[opix * a.ldres + n]);
+  if (a.tanh_out) v = tanhf(v);
+  return v;
+}
+
+template <typename TO>
+GHOST_DEV void store_std(const ConvArgs& a, float v, int n, long opix) {
+  reinterpret_cast<TO*>(a.y)[opix * a.ldy + n] = from_f<TO>(v);
+  if (a.u8) {
+    // ((Y*0.5+0.5)*255)[..., [2,1,0]].type(uint8)   (faceshifter_run.py:20-21)
+    float t = (v * 0.5f + 0.5f) * 255.0f;
+    a.u8[opix * 3 + (2 - n)] = (uint8_t)(int)t;
+  }
+}
+
+// AADLayer.forward (AADLayer.py:20-38) for one (pixel m, channel c), followed by the
+// ReLU of AddBlocksSequential when slope == 0:
+//   h = (h_in - mu) * rstd;  A = ga*h + ba;  I = gi*h + bi;  out = (1-M)*A + M*I
+template <typename TO>
+GHOST_DEV float epi_aad(const ConvArgs& a, float ga, float ba, int c, long m) {
+  const int HW = a.Ho * a.Wo;
+  const int b = (int)(m / HW);
+  const float hin = to_f(reinterpret_cast<const TO*>(a.hin)[m * a.ldh + c]);
+  const float mu = a.stat[((long)b * a.C_aad + c) * 2 + 0];
+  const float rs = a.stat[((long)b * a.C_aad + c) * 2 + 1];
+  const float h = (hin - mu) * rs;
+  const float gi = a.idgb[(long)b * a.id_ld + c];
+  const float bi = a.idgb[(long)b * a.id_ld + a.C_aad + c];
+  const float Mk = a.mask[m];
+  const float A = ga * h + ba;
+  const float I = gi * h + bi;
+  float out = (1.0f - Mk) * A + Mk * I;
+  return out > 0.f ? out : out * a.slope;
+}
+
+GHOST_DEV long out_pixel(const ConvArgs& a, long m, int py, int px) {
+  if (!a.deconv) return m;
+  const int HW = a.Ho * a.Wo;
+  const int b = (int)(m / HW);
+  const int r = (int)(m - (long)b * HW);
+  const int qy = r / a.Wo, qx = r - qy * a.Wo;
+  return ((long)b * (2 * a.Ho) + 2 * qy + py) * (2 * a.Wo) + 2 * qx + px;
+}
+
+// ---------------------------------------------------------------------------
+// the GEMM kernel
+// ---------------------------------------------------------------------------
+enum { KEPI_STD = 0, KEPI_AAD = 1, KEPI_SPLIT = 2 };
+
+template <typename TI, typename TO, int BM, int BN, int EPI, bool FAST>
+__global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
+  constexpr int BK = 32;
+  constexpr int VEC = Vec16<TI>::N;
+  constexpr int CPR = BK / VEC;   // 16 B chunks per tile row
+  constexpr int RPP = 256 / CPR;  // tile rows covered per load pass
+  constexpr int AP = BM / RPP;
+  constexpr int BP = (BN + RPP - 1) / RPP;   // BN may be smaller than one pass
+  constexpr int LDR = BK + VEC;   // padded LDS row, elements
+  constexpr int TM = BM / 32, TN = BN / 32;
+  static_assert(BM % RPP == 0 && (BN % RPP == 0 || RPP % BN == 0), "tile/load mismatch");
+  static_assert(EPI != KEPI_AAD || (TN % 2 == 0), "AAD epilogue needs gamma/beta tile pairs");
+
+  __shared__ __attribute__((aligned(16))) TI smem[2 * (BM + BN) * LDR];
+
+  const int tid = threadIdx.x;
+  const int nt = blockIdx.x % a.nNt;
+  const int mt = blockIdx.x / a.nNt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int split = blockIdx.y;
+  const int par = blockIdx.z;
+  const int py = par >> 1, px = par & 1;
+  const TI* __restrict__ x = reinterpret_cast<const TI*>(a.x);
+  const TI* __restrict__ w = reinterpret_cast<const TI*>(a.w) + par * a.wpar_stride;
+
+  const int nk = a.Kpad / BK;
+  const int kt0 = split * a.kt_per_split;
+  const int kt1 = min(nk, kt0 + a.kt_per_split);
+
+  // per-thread rows of the A tile
+  const int crow = tid / CPR, cch = tid % CPR;
+  const int HoWo = a.Ho * a.Wo;
+  int a_base[AP], a_iy[AP], a_ix[AP];
+  bool a_ok[AP];
+#pragma unroll
+  for (int p = 0; p < AP; ++p) {
+    const int m = m0 + crow + p * RPP;
+    a_ok[p] = m < a.M;
+    const int mm = a_ok[p] ? m : 0;
+    const int b = mm / HoWo;
+    const int r = mm - b * HoWo;
+    const int oy = r / a.Wo, ox = r - oy * a.Wo;
+    a_base[p] = b * a.Hi * a.Wi;
+    a_iy[p] = oy * a.stride;
+    a_ix[p] = ox * a.stride;
+  }
+  const int tby = a.deconv ? py : a.tbase;
+  const int tbx = a.deconv ? px : a.tbase;
+
+  u32x4 ra[AP], rb[BP];
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+    if constexpr (FAST) {
+      const int tap = k0 / a.Cin;
+      const int c = k0 - tap * a.Cin + cch * VEC;
+      const int ty = tap / a.ntx, tx = tap - ty * a.ntx;
+      const int dy = tby + a.tsign * ty, dx = tbx + a.tsign * tx;
+#pragma unroll
+      for (int p = 0; p < AP; ++p) {
+        const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;
+        const bool ok = a_ok[p] && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+        if (ok)
+          ra[p] = *reinterpret_cast<const u32x4*>(x + (long)(a_base[p] + iy * a.Wi + ix) * a.ldx + c);
+        else
+          ra[p] = u32x4{0u, 0u, 0u, 0u};
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < AP; ++p) {
+        TI* e = reinterpret_cast<TI*>(&ra[p]);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const int k = k0 + cch * VEC + j;
+          float v = 0.f;
+          if (a_ok[p] && k < a.K) {
+            const int tap = k / a.Cin;
+            const int c = k - tap * a.Cin;
+            const int ty = tap / a.ntx, tx = tap - ty * a.ntx;
+            const int iy = a_iy[p] + tby + a.tsign * ty, ix = a_ix[p] + tbx + a.tsign * tx;
+            if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi)
+              v = to_f(x[(long)(a_base[p] + iy * a.Wi + ix) * a.ldx + c]);
+          }
+          e[j] = from_f<TI>(v);
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < BP; ++p) {
+      // BN < RPP: the surplus threads re-load an in-tile row and do not store it
+      const int n = n0 + (BN >= RPP ? crow + p * RPP : crow % BN);
+      rb[p] = *reinterpret_cast<const u32x4*>(w + (long)n * a.Kpad + k0 + cch * VEC);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    TI* As = smem + buf * (BM + BN) * LDR;
+    TI* Bs = As + BM * LDR;
+#pragma unroll
+    for (int p = 0; p < AP; ++p) *reinterpret_cast<u32x4*>(As + (crow + p * RPP) * LDR + cch * VEC) = ra[p];
+#pragma unroll
+    for (int p = 0; p < BP; ++p)
+      if (BN >= RPP || crow < BN) *reinterpret_cast<u32x4*>(Bs + (crow + p * RPP) * LDR + cch * VEC) = rb[p];
+  };
+
+  const int wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const TI* As = smem + buf * (BM + BN) * LDR;
+    const TI* Bs = As + BM * LDR;
+    const TI* Ab = As + (wm * (BM / 2) + lr) * LDR;
+    const TI* Bb = Bs + (wn * (BN / 2) + lr) * LDR;
+    if constexpr (sizeof(TI) == 2) {
+      bf16x8 af[TM], bfv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * LDR + lq * 8);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * LDR + lq * 8);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 af[TM], bfv[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f32x4*>(Ab + i * 16 * LDR + h * 16 + lq * 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const f32x4*>(Bb + j * 16 * LDR + h * 16 + lq * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bfv[j][e], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // one load site and one store site keep the staging registers out of scratch
+  int cur = 0;
+  if (kt0 < kt1) load_tile(kt0);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    store_tile(cur);
+    __syncthreads();   // LDS[cur] visible; every wave is past compute(kt-2) on this buffer
+    if (kt + 1 < kt1) load_tile(kt + 1);
+    compute(cur);
+    cur ^= 1;
+  }
+
+  // ---- epilogue ----
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * (BM / 2) + i * 16 + lq * 4 + r;
+      if (m >= a.M) continue;
+      if constexpr (EPI == KEPI_SPLIT) {
+        float* dst = a.partial + (((long)par * a.nsplit + split) * a.M + m) * a.NT;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) dst[n0 + wn * (BN / 2) + j * 16 + lr] = acc[i][j][r];
+      } else if constexpr (EPI == KEPI_STD) {
+        const long op = out_pixel(a, m, py, px);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * (BN / 2) + j * 16 + lr;
+          if (n < a.N) store_std<TO>(a, epi_std<TO>(a, acc[i][j][r], n, op), n, op);
+        }
+      } else {  // AAD: column tiles (2jp, 2jp+1) = (gamma, beta) of the same 16 channels
+#pragma unroll
+        for (int jp = 0; jp < TN / 2; ++jp) {
+          const int ng = n0 + wn * (BN / 2) + (2 * jp) * 16 + lr;
+          const int c = (ng >> 5) * 16 + lr;
+          if (c < a.C_aad) {
+            const float ga = acc[i][2 * jp][r] + a.shift[ng];
+            const float ba = acc[i][2 * jp + 1][r] + a.shift[ng + 16];
+            const float v = epi_aad<TO>(a, ga, ba, c, m);
+            reinterpret_cast<TO*>(a.y)[(long)m * a.ldy + c] = from_f<TO>(v);
+          }
+        }
+      }
+    }
+  }
+}
+
+// split-K reduction + epilogue: one thread per (pixel, channel) [STD] or (pixel, AAD channel)
+template <typename TO, int EPI>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a) {
+  const int par = blockIdx.z;
+  const int py = par >> 1, px = par & 1;
+  const int ncols = (EPI == KEPI_AAD) ? a.C_aad : a.N;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)a.M * ncols) return;
+  const long m = idx / ncols;
+  const int c = (int)(idx - m * ncols);
+  const float* base = a.partial + ((long)par * a.nsplit * a.M + m) * a.NT;
+  const long sstride = (long)a.M * a.NT;
+  if constexpr (EPI == KEPI_STD) {
+    float v = 0.f;
+    for (int s = 0; s < a.nsplit; ++s) v += base[s * sstride + c];
+    const long op = out_pixel(a, m, py, px);
+    store_std<TO>(a, epi_std<TO>(a, v, c, op), c, op);
+  } else {
+    const int ng = (c >> 4) * 32 + (c & 15);
+    float ga = 0.f, ba = 0.f;
+    for (int s = 0; s < a.nsplit; ++s) {
+      ga += base[s * sstride + ng];
+      ba += base[s * sstride + ng + 16];
+    }
+    ga += a.shift[ng];
+    ba += a.shift[ng + 16];
+    reinterpret_cast<TO*>(a.y)[m * a.ldy + c] = from_f<TO>(epi_aad<TO>(a, ga, ba, c, m));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side: tile choice, split-K heuristic, dispatch
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Plan {
+  int BM, BN, nNt, nMt, npar, nsplit, kt_per_split, NT, M, Ho, Wo;
+  bool fast;
+};
+
+Plan make_plan(const ConvDesc& d) {
+  Plan p{};
+  p.npar = d.kind == CONV_T4S2 ? 4 : 1;
+  if (d.kind == CONV_T4S2) {
+    p.Ho = d.Hi;
+    p.Wo = d.Wi;
+  } else {
+    p.Ho = (d.Hi + 2 * d.pad - d.kh) / d.stride + 1;
+    p.Wo = (d.Wi + 2 * d.pad - d.kw) / d.stride + 1;
+  }
+  p.M = d.B * p.Ho * p.Wo;
+  const int vec = d.ti == GHOST_BF16 ? 8 : 4;
+  p.fast = (d.Cin % 32 == 0) && (d.ldx % vec == 0) && ((uintptr_t)d.x % 16 == 0);
+  if (d.epi == EPI_AAD)
+    p.BN = d.N > 64 ? 128 : 64;
+  else
+    p.BN = d.N <= 32 ? 32 : (d.N <= 64 ? 64 : 128);
+  p.nNt = (d.N + p.BN - 1) / p.BN;
+  const int tiles128 = ((p.M + 127) / 128) * p.nNt * p.npar;
+  p.BM = (tiles128 >= 512 || !p.fast) ? 128 : 64;
+  p.nMt = (p.M + p.BM - 1) / p.BM;
+  p.NT = p.nNt * p.BN;
+  const int nk = d.Kpad / 32;
+  const int tiles = p.nMt * p.nNt * p.npar;
+  int s = 1;
+  if (d.force_split > 0) {
+    s = d.force_split;
+  } else if (tiles < 256 && nk >= 16) {
+    s = (512 + tiles - 1) / tiles;          // aim for >= 2 workgroups per CU
+    s = s < nk / 8 ? s : nk / 8;            // keep >= 8 K steps per split
+    if (s < 1) s = 1;
+  }
+  if (s > nk) s = nk;
+  p.kt_per_split = (nk + s - 1) / s;
+  p.nsplit = (nk + p.kt_per_split - 1) / p.kt_per_split;
+  return p;
+}
+
+ConvArgs make_args(const ConvDesc& d, const Plan& p, float* partial) {
+  ConvArgs a{};
+  a.x = d.x; a.w = d.w; a.y = d.y;
+  a.scale = d.scale; a.shift = d.shift; a.res = d.res;
+  a.hin = d.hin; a.stat = d.stat; a.idgb = d.idgb; a.mask = d.mask;
+  a.partial = partial; a.u8 = d.u8;
+  a.wpar_stride = (long)d.Npad * d.Kpad;
+  a.B = d.B; a.Hi = d.Hi; a.Wi = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx;
+  a.Ho = p.Ho; a.Wo = p.Wo; a.M = p.M;
+  a.N = d.N; a.Kpad = d.Kpad; a.NT = p.NT; a.nNt = p.nNt;
+  a.ldy = d.ldy; a.ldres = d.ldres; a.ldh = d.ldh; a.id_ld = d.id_ld; a.C_aad = d.C_aad;
+  if (d.kind == CONV_T4S2) {
+    a.K = 4 * d.Cin; a.stride = 1; a.ntx = 2; a.tbase = 0; a.tsign = -1; a.deconv = 1;
+  } else {
+    a.K = d.kh * d.kw * d.Cin; a.stride = d.stride; a.ntx = d.kw; a.tbase = -d.pad; a.tsign = 1; a.deconv = 0;
+  }
+  a.nsplit = p.nsplit; a.kt_per_split = p.kt_per_split;
+  a.slope = d.slope; a.tanh_out = d.tanh_out;
+  return a;
+}
+
+template <typename TI, typename TO, int BM, int BN, int EPI, bool FAST>
+void launch_gemm(const ConvArgs& a, const Plan& p, hipStream_t s) {
+  dim3 grid(p.nMt * p.nNt, p.nsplit, p.npar);
+  hipLaunchKernelGGL((conv_igemm_kernel<TI, TO, BM, BN, EPI, FAST>), grid, dim3(256), 0, s, a);
+}
+
+template <typename TI, typename TO, int EPI, bool FAST>
+int dispatch_tile(const ConvArgs& a, const Plan& p, hipStream_t s) {
+  if (p.BM == 128 && p.BN == 128) launch_gemm<TI, TO, 128, 128, EPI, FAST>(a, p, s);
+  else if (p.BM == 128 && p.BN == 64) launch_gemm<TI, TO, 128, 64, EPI, FAST>(a, p, s);
+  else if (p.BM == 64 && p.BN == 128) launch_gemm<TI, TO, 64, 128, EPI, FAST>(a, p, s);
+  else if (p.BM == 64 && p.BN == 64) launch_gemm<TI, TO, 64, 64, EPI, FAST>(a, p, s);
+  else {
+    if constexpr (EPI != KEPI_AAD) {
+      if (p.BM == 128 && p.BN == 32) { launch_gemm<TI, TO, 128, 32, EPI, FAST>(a, p, s); return 0; }
+      if (p.BM == 64 && p.BN == 32) { launch_gemm<TI, TO, 64, 32, EPI, FAST>(a, p, s); return 0; }
+    }
+    return -1;
+  }
+  return 0;
+}
+
+template <typename TI, typename TO>
+int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStream_t s) {
+  int rc;
+  if (p.nsplit > 1) {
+    rc = p.fast ? dispatch_tile<TI, TO, KEPI_SPLIT, true>(a, p, s) : dispatch_tile<TI, TO, KEPI_SPLIT, false>(a, p, s);
+    if (rc) return rc;
+    const int ncols = d.epi == EPI_AAD ? d.C_aad : d.N;
+    const long total = (long)p.M * ncols;
+    dim3 grid((unsigned)((total + 255) / 256), 1, p.npar);
+    if (d.epi == EPI_AAD)
+      hipLaunchKernelGGL((splitk_reduce_kernel<TO, KEPI_AAD>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((splitk_reduce_kernel<TO, KEPI_STD>), grid, dim3(256), 0, s, a);
+    return 0;
+  }
+  if (d.epi == EPI_AAD) {
+    if (!p.fast) return -1;
+    return dispatch_tile<TI, TO, KEPI_AAD, true>(a, p, s);
+  }
+  return p.fast ? dispatch_tile<TI, TO, KEPI_STD, true>(a, p, s) : dispatch_tile<TI, TO, KEPI_STD, false>(a, p, s);
+}
+
+}  // namespace
+
+size_t conv_workspace_bytes(const ConvDesc& d) {
+  Plan p = make_plan(d);
+  if (p.nsplit <= 1) return 0;
+  return (size_t)p.npar * p.nsplit * p.M * p.NT * sizeof(float);
+}
+
+int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream) {
+  if (!d.x || !d.w || !d.y || d.B <= 0 || d.Cin <= 0 || d.N <= 0) return -1;
+  if (d.Kpad % 32 != 0 || d.Npad < d.N) return -1;
+  if (d.epi == EPI_AAD && (d.C_aad % 16 != 0 || d.N != 2 * d.C_aad || !d.hin || !d.stat || !d.idgb || !d.mask || !d.shift))
+    return -1;
+  Plan p = make_plan(d);
+  if (p.NT > d.Npad) return -1;  // weight rows read by the last tile must exist
+  const int K = d.kind == CONV_T4S2 ? 4 * d.Cin : d.kh * d.kw * d.Cin;
+  if (d.Kpad < K) return -1;
+  float* partial = nullptr;
+  if (p.nsplit > 1) {
+    size_t need = (size_t)p.npar * p.nsplit * p.M * p.NT * sizeof(float);
+    if (!ws || ws_bytes < need) return -1;
+    partial = reinterpret_cast<float*>(ws);
+  }
+  ConvArgs a = make_args(d, p, partial);
+  int rc;
+  if (d.ti == GHOST_F32 && d.to == GHOST_F32) rc = dispatch_types<float, float>(d, a, p, stream);
+  else if (d.ti == GHOST_BF16 && d.to == GHOST_BF16) rc = dispatch_types<bf16, bf16>(d, a, p, stream);
+  else if (d.ti == GHOST_F32 && d.to == GHOST_BF16) rc = dispatch_types<float, bf16>(d, a, p, stream);
+  else return -1;
+  if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+}  // namespace ghost

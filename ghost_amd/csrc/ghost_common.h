@@ -1,0 +1,57 @@
+// ghost_amd — shared device helpers for the gfx950 (MI355X / CDNA4) kernels.
+//
+// Activations are NHWC ("pixel-major, channel-contiguous") so that
+//   * every conv is an implicit GEMM whose K dimension (tap, channel) is contiguous,
+//   * the AAD mask (a dot product over channels per pixel) is a contiguous reduction,
+//   * 1x1 convs on z_attr are plain row-major GEMMs.
+// A channel stride `ld` (elements between consecutive pixels) lets producers write
+// straight into a channel slice of a wider buffer (the unet skip concat, the fused
+// x/h' concat of AAD_ResBlk) with no copy.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GHOST_DEV __device__ __forceinline__
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+enum GhostDType { GHOST_F32 = 0, GHOST_BF16 = 1, GHOST_F16 = 2, GHOST_U8 = 3 };
+
+GHOST_DEV float to_f(float v) { return v; }
+GHOST_DEV float to_f(bf16 v) { return (float)v; }
+GHOST_DEV float to_f(_Float16 v) { return (float)v; }
+GHOST_DEV float to_f(uint8_t v) { return (float)v; }
+
+template <typename T> GHOST_DEV T from_f(float v);
+template <> GHOST_DEV float from_f<float>(float v) { return v; }
+template <> GHOST_DEV bf16 from_f<bf16>(float v) { return (bf16)v; }
+template <> GHOST_DEV _Float16 from_f<_Float16>(float v) { return (_Float16)v; }
+
+// elements per 16-byte vector
+template <typename T> struct Vec16 { static constexpr int N = 16 / sizeof(T); };
+
+// load / store VEC elements (16 bytes) converting to / from fp32
+template <typename T> GHOST_DEV void load16_f(const T* p, float* out) {
+  u32x4 raw = *reinterpret_cast<const u32x4*>(p);
+  const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+  for (int i = 0; i < Vec16<T>::N; ++i) out[i] = to_f(e[i]);
+}
+template <typename T> GHOST_DEV void store16_f(T* p, const float* in) {
+  u32x4 raw;
+  T* e = reinterpret_cast<T*>(&raw);
+#pragma unroll
+  for (int i = 0; i < Vec16<T>::N; ++i) e[i] = from_f<T>(in[i]);
+  *reinterpret_cast<u32x4*>(p) = raw;
+}
+
+GHOST_DEV float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// shuffle-xor reduction over `width` lanes (width power of two, <= 64)
+GHOST_DEV float group_sum(float v, int width) {
+  for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}

@@ -1,0 +1,40 @@
+// ghost_amd — launchers for the bandwidth-bound kernels around the GEMMs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ghost {
+
+// InstanceNorm2d(affine=False) statistics (AADLayer.py:16,24): per (b, c) mean and
+// 1/sqrt(biased var + eps) over H*W, from shifted partial sums (no Sigma x^2 - n mu^2
+// cancellation) merged in fp64.  stat = [B][C][2].
+size_t in_stats_workspace_bytes(int B, int HW, int C);
+int in_stats(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, void* ws, size_t ws_bytes,
+             hipStream_t s);
+
+// AAD mask: M[p] = sigmoid(sum_c wh[c] * (h[p,c]-mu[b,c])*rstd[b,c] + bh)   (AADLayer.py:35)
+int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh,
+             const float* bh, float* mask, hipStream_t s);
+
+// bilinear x2, align_corners=True, NHWC (AEI_Net.py:94,125-137)
+int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C, hipStream_t s);
+
+// Xt [B,C,H,W] of dtype xdt with arbitrary element strides -> NHWC (ld = C) of dtype dt
+int input_to_nhwc(int xdt, const void* x, const int64_t strides[4], int B, int C, int H, int W, int dt, void* y,
+                  hipStream_t s);
+
+// uint8 BGR NHWC crops -> RGB NHWC in [-1,1]: (v/255 - 0.5)/0.5  (core.py:13-26)
+int crops_u8_to_input(const uint8_t* crops, int64_t batch_stride, int B, int H, int W, int dt, void* y,
+                      hipStream_t s);
+
+// Y NHWC (3 channels, ld) -> uint8 BGR NHWC: ((Y*0.5+0.5)*255)[..., [2,1,0]].uint8  (faceshifter_run.py:20-21)
+int y_to_u8_bgr(int dt, const void* y, int ldy, int B, int H, int W, uint8_t* out, hipStream_t s);
+
+// rows of z_id ([B, c_id] with a row stride, any float dtype) -> fp32 [B, c_id]
+int rows_to_f32(int xdt, const void* x, int64_t row_stride, int B, int n, float* y, hipStream_t s);
+
+// NHWC (ld) -> NCHW contiguous copy in the same dtype (attr export / tests)
+int nhwc_to_nchw(int dt, const void* x, int ldx, int B, int H, int W, int C, void* y, hipStream_t s);
+
+}  // namespace ghost

@@ -1,0 +1,355 @@
+// ghost_amd — bandwidth-bound kernels: InstanceNorm statistics, AAD mask, bilinear x2,
+// and the layout/precision conversions at the AEI_Net boundary.  All NHWC, 16-byte
+// vector accesses along channels, fp32 arithmetic.
+#include "ghost_common.h"
+#include "ops.h"
+
+namespace ghost {
+
+static constexpr float kInEps = 1e-5f;   // nn.InstanceNorm2d default (AADLayer.py:16)
+
+// ---------------------------------------------------------------------------
+// InstanceNorm statistics
+// grid (nchunk, ceil(C/64), B); a block reduces `chunk` pixels x 64 channels.
+// Shift K_c = x[b, pixel 0, c] makes the partial sums robust to |mean| >> std.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256)
+in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chunk, int nchunk, float* __restrict__ part) {
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int TPP = 64 / VEC;   // threads per pixel (64 channels)
+  constexpr int PPP = 256 / TPP;  // pixels per pass
+  __shared__ float red[2][PPP][65];
+  const int b = blockIdx.z, cg = blockIdx.y, ch = blockIdx.x;
+  const int t = threadIdx.x, cc = t % TPP, po = t / TPP;
+  const int c0 = cg * 64 + cc * VEC;
+  const bool cok = c0 < C;
+  const T* xb = x + (long)b * HW * ldx;
+  float K[VEC], s1[VEC], s2[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) { K[e] = 0.f; s1[e] = 0.f; s2[e] = 0.f; }
+  if (cok) load16_f(xb + c0, K);
+  const int p0 = ch * chunk;
+  const int p1 = min(HW, p0 + chunk);
+  if (cok) {
+    for (int p = p0 + po; p < p1; p += PPP) {
+      float v[VEC];
+      load16_f(xb + (long)p * ldx + c0, v);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float d = v[e] - K[e];
+        s1[e] += d;
+        s2[e] = fmaf(d, d, s2[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    red[0][po][cc * VEC + e] = s1[e];
+    red[1][po][cc * VEC + e] = s2[e];
+  }
+  __syncthreads();
+  if (t < 64) {
+    const int c = cg * 64 + t;
+    float a = 0.f, q = 0.f;
+    for (int i = 0; i < PPP; ++i) { a += red[0][i][t]; q += red[1][i][t]; }
+    if (c < C) {
+      float* o = part + (((long)b * nchunk + ch) * C + c) * 2;
+      o[0] = a;
+      o[1] = q;
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+in_stats_final_kernel(const T* __restrict__ x, int ldx, int B, int HW, int C, int nchunk, const float* __restrict__ part,
+                      float* __restrict__ stat) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i - b * C;
+  const double K = (double)to_f(x[(long)b * HW * ldx + c]);
+  double S1 = 0.0, S2 = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    const float* o = part + (((long)b * nchunk + k) * C + c) * 2;
+    S1 += (double)o[0];
+    S2 += (double)o[1];
+  }
+  const double n = (double)HW;
+  const double md = S1 / n;
+  double var = S2 / n - md * md;
+  if (var < 0.0) var = 0.0;
+  stat[(long)i * 2 + 0] = (float)(K + md);
+  stat[(long)i * 2 + 1] = (float)(1.0 / sqrt(var + (double)kInEps));
+}
+
+static void stats_geometry(int HW, int& chunk, int& nchunk) {
+  chunk = HW < 1024 ? HW : 1024;
+  nchunk = (HW + chunk - 1) / chunk;
+}
+
+size_t in_stats_workspace_bytes(int B, int HW, int C) {
+  int chunk, nchunk;
+  stats_geometry(HW, chunk, nchunk);
+  return (size_t)B * nchunk * C * 2 * sizeof(float);
+}
+
+int in_stats(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, void* ws, size_t ws_bytes,
+             hipStream_t s) {
+  if (C % 16 || ldx % 8 || (uintptr_t)x % 16) return -1;
+  int chunk, nchunk;
+  stats_geometry(HW, chunk, nchunk);
+  if (!ws || ws_bytes < in_stats_workspace_bytes(B, HW, C)) return -1;
+  float* part = reinterpret_cast<float*>(ws);
+  dim3 g1(nchunk, (C + 63) / 64, B);
+  dim3 g2((B * C + 255) / 256);
+  if (dt == GHOST_F32) {
+    hipLaunchKernelGGL(in_stats_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)x, ldx, HW, C, chunk, nchunk, part);
+    hipLaunchKernelGGL(in_stats_final_kernel<float>, g2, dim3(256), 0, s, (const float*)x, ldx, B, HW, C, nchunk, part, stat);
+  } else if (dt == GHOST_BF16) {
+    hipLaunchKernelGGL(in_stats_partial_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)x, ldx, HW, C, chunk, nchunk, part);
+    hipLaunchKernelGGL(in_stats_final_kernel<bf16>, g2, dim3(256), 0, s, (const bf16*)x, ldx, B, HW, C, nchunk, part, stat);
+  } else {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// AAD mask: one lane group of G = min(64, C/VEC) lanes per pixel
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256)
+aad_mask_kernel(const T* __restrict__ h, int ldh, long P, int HW, int C, int G, const float* __restrict__ stat,
+                const float* __restrict__ wh, const float* __restrict__ bh, float* __restrict__ mask) {
+  constexpr int VEC = Vec16<T>::N;
+  const int t = threadIdx.x;
+  const int ppb = 256 / G;
+  const long p = (long)blockIdx.x * ppb + t / G;
+  const int gl = t % G;
+  float s = 0.f;
+  if (p < P) {
+    const int b = (int)(p / HW);
+    const float* st = stat + (long)b * C * 2;
+    for (int ci = gl; ci < C / VEC; ci += G) {
+      float v[VEC];
+      load16_f(h + p * ldh + ci * VEC, v);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const int c = ci * VEC + e;
+        s = fmaf(wh[c], (v[e] - st[2 * c]) * st[2 * c + 1], s);
+      }
+    }
+  }
+  s = group_sum(s, G);
+  if (p < P && gl == 0) mask[p] = sigmoidf_ref(s + bh[0]);
+}
+
+int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh, const float* bh,
+             float* mask, hipStream_t s) {
+  const int vec = dt == GHOST_F32 ? 4 : 8;
+  if (C % vec || ldh % vec || (uintptr_t)h % 16) return -1;
+  int G = C / vec;
+  if (G > 64) G = 64;
+  if (G & (G - 1)) return -1;   // power-of-two lane groups
+  const long P = (long)B * HW;
+  const int ppb = 256 / G;
+  dim3 grid((unsigned)((P + ppb - 1) / ppb));
+  if (dt == GHOST_F32)
+    hipLaunchKernelGGL(aad_mask_kernel<float>, grid, dim3(256), 0, s, (const float*)h, ldh, P, HW, C, G, stat, wh, bh, mask);
+  else if (dt == GHOST_BF16)
+    hipLaunchKernelGGL(aad_mask_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)h, ldh, P, HW, C, G, stat, wh, bh, mask);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// bilinear x2, align_corners=True: src = dst * (in-1)/(out-1)
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256)
+upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, int B, int H, int W, int C) {
+  constexpr int VEC = Vec16<T>::N;
+  const int nch = C / VEC;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const int Ho = 2 * H, Wo = 2 * W;
+  const long total = (long)B * Ho * Wo * nch;
+  if (idx >= total) return;
+  const int ci = (int)(idx % nch);
+  const long op = idx / nch;
+  const int ox = (int)(op % Wo);
+  const int oy = (int)((op / Wo) % Ho);
+  const int b = (int)(op / ((long)Wo * Ho));
+  const float sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
+  const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
+  const float ry = sh * (float)oy, rx = sw * (float)ox;
+  const int y0 = (int)ry, x0 = (int)rx;
+  const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+  const float ly1 = ry - (float)y0, ly0 = 1.f - ly1;
+  const float lx1 = rx - (float)x0, lx0 = 1.f - lx1;
+  const T* xb = x + (long)b * H * W * ldx + ci * VEC;
+  float v00[VEC], v01[VEC], v10[VEC], v11[VEC], o[VEC];
+  load16_f(xb + ((long)y0 * W + x0) * ldx, v00);
+  load16_f(xb + ((long)y0 * W + x1) * ldx, v01);
+  load16_f(xb + ((long)y1 * W + x0) * ldx, v10);
+  load16_f(xb + ((long)y1 * W + x1) * ldx, v11);
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) o[e] = ly0 * (lx0 * v00[e] + lx1 * v01[e]) + ly1 * (lx0 * v10[e] + lx1 * v11[e]);
+  store16_f(y + op * ldy + ci * VEC, o);
+}
+
+int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C, hipStream_t s) {
+  const int vec = dt == GHOST_F32 ? 4 : 8;
+  if (C % vec || ldx % vec || ldy % vec || (uintptr_t)x % 16 || (uintptr_t)y % 16) return -1;
+  const long total = (long)B * 4 * H * W * (C / vec);
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (dt == GHOST_F32)
+    hipLaunchKernelGGL(upsample2x_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, B, H, W, C);
+  else if (dt == GHOST_BF16)
+    hipLaunchKernelGGL(upsample2x_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, B, H, W, C);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// boundary conversions
+// ---------------------------------------------------------------------------
+template <typename TX, typename T>
+__global__ void __launch_bounds__(256)
+input_to_nhwc_kernel(const TX* __restrict__ x, long sb, long sc, long sh, long sw, int B, int C, int H, int W, T* __restrict__ y) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long total = (long)B * C * H * W;
+  if (idx >= total) return;
+  const int c = (int)(idx % C);
+  const long pix = idx / C;
+  const int w = (int)(pix % W);
+  const int h = (int)((pix / W) % H);
+  const int b = (int)(pix / ((long)W * H));
+  y[idx] = from_f<T>(to_f(x[b * sb + c * sc + h * sh + w * sw]));
+}
+
+template <typename TX>
+static int input_dispatch(const TX* x, const int64_t* st, int B, int C, int H, int W, int dt, void* y, hipStream_t s) {
+  const long total = (long)B * C * H * W;
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (dt == GHOST_F32)
+    hipLaunchKernelGGL((input_to_nhwc_kernel<TX, float>), grid, dim3(256), 0, s, x, (long)st[0], (long)st[1], (long)st[2], (long)st[3], B, C, H, W, (float*)y);
+  else if (dt == GHOST_BF16)
+    hipLaunchKernelGGL((input_to_nhwc_kernel<TX, bf16>), grid, dim3(256), 0, s, x, (long)st[0], (long)st[1], (long)st[2], (long)st[3], B, C, H, W, (bf16*)y);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+int input_to_nhwc(int xdt, const void* x, const int64_t strides[4], int B, int C, int H, int W, int dt, void* y,
+                  hipStream_t s) {
+  switch (xdt) {
+    case GHOST_F32: return input_dispatch((const float*)x, strides, B, C, H, W, dt, y, s);
+    case GHOST_BF16: return input_dispatch((const bf16*)x, strides, B, C, H, W, dt, y, s);
+    case GHOST_F16: return input_dispatch((const _Float16*)x, strides, B, C, H, W, dt, y, s);
+    case GHOST_U8: return input_dispatch((const uint8_t*)x, strides, B, C, H, W, dt, y, s);
+  }
+  return -1;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+crops_kernel(const uint8_t* __restrict__ crops, long bstride, int B, int H, int W, T* __restrict__ y) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;   // one output pixel
+  const long HW = (long)H * W;
+  if (idx >= (long)B * HW) return;
+  const int b = (int)(idx / HW);
+  const long p = idx - b * HW;
+  const uint8_t* src = crops + b * bstride + p * 3;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float t = (float)src[2 - c] / 255.0f;   // BGR -> RGB, /255.
+    t = (t - 0.5f) / 0.5f;
+    y[idx * 3 + c] = from_f<T>(t);
+  }
+}
+
+int crops_u8_to_input(const uint8_t* crops, int64_t batch_stride, int B, int H, int W, int dt, void* y, hipStream_t s) {
+  const long total = (long)B * H * W;
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (dt == GHOST_F32)
+    hipLaunchKernelGGL(crops_kernel<float>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (float*)y);
+  else if (dt == GHOST_BF16)
+    hipLaunchKernelGGL(crops_kernel<bf16>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (bf16*)y);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+y_u8_kernel(const T* __restrict__ y, int ldy, long P, uint8_t* __restrict__ out) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float t = (to_f(y[p * ldy + c]) * 0.5f + 0.5f) * 255.0f;
+    out[p * 3 + (2 - c)] = (uint8_t)(int)t;
+  }
+}
+
+int y_to_u8_bgr(int dt, const void* y, int ldy, int B, int H, int W, uint8_t* out, hipStream_t s) {
+  const long P = (long)B * H * W;
+  dim3 grid((unsigned)((P + 255) / 256));
+  if (dt == GHOST_F32)
+    hipLaunchKernelGGL(y_u8_kernel<float>, grid, dim3(256), 0, s, (const float*)y, ldy, P, out);
+  else if (dt == GHOST_BF16)
+    hipLaunchKernelGGL(y_u8_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)y, ldy, P, out);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+template <typename TX>
+__global__ void __launch_bounds__(256) rows_f32_kernel(const TX* __restrict__ x, long rs, int B, int n, float* __restrict__ y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * n) return;
+  const int b = (int)(i / n), k = (int)(i - (long)b * n);
+  y[i] = to_f(x[b * rs + k]);
+}
+
+int rows_to_f32(int xdt, const void* x, int64_t row_stride, int B, int n, float* y, hipStream_t s) {
+  dim3 grid((unsigned)(((long)B * n + 255) / 256));
+  if (xdt == GHOST_F32)
+    hipLaunchKernelGGL(rows_f32_kernel<float>, grid, dim3(256), 0, s, (const float*)x, (long)row_stride, B, n, y);
+  else if (xdt == GHOST_BF16)
+    hipLaunchKernelGGL(rows_f32_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, (long)row_stride, B, n, y);
+  else if (xdt == GHOST_F16)
+    hipLaunchKernelGGL(rows_f32_kernel<_Float16>, grid, dim3(256), 0, s, (const _Float16*)x, (long)row_stride, B, n, y);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+nhwc_nchw_kernel(const T* __restrict__ x, int ldx, int B, int H, int W, int C, T* __restrict__ y) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;   // NCHW linear index
+  const long HW = (long)H * W;
+  if (idx >= (long)B * C * HW) return;
+  const long p = idx % HW;
+  const int c = (int)((idx / HW) % C);
+  const int b = (int)(idx / (HW * C));
+  y[idx] = x[(b * HW + p) * ldx + c];
+}
+
+int nhwc_to_nchw(int dt, const void* x, int ldx, int B, int H, int W, int C, void* y, hipStream_t s) {
+  const long total = (long)B * C * H * W;
+  dim3 grid((unsigned)((total + 255) / 256));
+  if (dt == GHOST_F32)
+    hipLaunchKernelGGL(nhwc_nchw_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, B, H, W, C, (float*)y);
+  else if (dt == GHOST_BF16)
+    hipLaunchKernelGGL(nhwc_nchw_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, B, H, W, C, (bf16*)y);
+  else
+    return -1;
+  return (int)hipGetLastError();
+}
+
+}  // namespace ghost

@@ -1,0 +1,284 @@
+"""Drop-in for network/AEI_Net.py on MI355X.
+
+``AEI_Net(backbone, num_blocks=2, c_id=256)`` keeps the reference constructor,
+submodule names and state_dict keys (AEI_Net.py:19-159), so
+``G.load_state_dict(torch.load(path, map_location='cpu'))``, ``.cuda()``, ``.half()``,
+``.eval()`` and ``forward(Xt, z_id) -> (Y, attr)`` / ``get_attr(X)`` behave as in
+inference.py:26-30 and faceshifter_run.py:19.
+
+Execution: the whole forward is one call into libghost_amd.so (``ghost_aei_forward``),
+which runs hand-written gfx950 kernels on the caller's current HIP stream.  The weights
+are packed once per (device, dtype) into the kernels' layouts (pack.py) and re-packed
+automatically when a parameter changes.  Outputs are NHWC in device memory; ``Y`` and
+the attr maps are returned as NCHW *views* (``channels_last`` strides) — same shapes and
+values as the reference, no copy.
+
+Numerics: fp32 parameters run the fp32 path (exact-fp32 MFMA, |dY| <= 1e-3 vs the
+reference CPU forward); ``.half()`` / ``.bfloat16()`` parameters (or
+``compute_dtype=torch.bfloat16``) run the bf16 throughput path (bf16 storage, fp32
+accumulation) and return bf16 tensors.  There is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .. import _lib
+from .AADLayer import AAD_ResBlk, AADLayer, AddBlocksSequential  # noqa: F401  (reference re-exports)
+from .pack import pack_all
+
+
+def weight_init(m):
+    """AEI_Net.py:8-16 (irrelevant once a checkpoint is loaded; kept for state parity)."""
+    if isinstance(m, nn.Linear):
+        m.weight.data.normal_(0, 0.001)
+        m.bias.data.zero_()
+    if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)):
+        nn.init.xavier_normal_(m.weight.data)
+
+
+class _Container(nn.Sequential):
+    def forward(self, *inputs):
+        raise NotImplementedError("ghost_amd: encoder blocks run inside AEI_Net.forward / get_attr on the MI355X path")
+
+
+def conv4x4(in_c, out_c, norm=nn.BatchNorm2d):
+    """Conv4x4/s2/p1 -> BN -> LeakyReLU(0.1) container (AEI_Net.py:19-24)."""
+    return _Container(nn.Conv2d(in_channels=in_c, out_channels=out_c, kernel_size=4, stride=2, padding=1, bias=False),
+                      norm(out_c), nn.LeakyReLU(0.1, inplace=True))
+
+
+class deconv4x4(nn.Module):
+    """ConvT4x4/s2/p1 -> BN -> LReLU -> cat / add skip (AEI_Net.py:27-41)."""
+
+    def __init__(self, in_c, out_c, norm=nn.BatchNorm2d):
+        super().__init__()
+        self.deconv = nn.ConvTranspose2d(in_channels=in_c, out_channels=out_c, kernel_size=4, stride=2, padding=1,
+                                         bias=False)
+        self.bn = norm(out_c)
+        self.lrelu = nn.LeakyReLU(0.1, inplace=True)
+
+    def forward(self, input, skip, backbone):
+        raise NotImplementedError("ghost_amd: deconv4x4 runs inside AEI_Net.forward / get_attr on the MI355X path")
+
+
+class MLAttrEncoder(nn.Module):
+    """Multi-level attribute encoder (AEI_Net.py:44-95)."""
+
+    def __init__(self, backbone):
+        super().__init__()
+        self.backbone = backbone
+        self.conv1 = conv4x4(3, 32)
+        self.conv2 = conv4x4(32, 64)
+        self.conv3 = conv4x4(64, 128)
+        self.conv4 = conv4x4(128, 256)
+        self.conv5 = conv4x4(256, 512)
+        self.conv6 = conv4x4(512, 1024)
+        self.conv7 = conv4x4(1024, 1024)
+        if backbone == 'unet':
+            chans = [(1024, 1024), (2048, 512), (1024, 256), (512, 128), (256, 64), (128, 32)]
+        elif backbone == 'linknet':
+            chans = [(1024, 1024), (1024, 512), (512, 256), (256, 128), (128, 64), (64, 32)]
+        else:
+            chans = []
+        for i, (ci, co) in enumerate(chans, 1):
+            setattr(self, f"deconv{i}", deconv4x4(ci, co))
+        self.apply(weight_init)
+        self._owner = None
+
+    def forward(self, Xt):
+        if self._owner is None:
+            raise NotImplementedError("ghost_amd: call AEI_Net.get_attr (the encoder runs as part of the AEI_Net plan)")
+        return self._owner().get_attr(Xt)
+
+
+class AADGenerator(nn.Module):
+    """AAD generator (AEI_Net.py:98-139); executed by AEI_Net.forward."""
+
+    def __init__(self, backbone, c_id=256, num_blocks=2):
+        super().__init__()
+        self.up1 = nn.ConvTranspose2d(c_id, 1024, kernel_size=2, stride=1, padding=0)
+        self.AADBlk1 = AAD_ResBlk(1024, 1024, 1024, c_id, num_blocks)
+        if backbone == 'linknet':
+            self.AADBlk2 = AAD_ResBlk(1024, 1024, 1024, c_id, num_blocks)
+            self.AADBlk3 = AAD_ResBlk(1024, 1024, 512, c_id, num_blocks)
+            self.AADBlk4 = AAD_ResBlk(1024, 512, 256, c_id, num_blocks)
+            self.AADBlk5 = AAD_ResBlk(512, 256, 128, c_id, num_blocks)
+            self.AADBlk6 = AAD_ResBlk(256, 128, 64, c_id, num_blocks)
+            self.AADBlk7 = AAD_ResBlk(128, 64, 32, c_id, num_blocks)
+            self.AADBlk8 = AAD_ResBlk(64, 3, 32, c_id, num_blocks)
+        else:
+            self.AADBlk2 = AAD_ResBlk(1024, 1024, 2048, c_id, num_blocks)
+            self.AADBlk3 = AAD_ResBlk(1024, 1024, 1024, c_id, num_blocks)
+            self.AADBlk4 = AAD_ResBlk(1024, 512, 512, c_id, num_blocks)
+            self.AADBlk5 = AAD_ResBlk(512, 256, 256, c_id, num_blocks)
+            self.AADBlk6 = AAD_ResBlk(256, 128, 128, c_id, num_blocks)
+            self.AADBlk7 = AAD_ResBlk(128, 64, 64, c_id, num_blocks)
+            self.AADBlk8 = AAD_ResBlk(64, 3, 64, c_id, num_blocks)
+        self.apply(weight_init)
+
+    def forward(self, z_attr, z_id):
+        raise NotImplementedError("ghost_amd: AADGenerator runs inside AEI_Net.forward on the MI355X path")
+
+
+class _Runtime:
+    """Native handle + packed weights for one (device, compute dtype)."""
+
+    def __init__(self, backbone, num_blocks, c_id, dtype, slots):
+        self.lib = _lib.load()
+        self.dtype = dtype
+        h = C.c_void_p()
+        _lib.check(self.lib.ghost_aei_create(backbone.encode(), num_blocks, c_id, _lib.gdtype(dtype), C.byref(h)),
+                   "ghost_aei_create")
+        self.h = h
+        self.slots = slots  # keeps the packed tensors alive
+        for name, t in slots.items():
+            _lib.check(self.lib.ghost_aei_bind(h, name.encode(), t.data_ptr(), t.numel()), f"bind {name}")
+        if self.lib.ghost_aei_missing(h) != 0:
+            _lib.check(-2, "weights incomplete")
+        self.geom = []
+        for k in range(1, 9):
+            c_, h_, w_ = C.c_int(), C.c_int(), C.c_int()
+            _lib.check(self.lib.ghost_aei_attr_geometry(h, k, C.byref(c_), C.byref(h_), C.byref(w_)))
+            self.geom.append((c_.value, h_.value, w_.value))
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.ghost_aei_destroy(self.h)
+        except Exception:
+            pass
+
+
+class AEI_Net(nn.Module):
+    """AEI_Net(backbone, num_blocks=2, c_id=256)  (AEI_Net.py:143-159)."""
+
+    def __init__(self, backbone, num_blocks=2, c_id=256, *, compute_dtype: Optional[torch.dtype] = None):
+        super().__init__()
+        self.c_id = c_id
+        self.backbone = backbone
+        self.num_blocks = num_blocks
+        self.compute_dtype = compute_dtype
+        if backbone in ['unet', 'linknet']:
+            self.encoder = MLAttrEncoder(backbone)
+        elif backbone == 'resnet':
+            raise NotImplementedError("ghost_amd: backbone='resnet' has no MI355X path yet (SURVEY.md §8f row 4)")
+        else:
+            raise ValueError(f"unknown backbone {backbone!r}")
+        self.generator = AADGenerator(backbone, c_id, num_blocks)
+        self._rt = None
+        self._rt_sig = None
+        import weakref
+        self.encoder._owner = weakref.ref(self)
+
+    # -- weights -------------------------------------------------------------------
+    def _dtype(self) -> torch.dtype:
+        if self.compute_dtype is not None:
+            return self.compute_dtype
+        return torch.float32 if self.generator.up1.weight.dtype == torch.float32 else torch.bfloat16
+
+    def _runtime(self, device) -> _Runtime:
+        dt = self._dtype()
+        sig = (device, dt) + tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
+        if self._rt is None or self._rt_sig != sig:
+            sd = {k: v.detach() for k, v in self.state_dict().items()}
+            for k, v in sd.items():
+                if v.is_floating_point() and v.device != device:
+                    raise RuntimeError(f"ghost_amd: parameter {k} is on {v.device}, input on {device}")
+            with torch.no_grad():
+                slots = pack_all(sd, self.backbone, self.num_blocks, self.c_id, dt)
+            self._rt = _Runtime(self.backbone, self.num_blocks, self.c_id, dt, slots)
+            self._rt_sig = sig
+        return self._rt
+
+    # -- execution -----------------------------------------------------------------
+    def _prep(self, Xt, what):
+        _lib.require_gpu(Xt, what)
+        if Xt.ndim != 4 or tuple(Xt.shape[1:]) != (3, 256, 256):
+            raise RuntimeError(f"ghost_amd: {what} expects Xt of shape [B,3,256,256], got {tuple(Xt.shape)}")
+        if Xt.dtype not in (torch.float32, torch.float16, torch.bfloat16):
+            raise TypeError(f"ghost_amd: unsupported input dtype {Xt.dtype}")
+        rt = self._runtime(Xt.device)
+        B = Xt.shape[0]
+        attrs = [torch.empty(B, h, w, c, dtype=rt.dtype, device=Xt.device) for (c, h, w) in rt.geom]
+        st = (C.c_int64 * 4)(*Xt.stride())
+        return rt, B, attrs, st
+
+    @torch.no_grad()
+    def forward(self, Xt, z_id, *, out_u8: Optional[torch.Tensor] = None):
+        rt, B, attrs, st = self._prep(Xt, "AEI_Net.forward")
+        z = z_id.reshape(z_id.shape[0], -1)
+        if z.shape[0] != B or z.shape[1] != self.c_id:
+            raise RuntimeError(f"ghost_amd: z_id must hold {B} rows of {self.c_id}, got {tuple(z_id.shape)}")
+        if z.stride(1) != 1:
+            z = z.contiguous()
+        dev = Xt.device
+        Y = torch.empty(B, 256, 256, 3, dtype=rt.dtype, device=dev)
+        if out_u8 is not None and (out_u8.shape != (B, 256, 256, 3) or out_u8.dtype != torch.uint8
+                                   or not out_u8.is_contiguous() or out_u8.device != dev):
+            raise RuntimeError("ghost_amd: out_u8 must be a contiguous uint8 [B,256,256,3] tensor on the input device")
+        lib = rt.lib
+        nbytes = lib.ghost_aei_workspace_bytes(rt.h, B)
+        if nbytes < 0:
+            _lib.check(int(nbytes), "workspace sizing")
+        ws = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
+        ap = (C.c_void_p * 8)(*[a.data_ptr() for a in attrs])
+        _lib.check(lib.ghost_aei_forward(rt.h, Xt.data_ptr(), _lib.gdtype(Xt.dtype), st, B, z.data_ptr(),
+                                         _lib.gdtype(z.dtype), z.stride(0), Y.data_ptr(),
+                                         out_u8.data_ptr() if out_u8 is not None else None, ap, ws.data_ptr(),
+                                         ws.numel(), _lib.stream_ptr(dev)), "AEI_Net.forward")
+        return Y.permute(0, 3, 1, 2), tuple(a.permute(0, 3, 1, 2) for a in attrs)
+
+    @torch.no_grad()
+    def get_attr(self, X):
+        rt, B, attrs, st = self._prep(X, "AEI_Net.get_attr")
+        lib = rt.lib
+        nbytes = lib.ghost_aei_workspace_bytes(rt.h, B)
+        ws = torch.empty(int(nbytes), dtype=torch.uint8, device=X.device)
+        ap = (C.c_void_p * 8)(*[a.data_ptr() for a in attrs])
+        _lib.check(lib.ghost_aei_get_attr(rt.h, X.data_ptr(), _lib.gdtype(X.dtype), st, B, ap, ws.data_ptr(),
+                                          ws.numel(), _lib.stream_ptr(X.device)), "AEI_Net.get_attr")
+        return tuple(a.permute(0, 3, 1, 2) for a in attrs)
+
+    @torch.no_grad()
+    def swap_u8(self, crops_u8: torch.Tensor, z_id: torch.Tensor, out: Optional[torch.Tensor] = None):
+        """Fused faceshifter_batch on device uint8 BGR crops [B,256,256,3] -> uint8 BGR [B,256,256,3]."""
+        _lib.require_gpu(crops_u8, "AEI_Net.swap_u8")
+        if crops_u8.dtype != torch.uint8 or crops_u8.ndim != 4 or tuple(crops_u8.shape[1:]) != (256, 256, 3):
+            raise RuntimeError("ghost_amd: crops must be uint8 [B,256,256,3]")
+        if crops_u8[0].stride() != (768, 3, 1):
+            crops_u8 = crops_u8.contiguous()
+        dev = crops_u8.device
+        rt = self._runtime(dev)
+        B = crops_u8.shape[0]
+        z = z_id.reshape(z_id.shape[0], -1)
+        if z.stride(1) != 1:
+            z = z.contiguous()
+        zrs = z.stride(0) if z.shape[0] == B else 0   # one identity row broadcast (faceshifter_run.py:15-16)
+        if z.shape[0] not in (1, B):
+            raise RuntimeError("ghost_amd: z_id must have 1 or B rows")
+        if out is None:
+            out = torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev)
+        lib = rt.lib
+        nbytes = lib.ghost_aei_swap_workspace_bytes(rt.h, B)
+        ws = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
+        _lib.check(lib.ghost_aei_swap_u8(rt.h, crops_u8.data_ptr(), crops_u8.stride(0), B, z.data_ptr(),
+                                         _lib.gdtype(z.dtype), zrs, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                         _lib.stream_ptr(dev)), "AEI_Net.swap_u8")
+        return out
+
+    def profile(self, class_mask: int):
+        """Enable per-kernel-class HIP-event timing on the native runtime (bench instrumentation)."""
+        rt = self._rt
+        if rt is None:
+            raise RuntimeError("ghost_amd: run one forward before enabling profiling")
+        _lib.check(rt.lib.ghost_aei_profile(rt.h, class_mask))
+
+    def profile_read(self, cls: int):
+        rt = self._rt
+        ms, n, by, fl = C.c_double(), C.c_int64(), C.c_double(), C.c_double()
+        _lib.check(rt.lib.ghost_aei_profile_read(rt.h, cls, C.byref(ms), C.byref(n), C.byref(by), C.byref(fl)))
+        return {"ms": ms.value, "launches": n.value, "bytes": by.value, "flops": fl.value}

@@ -1,0 +1,147 @@
+"""Weight packing: reference state_dict tensors -> the layouts the gfx950 kernels read.
+
+Host-side tensor plumbing only (torch ops on the device, once per weight load).
+Slot names are the ones ``ghost_aei_bind`` accepts (see aei_runtime.hip
+``declare_slots``); INTEGRATION.md documents every layout.
+
+Layouts (Npad = Cout rounded up to 128, Kpad = K rounded up to 32, zero padded):
+  conv  [Cout,Cin,kh,kw]      -> [Npad][Kpad], K = (ky*kw + kx)*Cin + c
+  convT [Cin,Cout,4,4] (s2p1) -> [4][Npad][Kpad], phase = 2*py+px, K = (ty*2+tx)*Cin + c,
+                                 kernel tap ky = ((1,3),(0,2))[py][ty]  (sub-pixel decomposition)
+  AAD conv1/conv2 (1x1)       -> [Npad][Kpad] rows interleaved per 16 channels: gamma c0..15,
+                                 beta c0..15, gamma c16..31, ...  (+ the same for the biases)
+  all fc1/fc2 (Linear)        -> one fp32 [Npad][Kpad] = [gamma_l | beta_l] per AADLayer l in plan order
+  up1 ConvT k2 on 1x1         -> fp32 [4096][Kpad], n = (y*2+x)*1024 + co
+  BatchNorm (eval)            -> fp32 scale = g/sqrt(rv+eps), shift = b - rm*scale
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import torch
+
+BN_EPS = 1e-5
+_KTAP = ((1, 3), (0, 2))  # convT 4x4/s2/p1: kernel index of sub-pixel tap t at output parity p
+
+ENC_DOWN = [(3, 32), (32, 64), (64, 128), (128, 256), (256, 512), (512, 1024), (1024, 1024)]
+ENC_UP = {"unet": [(1024, 1024), (2048, 512), (1024, 256), (512, 128), (256, 64), (128, 32)],
+          "linknet": [(1024, 1024), (1024, 512), (512, 256), (256, 128), (128, 64), (64, 32)]}
+GEN_BLOCKS = {
+    "unet": [(1024, 1024, 1024), (1024, 1024, 2048), (1024, 1024, 1024), (1024, 512, 512),
+             (512, 256, 256), (256, 128, 128), (128, 64, 64), (64, 3, 64)],
+    "linknet": [(1024, 1024, 1024), (1024, 1024, 1024), (1024, 1024, 512), (1024, 512, 256),
+                (512, 256, 128), (256, 128, 64), (128, 64, 32), (64, 3, 32)],
+}
+
+
+def rup(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+def pack_conv(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    co, ci, kh, kw = w.shape
+    k = kh * kw * ci
+    out = torch.zeros(rup(co, 128), rup(k, 32), dtype=dtype, device=w.device)
+    out[:co, :k] = w.permute(0, 2, 3, 1).reshape(co, k).to(dtype)
+    return out
+
+
+def pack_convT4x4(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    ci, co = w.shape[:2]
+    out = torch.zeros(4, rup(co, 128), rup(4 * ci, 32), dtype=dtype, device=w.device)
+    for py in range(2):
+        for px in range(2):
+            taps = [w[:, :, _KTAP[py][ty], _KTAP[px][tx]].t() for ty in range(2) for tx in range(2)]
+            out[2 * py + px, :co, :4 * ci] = torch.stack(taps, 1).reshape(co, 4 * ci).to(dtype)
+    return out
+
+
+def bn_fold(sd: Dict[str, torch.Tensor], prefix: str, npad: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    g = sd[f"{prefix}.weight"].float()
+    b = sd[f"{prefix}.bias"].float()
+    rm = sd[f"{prefix}.running_mean"].float()
+    rv = sd[f"{prefix}.running_var"].float()
+    scale = g / torch.sqrt(rv + BN_EPS)
+    shift = b - rm * scale
+    s = torch.zeros(npad, dtype=torch.float32, device=g.device)
+    t = torch.zeros(npad, dtype=torch.float32, device=g.device)
+    s[:scale.numel()] = scale
+    t[:shift.numel()] = shift
+    return s, t
+
+
+def interleave16(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """rows [a0..15, b0..15, a16..31, b16..31, ...] (the AAD GEMM's gamma/beta column pairs)."""
+    c = a.shape[0]
+    assert c % 16 == 0
+    rest = a.shape[1:]
+    return torch.stack([a.reshape(c // 16, 16, *rest), b.reshape(c // 16, 16, *rest)], 1).reshape(2 * c, *rest)
+
+
+def pack_aad(sd, prefix: str, dtype) -> Dict[str, torch.Tensor]:
+    w1 = sd[f"{prefix}.conv1.weight"]
+    c, ca = w1.shape[:2]
+    gb = interleave16(w1.reshape(c, ca), sd[f"{prefix}.conv2.weight"].reshape(c, ca))
+    gbw = torch.zeros(rup(2 * c, 128), rup(ca, 32), dtype=dtype, device=w1.device)
+    gbw[:2 * c, :ca] = gb.to(dtype)
+    gbb = torch.zeros(rup(2 * c, 128), dtype=torch.float32, device=w1.device)
+    gbb[:2 * c] = interleave16(sd[f"{prefix}.conv1.bias"].float(), sd[f"{prefix}.conv2.bias"].float())
+    return {"gbw": gbw, "gbb": gbb,
+            "wh": sd[f"{prefix}.conv_h.weight"].reshape(c).float().contiguous(),
+            "bh": sd[f"{prefix}.conv_h.bias"].reshape(1).float().contiguous()}
+
+
+def aad_plan(backbone: str, num_blocks: int) -> List[Tuple[str, str]]:
+    """(slot prefix, state_dict prefix) of every AADLayer in the runtime's plan order."""
+    out = []
+    for k, (cin, cout, _) in enumerate(GEN_BLOCKS[backbone], 1):
+        for i in range(num_blocks):
+            out.append((f"gen.blk{k}.aad{i}", f"generator.AADBlk{k}.add_blocks.{3 * i}"))
+        if cin != cout:
+            out.append((f"gen.blk{k}.aadlast", f"generator.AADBlk{k}.last_add_block.0"))
+    return out
+
+
+def pack_all(sd: Dict[str, torch.Tensor], backbone: str, num_blocks: int, c_id: int,
+             dtype: torch.dtype) -> Dict[str, torch.Tensor]:
+    """Every runtime slot -> a contiguous device tensor."""
+    if backbone not in GEN_BLOCKS:
+        raise NotImplementedError(f"ghost_amd: backbone {backbone!r} has no MI355X path yet")
+    slots: Dict[str, torch.Tensor] = {}
+    for i, (_ci, co) in enumerate(ENC_DOWN, 1):
+        slots[f"enc.conv{i}.w"] = pack_conv(sd[f"encoder.conv{i}.0.weight"], dtype)
+        s, t = bn_fold(sd, f"encoder.conv{i}.1", rup(co, 128))
+        slots[f"enc.conv{i}.scale"], slots[f"enc.conv{i}.shift"] = s, t
+    for i, (_ci, co) in enumerate(ENC_UP[backbone], 1):
+        slots[f"enc.deconv{i}.w"] = pack_convT4x4(sd[f"encoder.deconv{i}.deconv.weight"], dtype)
+        s, t = bn_fold(sd, f"encoder.deconv{i}.bn", rup(co, 128))
+        slots[f"enc.deconv{i}.scale"], slots[f"enc.deconv{i}.shift"] = s, t
+    # up1: ConvTranspose2d(c_id, 1024, k=2) on a 1x1 input
+    w = sd["generator.up1.weight"].float()
+    dev = w.device
+    up = torch.zeros(4096, rup(c_id, 32), dtype=torch.float32, device=dev)
+    up[:, :c_id] = w.permute(2, 3, 1, 0).reshape(4096, c_id)
+    slots["gen.up1.w"] = up
+    slots["gen.up1.shift"] = sd["generator.up1.bias"].float().repeat(4).contiguous()
+    # AAD layers + the identity table
+    ids_w, ids_b = [], []
+    for slot, pre in aad_plan(backbone, num_blocks):
+        for k, v in pack_aad(sd, pre, dtype).items():
+            slots[f"{slot}.{k}"] = v
+        ids_w += [sd[f"{pre}.fc1.weight"].float(), sd[f"{pre}.fc2.weight"].float()]
+        ids_b += [sd[f"{pre}.fc1.bias"].float(), sd[f"{pre}.fc2.bias"].float()]
+    wid = torch.cat(ids_w, 0)
+    ntot = wid.shape[0]
+    idw = torch.zeros(rup(ntot, 128), rup(c_id, 32), dtype=torch.float32, device=dev)
+    idw[:ntot, :c_id] = wid
+    idb = torch.zeros(rup(ntot, 128), dtype=torch.float32, device=dev)
+    idb[:ntot] = torch.cat(ids_b, 0)
+    slots["gen.id.w"], slots["gen.id.shift"] = idw, idb
+    # AAD_ResBlk 3x3 convs; the last one of a cin != cout block is fused with last_add_block's
+    for k, (cin, cout, _) in enumerate(GEN_BLOCKS[backbone], 1):
+        for i in range(num_blocks):
+            w = sd[f"generator.AADBlk{k}.add_blocks.{3 * i + 2}.weight"]
+            if i == num_blocks - 1 and cin != cout:
+                w = torch.cat([w, sd[f"generator.AADBlk{k}.last_add_block.2.weight"]], 1)
+            slots[f"gen.blk{k}.conv{i}.w"] = pack_conv(w, dtype)
+    return {k: v.contiguous() for k, v in slots.items()}

@@ -1,0 +1,126 @@
+/* ghost_amd — C ABI of the MI355X-native GHOST swap forward path.
+ *
+ * This is the drop-in boundary for the per-frame face-swap hot path of GHOST
+ * (postworthy/ghost, a fork of sber-swap): the AEI_Net generator = attribute
+ * encoder + AAD ResBlk decoder.  Every entry point takes plain device pointers,
+ * sizes and an hipStream_t (passed as void*), returns an int status
+ * (0 = success, <0 = invalid argument / state, >0 = hipError_t), never throws,
+ * and never allocates device memory on the hot path (the caller supplies the
+ * workspace).  ghost_last_error() describes the last failure of the calling thread.
+ *
+ * Reference interfaces replaced (paths under the reference repository):
+ *   network/AEI_Net.py:143-151   AEI_Net(backbone, num_blocks, c_id)        -> ghost_aei_create
+ *   inference.py:27-30           G.load_state_dict(...); .cuda(); .half()   -> ghost_aei_bind (prepacked)
+ *   network/AEI_Net.py:153-156   AEI_Net.forward(Xt, z_id) -> (Y, attr)     -> ghost_aei_forward
+ *   network/AEI_Net.py:158-159   AEI_Net.get_attr(X)                       -> ghost_aei_get_attr
+ *   utils/inference/faceshifter_run.py:5-22 + utils/inference/core.py:13-26
+ *                                faceshifter_batch(transform_target_to_torch(crops)) -> ghost_aei_swap_u8
+ *   network/AADLayer.py:20-38    AADLayer.forward(h_in, z_attr, z_id)       -> ghost_aad_layer_nhwc
+ *   network/AEI_Net.py:19-24     conv4x4 (Conv 4x4/s2 + BN + LReLU)         -> ghost_conv2d_nhwc
+ *   network/AEI_Net.py:27-41     deconv4x4 (ConvT 4x4/s2 + BN + LReLU + skip) -> ghost_conv_transpose4x4s2_nhwc
+ *   network/AADLayer.py:64,71    Conv2d 3x3 of AAD_ResBlk (+ residual)     -> ghost_conv2d_nhwc
+ *   network/AADLayer.py:16,24    InstanceNorm2d statistics                 -> ghost_instnorm_stats_nhwc
+ *   network/AEI_Net.py:94,125    F.interpolate(x2, bilinear, align_corners) -> ghost_upsample2x_nhwc
+ *
+ * Activations crossing this ABI are NHWC with an explicit channel stride `ld`
+ * (elements between consecutive pixels).  Packed weight layouts are documented
+ * in INTEGRATION.md and produced by ghost_amd/network/pack.py.
+ */
+#ifndef GHOST_AMD_H
+#define GHOST_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { GHOST_DTYPE_F32 = 0, GHOST_DTYPE_BF16 = 1, GHOST_DTYPE_F16 = 2, GHOST_DTYPE_U8 = 3 };
+enum { GHOST_OK = 0, GHOST_EINVAL = -1, GHOST_ENOTREADY = -2, GHOST_ENOWS = -3 };
+
+typedef struct ghost_aei ghost_aei;
+
+const char* ghost_version(void);
+const char* ghost_last_error(void);
+
+/* ---- whole-network handle (one per device) ---------------------------------------- */
+/* backbone: "unet" | "linknet"; dtype: compute/storage dtype of activations and
+ * conv weights (GHOST_DTYPE_F32 = parity path, GHOST_DTYPE_BF16 = throughput path). */
+int ghost_aei_create(const char* backbone, int num_blocks, int c_id, int dtype, ghost_aei** out);
+void ghost_aei_destroy(ghost_aei* h);
+/* bind one prepacked weight tensor (device pointer, numel elements) under its slot name */
+int ghost_aei_bind(ghost_aei* h, const char* name, const void* dev_ptr, int64_t numel);
+/* number of slots still unbound (0 = ready); name of the first missing one in ghost_last_error() */
+int ghost_aei_missing(ghost_aei* h);
+/* geometry of z_attr_k (k = 1..8): channels, height, width (NHWC contiguous) */
+int ghost_aei_attr_geometry(ghost_aei* h, int level, int* C, int* H, int* W);
+/* device workspace needed by one forward of batch B (attr buffers supplied by the caller) */
+int64_t ghost_aei_workspace_bytes(ghost_aei* h, int B);
+
+/* AEI_Net.forward.  xt: [B,3,256,256] addressed with element strides xt_strides (any
+ * layout, e.g. the permuted NHWC view of core.py:24), dtype f32/f16/bf16.  z_id: [B, c_id]
+ * rows with row stride zid_row_stride.  y_nhwc: [B,256,256,3] in the handle dtype (tanh
+ * output).  y_u8_bgr (optional): [B,256,256,3] uint8 BGR.  attr_nhwc: 8 device buffers
+ * with the geometry above in the handle dtype (all required). */
+int ghost_aei_forward(ghost_aei* h, const void* xt, int xt_dtype, const int64_t xt_strides[4], int B,
+                      const void* z_id, int zid_dtype, int64_t zid_row_stride, void* y_nhwc, uint8_t* y_u8_bgr,
+                      void* const attr_nhwc[8], void* ws, int64_t ws_bytes, void* stream);
+/* AEI_Net.get_attr: the encoder only */
+int ghost_aei_get_attr(ghost_aei* h, const void* xt, int xt_dtype, const int64_t xt_strides[4], int B,
+                       void* const attr_nhwc[8], void* ws, int64_t ws_bytes, void* stream);
+/* faceshifter_batch on uint8 BGR crops [B,256,256,3] (crop_batch_stride bytes apart):
+ * normalise -> AEI_Net -> ((Y*0.5+0.5)*255)[...,BGR].uint8 into out_u8 [B,256,256,3].
+ * y_nhwc and attr buffers come from the workspace. */
+int64_t ghost_aei_swap_workspace_bytes(ghost_aei* h, int B);
+int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_stride, int B, const void* z_id,
+                      int zid_dtype, int64_t zid_row_stride, uint8_t* out_u8, void* ws, int64_t ws_bytes,
+                      void* stream);
+
+/* per-kernel-class device timing with HIP events (bench instrumentation).
+ * class_mask bit i enables class i; classes: 0 AAD GEMM (all stages), 1 AAD GEMM at
+ * 256x256, 2 conv3x3 (all), 3 conv3x3 at 256x256, 4 IN stats + mask, 5 encoder, 6 upsample. */
+int ghost_aei_profile(ghost_aei* h, int class_mask);
+/* after the stream is synchronised: total ms, launches, algorithmic bytes and flops of class i */
+int ghost_aei_profile_read(ghost_aei* h, int cls, double* ms, int64_t* launches, double* bytes, double* flops);
+
+/* ---- single operators (NHWC, per-op parity tests and callers of single layers) ------ */
+/* Conv2d kh x kw / stride / pad (+ per-channel scale/shift, leaky slope, residual, tanh).
+ * w_packed: [Npad][Kpad] with K index (ky*kw + kx)*Cin + c. */
+int ghost_conv2d_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx, const void* w_packed, int Cout,
+                      int Npad, int Kpad, int kh, int kw, int stride, int pad, const float* scale, const float* shift,
+                      float slope, const void* res, int ldres, int tanh_out, void* y, int ldy, void* ws,
+                      int64_t ws_bytes, void* stream);
+/* ConvTranspose2d 4x4/s2/p1 as four 2x2 sub-pixel phases; w_packed: [4][Npad][Kpad],
+ * phase = 2*py + px, K index (ty*2 + tx)*Cin + c. */
+int ghost_conv_transpose4x4s2_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx,
+                                   const void* w_packed, int Cout, int Npad, int Kpad, const float* scale,
+                                   const float* shift, float slope, const void* res, int ldres, void* y, int ldy,
+                                   void* ws, int64_t ws_bytes, void* stream);
+/* fp32 GEMM y[B, N] = x[B, K] * W^T + bias (Linear / ConvT-on-1x1); out dtype f32 or bf16 */
+int ghost_linear_f32(const float* x, int B, int K, const float* w_packed, int N, int Npad, int Kpad,
+                     const float* bias, int out_dtype, void* y, int ldy, void* ws, int64_t ws_bytes, void* stream);
+/* InstanceNorm statistics: stat[b][c] = (mean, 1/sqrt(var+1e-5)) */
+int ghost_instnorm_stats_nhwc(int dtype, const void* x, int B, int HW, int C, int ldx, float* stat, void* ws,
+                              int64_t ws_bytes, void* stream);
+/* AADLayer.forward: gbw_packed [Npad][Kpad] rows interleaved per 16 channels
+ * (gamma c0..15, beta c0..15, gamma c16..31, ...), gbb the matching biases (fp32);
+ * wh [C] / bh [1] the conv_h weights; idgb [B][id_ld] holds gamma_id at c and beta_id
+ * at C + c (fp32).  slope = 1: plain AADLayer; slope = 0: fused following ReLU. */
+int ghost_aad_layer_nhwc(int dtype, const void* h_in, int ldh, const void* z_attr, int lda, int B, int H, int W, int C,
+                         int Ca, const void* gbw_packed, int Npad, int Kpad, const float* gbb, const float* wh,
+                         const float* bh, const float* idgb, int id_ld, float slope, void* out, int ldo, void* ws,
+                         int64_t ws_bytes, void* stream);
+int ghost_upsample2x_nhwc(int dtype, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C,
+                          void* stream);
+int ghost_nhwc_to_nchw(int dtype, const void* x, int ldx, int B, int H, int W, int C, void* y, void* stream);
+/* transform_target_to_torch (core.py:13-26): uint8 BGR NHWC crops -> RGB NHWC in [-1,1] (dtype f32/bf16) */
+int ghost_crops_to_input_nhwc(const uint8_t* crops, int64_t crop_batch_stride, int B, int H, int W, int dtype, void* y,
+                              void* stream);
+/* testing knob: force the split-K factor of subsequent single-operator convs (0 = heuristic) */
+int ghost_set_split_k(int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GHOST_AMD_H */

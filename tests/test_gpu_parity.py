@@ -1,0 +1,303 @@
+"""GPU parity tests (MI355X): the HIP path through the C ABI against the oracle and the
+reference golden vectors.
+
+Gates
+* fp32 path: max|dY| <= 1e-3 against the reference CPU fp32 forward (BASELINE.json
+  north_star), u8 output within 1 LSB (truncation flips at integer boundaries).
+* per-op fp32 kernels: against torch fp32 CPU ops of the same op, max abs <= 1e-4
+  relative to the output scale.
+* bf16 path: bf16 storage of weights and activations cannot meet 1e-3 (SURVEY.md §7
+  "Hard parts" 1); it is gated against the fp32 oracle by mean|dY| <= 0.03 and
+  max|dY| <= 0.5 on tanh outputs in [-1, 1].
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import aei_ref
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DEV = torch.device("cuda:0")
+
+
+def gold(name):
+    return np.load(os.path.join(GOLD, name + ".npz"))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from ghost_amd import _lib
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return _lib.load()
+
+
+_WEIGHTS = {}
+
+
+def weights(backbone, nb):
+    key = (backbone, nb)
+    if key not in _WEIGHTS:
+        _WEIGHTS[key] = aei_ref.make_weights(aei_ref.param_specs(backbone, nb))
+    return _WEIGHTS[key]
+
+
+def model(backbone, nb, compute_dtype=None):
+    from ghost_amd.network import AEI_Net
+    G = AEI_Net(backbone, num_blocks=nb, c_id=512, compute_dtype=compute_dtype).eval()
+    G.load_state_dict(weights(backbone, nb))
+    return G.to(DEV)
+
+
+def stream(lib):
+    return torch.cuda.current_stream().cuda_stream
+
+
+# ----------------------------------------------------------------------------------------
+# single operators
+# ----------------------------------------------------------------------------------------
+def nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,k,s,p,H", [(32, 64, 4, 2, 1, 32), (3, 32, 4, 2, 1, 64), (64, 64, 3, 1, 1, 40),
+                                              (128, 3, 3, 1, 1, 32), (96, 200, 1, 1, 0, 9)])
+def test_conv2d_op(lib, dt, cin, cout, k, s, p, H):
+    from ghost_amd import _lib
+    from ghost_amd.network.pack import pack_conv, rup
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    x = torch.randn(2, cin, H, H, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh = torch.randn(cout, generator=g) * 0.1
+    Ho = (H + 2 * p - k) // s + 1
+    res = torch.randn(2, cout, Ho, Ho, generator=g)
+    xr = x.to(dt).float()
+    wr = w.to(dt).float()
+    ref = F.leaky_relu(F.conv2d(xr, wr, stride=s, padding=p) * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1), 0.1)
+    ref = ref + res.to(dt).float()
+    wp = pack_conv(w, dt).to(DEV)
+    xd = nhwc(x).to(dt).to(DEV)
+    rd = nhwc(res).to(dt).to(DEV)
+    y = torch.empty(2, Ho, Ho, cout, dtype=dt, device=DEV)
+    scp = torch.zeros(rup(cout, 128), device=DEV); scp[:cout] = sc.to(DEV)
+    shp = torch.zeros(rup(cout, 128), device=DEV); shp[:cout] = sh.to(DEV)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=DEV)
+    _lib.check(lib.ghost_conv2d_nhwc(_lib.gdtype(dt), xd.data_ptr(), 2, H, H, cin, cin, wp.data_ptr(), cout,
+                                     wp.shape[0], wp.shape[1], k, k, s, p, scp.data_ptr(), shp.data_ptr(), 0.1,
+                                     rd.data_ptr(), cout, 0, y.data_ptr(), cout, ws.data_ptr(), ws.numel(),
+                                     stream(lib)))
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    assert float((got - ref).abs().max()) <= tol * max(1.0, float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,H,ldy_extra,skip_add", [(64, 32, 8, 32, False), (1024, 1024, 2, 1024, False),
+                                                           (128, 64, 16, 0, True), (32, 48, 5, 16, False)])
+def test_convT_op(lib, dt, cin, cout, H, ldy_extra, skip_add):
+    """ConvT4x4/s2/p1 + BN + LReLU, written into a channel slice (unet concat) or + skip (linknet)."""
+    from ghost_amd import _lib
+    from ghost_amd.network.pack import pack_convT4x4, rup
+    g = torch.Generator().manual_seed(cin + H)
+    x = torch.randn(2, cin, H, H, generator=g)
+    w = torch.randn(cin, cout, 4, 4, generator=g) * (2.0 / (cin * 16)) ** 0.5
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh = torch.randn(cout, generator=g) * 0.1
+    skip = torch.randn(2, cout, 2 * H, 2 * H, generator=g)
+    ref = F.leaky_relu(F.conv_transpose2d(x.to(dt).float(), w.to(dt).float(), stride=2, padding=1)
+                       * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1), 0.1)
+    if skip_add:
+        ref = ref + skip.to(dt).float()
+    wp = pack_convT4x4(w, dt).to(DEV)
+    ld = cout + ldy_extra
+    y = torch.full((2, 2 * H, 2 * H, ld), 7.0, dtype=dt, device=DEV)
+    scp = torch.zeros(rup(cout, 128), device=DEV); scp[:cout] = sc.to(DEV)
+    shp = torch.zeros(rup(cout, 128), device=DEV); shp[:cout] = sh.to(DEV)
+    sk = nhwc(skip).to(dt).to(DEV)
+    ws = torch.empty(256 << 20, dtype=torch.uint8, device=DEV)
+    xd = nhwc(x).to(dt).to(DEV)
+    _lib.check(lib.ghost_conv_transpose4x4s2_nhwc(_lib.gdtype(dt), xd.data_ptr(), 2, H, H, cin, cin, wp.data_ptr(),
+                                                  cout, wp.shape[1], wp.shape[2], scp.data_ptr(), shp.data_ptr(), 0.1,
+                                                  sk.data_ptr() if skip_add else None, cout, y.data_ptr(), ld,
+                                                  ws.data_ptr(), ws.numel(), stream(lib)))
+    got = y.float().cpu()
+    assert torch.all(got[..., cout:] == 7.0), "wrote outside its channel slice"
+    got = got[..., :cout].permute(0, 3, 1, 2)
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    assert float((got - ref).abs().max()) <= tol * max(1.0, float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("split", [1, 3, 8])
+def test_conv3x3_splitk_residual_tanh(lib, split):
+    """conv3x3 with forced split-K (the low-resolution AADBlk path), residual add and tanh epilogue."""
+    from ghost_amd import _lib
+    from ghost_amd.network.pack import pack_conv
+    # drive split-K through the generic entry by a shape whose tile count is small (B*H*W = 128)
+    g = torch.Generator().manual_seed(split)
+    cin, cout, H = 512, 256, 8
+    x = torch.randn(2, cin, H, H, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * (1.0 / (cin * 9)) ** 0.5
+    res = torch.randn(2, cout, H, H, generator=g)
+    ref = torch.tanh(F.conv2d(x, w, padding=1) + res)
+    wp = pack_conv(w, torch.float32).to(DEV)
+    y = torch.empty(2, H, H, cout, device=DEV)
+    ws = torch.empty(256 << 20, dtype=torch.uint8, device=DEV)
+    xd, rd = nhwc(x).to(DEV), nhwc(res).to(DEV)
+    _lib.check(lib.ghost_set_split_k(split))
+    rc = (lib.ghost_conv2d_nhwc(_lib.F32, xd.data_ptr(), 2, H, H, cin, cin, wp.data_ptr(), cout, wp.shape[0],
+                                     wp.shape[1], 3, 3, 1, 1, None, None, 1.0, rd.data_ptr(), cout, 1, y.data_ptr(),
+                                     cout, ws.data_ptr(), ws.numel(), stream(lib)))
+    lib.ghost_set_split_k(0)
+    _lib.check(rc)
+    got = y.cpu().permute(0, 3, 1, 2)
+    assert float((got - ref).abs().max()) <= 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C,H", [(2, 64, 256), (3, 1024, 2), (2, 256, 32), (1, 32, 5)])
+def test_instnorm_stats(lib, dt, B, C, H):
+    from ghost_amd import _lib
+    g = torch.Generator().manual_seed(C + H)
+    x = (torch.randn(B, C, H, H, generator=g) * 0.3 + 5.0).to(dt)   # |mean| >> std: cancellation check
+    var, mean = torch.var_mean(x.double(), dim=(2, 3), unbiased=False)
+    rstd = 1.0 / torch.sqrt(var + 1e-5)
+    stat = torch.empty(B, C, 2, device=DEV)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=DEV)
+    xd = nhwc(x).to(DEV)
+    _lib.check(lib.ghost_instnorm_stats_nhwc(_lib.gdtype(dt), xd.data_ptr(), B, H * H, C, C, stat.data_ptr(),
+                                             ws.data_ptr(), ws.numel(), stream(lib)))
+    st = stat.cpu().double()
+    torch.testing.assert_close(st[..., 0], mean, atol=1e-5, rtol=1e-6)
+    torch.testing.assert_close(st[..., 1], rstd, atol=0, rtol=2e-4)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,H", [(64, 128), (1024, 2), (32, 64), (128, 7)])
+def test_upsample2x(lib, dt, C, H):
+    from ghost_amd import _lib
+    x = torch.randn(2, C, H, H).to(dt)
+    ref = F.interpolate(x.float(), scale_factor=2, mode="bilinear", align_corners=True)
+    y = torch.empty(2, 2 * H, 2 * H, C, dtype=dt, device=DEV)
+    xd = nhwc(x).to(DEV)
+    _lib.check(lib.ghost_upsample2x_nhwc(_lib.gdtype(dt), xd.data_ptr(), C, y.data_ptr(), C, 2, H, H, C, stream(lib)))
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    tol = 2e-6 if dt == torch.float32 else 1e-2
+    assert float((got - ref).abs().max()) <= tol * max(1.0, float(ref.abs().max()))
+
+
+def test_aad_layer_module_vs_reference_golden(lib):
+    """ghost_amd.network.AADLayer.forward (native) against the reference AADLayer outputs."""
+    from ghost_amd.network import AADLayer
+    g = gold("aad_layer_cases")
+    for i, (c_x, c_a, n) in enumerate(g["cases"].tolist()):
+        layer = AADLayer(c_x, c_a, 512)
+        specs = [(f"case{i}.{k}", tuple(v.shape), "lin_w" if k.startswith("fc") and k.endswith("weight")
+                  else ("bias" if k.endswith("bias") else "conv")) for k, v in layer.state_dict().items()]
+        w = aei_ref.make_weights(specs)
+        layer.load_state_dict({k.split(".", 1)[1]: v for k, v in w.items()})
+        layer = layer.to(DEV)
+        rg = np.random.Generator(np.random.PCG64(100 + i))
+        h = torch.from_numpy(rg.normal(0.5, 2.0, size=(2, c_x, n, n)).astype(np.float32)).to(DEV)
+        za = torch.from_numpy(rg.normal(0, 1, size=(2, c_a, n, n)).astype(np.float32)).to(DEV)
+        zi = torch.from_numpy(rg.normal(0, 1, size=(2, 512)).astype(np.float32)).to(DEV)
+        out = layer(h, za, zi).float().cpu()
+        ref = torch.from_numpy(g[f"case{i}_out"])
+        assert float((out - ref).abs().max()) <= 1e-4 * max(1.0, float(ref.abs().max())), (c_x, c_a, n)
+
+
+# ----------------------------------------------------------------------------------------
+# whole network
+# ----------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["aei_unet2_b2", "aei_linknet3_b2", "aei_unet1_b1", "aei_unet3_b1"])
+def test_forward_fp32_matches_reference(lib, name):
+    g = gold(name)
+    backbone, nb, B = str(g["backbone"]), int(g["num_blocks"]), int(g["batch"])
+    G = model(backbone, nb)
+    xt, z = aei_ref.make_inputs(B, int(g["seed"]))
+    Y, attr = G(xt.to(DEV), z.to(DEV))
+    torch.cuda.synchronize()
+    assert Y.shape == (B, 3, 256, 256) and Y.dtype == torch.float32
+    dy = float((Y.cpu() - torch.from_numpy(g["Y"])).abs().max())
+    assert dy <= 1e-3, f"max|dY| = {dy}"
+    for i, a in enumerate(attr, 1):
+        assert tuple(a.shape) == tuple(g[f"attr{i}_shape"])
+        flat = a.contiguous().reshape(-1)      # NCHW order, as the reference stored it
+        samp = flat.cpu()[torch.from_numpy(g[f"attr{i}_idx"])]
+        assert float((samp - torch.from_numpy(g[f"attr{i}_sample"])).abs().max()) <= 1e-4
+
+
+@pytest.mark.parametrize("name", ["aei_unet2_b2", "aei_linknet3_b2"])
+def test_swap_u8_pipeline_matches_reference(lib, name):
+    """u8 crops -> normalise -> AEI_Net -> BGR uint8, fp32 path, against faceshifter_batch's output."""
+    g = gold(name)
+    backbone, nb, B = str(g["backbone"]), int(g["num_blocks"]), int(g["batch"])
+    G = model(backbone, nb)
+    _, z = aei_ref.make_inputs(B, int(g["seed"]))
+    crops = torch.from_numpy(aei_ref.make_u8_crops(B, int(g["crops_seed"]))).to(DEV)
+    out = G.swap_u8(crops, z[:1].to(DEV)).cpu().numpy()
+    diff = np.abs(out.astype(np.int16) - g["U8"].astype(np.int16))
+    assert diff.max() <= 1 and (diff > 0).mean() < 1e-3
+    # the faceshifter_batch drop-in (host-side API) gives the same bytes
+    from ghost_amd.inference import faceshifter_batch, transform_target_to_torch
+    tgt = transform_target_to_torch(aei_ref.make_u8_crops(B, int(g["crops_seed"])), half=False)
+    out2 = faceshifter_batch(z[:1].to(DEV), tgt, G)
+    d2 = np.abs(out2.astype(np.int16) - g["U8"].astype(np.int16))
+    assert d2.max() <= 1 and (d2 > 0).mean() < 1e-3
+
+
+def test_forward_bf16_close_to_oracle(lib):
+    g = gold("aei_unet2_b2")
+    G = model("unet", 2, compute_dtype=torch.bfloat16)
+    xt, z = aei_ref.make_inputs(2, int(g["seed"]))
+    Y, attr = G(xt.to(DEV), z.to(DEV))
+    d = (Y.float().cpu() - torch.from_numpy(g["Y"])).abs()
+    assert Y.dtype == torch.bfloat16
+    assert float(d.mean()) <= 0.03 and float(d.max()) <= 0.5, (float(d.mean()), float(d.max()))
+
+
+def test_full_batch64_bf16_properties_and_fp32_rows(lib):
+    """B=64 (the bench configuration): batch independence and oracle parity on sampled rows."""
+    G32 = model("unet", 2)
+    xt, z = aei_ref.make_inputs(64, 11)
+    Y, _ = G32(xt.to(DEV), z.to(DEV))
+    Ycpu = Y.cpu()
+    p = weights("unet", 2)
+    for r in (0, 37, 63):
+        yr, _ = aei_ref.aei_forward(p, xt[r:r + 1], z[r:r + 1])
+        assert float((Ycpu[r:r + 1] - yr).abs().max()) <= 1e-3, r
+    Gb = model("unet", 2, compute_dtype=torch.bfloat16)
+    Yb, _ = Gb(xt.to(DEV), z.to(DEV))
+    Y1, _ = Gb(xt[5:6].to(DEV), z[5:6].to(DEV))
+    # split-K / tile choice depends on B; rounding may differ but not the result
+    assert float((Yb[5:6].float() - Y1.float()).abs().max()) <= 0.05
+    assert torch.isfinite(Yb.float()).all()
+    assert float((Yb.float().cpu() - Ycpu).abs().mean()) <= 0.03
+
+
+def test_get_attr_matches_forward_attr(lib):
+    G = model("unet", 2)
+    xt, z = aei_ref.make_inputs(2, 3)
+    _, attr = G(xt.to(DEV), z.to(DEV))
+    attr2 = G.get_attr(xt.to(DEV))
+    for a, b in zip(attr, attr2):
+        assert torch.equal(a, b)
+
+
+def test_strided_half_input_view(lib):
+    """core.py:24 hands over a permuted (channels-last) fp16 view; it must be read as-is."""
+    G = model("unet", 2)
+    crops = aei_ref.make_u8_crops(2, 5)
+    t = torch.from_numpy(crops).to(DEV)[:, :, :, [2, 1, 0]] / 255.0
+    t = ((t.half() - 0.5) / 0.5).permute(0, 3, 1, 2)          # non-contiguous fp16 view
+    assert not t.is_contiguous()
+    _, z = aei_ref.make_inputs(2, 5)
+    Y1, _ = G(t, z.to(DEV))
+    Y2, _ = G(t.contiguous().float(), z.to(DEV))
+    assert torch.equal(Y1, Y2)

@@ -1,0 +1,163 @@
+"""CPU tests of the host side: library exports, runtime plan / slot naming, weight packing.
+
+No GPU compute here: the C ABI is exercised only through calls that touch no device
+(handle creation, slot binding with dummy addresses, dry-run workspace sizing).  The
+packed layouts are validated by replaying the kernels' index arithmetic with torch on
+CPU and comparing against torch's own conv ops.
+"""
+import ctypes as C
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ghost_amd import _lib
+from ghost_amd.network import pack
+from oracle import aei_ref
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from ghost_amd import build
+    build.build(verbose=False)
+    return _lib.load()
+
+
+def test_library_exports_every_header_symbol(lib):
+    declared = _lib.header_symbols()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(declared) == set(_lib._SIGS), "ctypes signature table out of sync with include/ghost_amd.h"
+
+
+@pytest.mark.parametrize("backbone,nb", [("unet", 2), ("linknet", 3), ("unet", 1), ("unet", 3)])
+def test_pack_slots_match_runtime_plan(lib, backbone, nb):
+    specs = aei_ref.param_specs(backbone, nb)
+    sd = aei_ref.make_weights(specs)
+    slots = pack.pack_all(sd, backbone, nb, 512, torch.bfloat16)
+    h = C.c_void_p()
+    _lib.check(lib.ghost_aei_create(backbone.encode(), nb, 512, _lib.BF16, C.byref(h)))
+    try:
+        n_before = lib.ghost_aei_missing(h)
+        assert n_before == len(slots)
+        for i, (name, t) in enumerate(slots.items()):
+            _lib.check(lib.ghost_aei_bind(h, name.encode(), 0x100000 + 256 * i, t.numel()), name)
+        assert lib.ghost_aei_missing(h) == 0
+        assert lib.ghost_aei_bind(h, b"no.such.slot", 0x1000, 1) != 0
+        # the identity table rows equal 2*sum(c_x) over the plan
+        ntot = sum(2 * sd[f"{pre}.fc1.weight"].shape[0] for _, pre in pack.aad_plan(backbone, nb))
+        assert slots["gen.id.w"].shape[0] == pack.rup(ntot, 128)
+        for B in (1, 8, 64):
+            assert lib.ghost_aei_workspace_bytes(h, B) > 0
+            assert lib.ghost_aei_swap_workspace_bytes(h, B) > lib.ghost_aei_workspace_bytes(h, B)
+    finally:
+        lib.ghost_aei_destroy(h)
+
+
+def test_create_rejects_bad_arguments(lib):
+    h = C.c_void_p()
+    assert lib.ghost_aei_create(b"resnet", 2, 512, 0, C.byref(h)) != 0
+    assert b"backbone" in lib.ghost_last_error()
+    assert lib.ghost_aei_create(b"unet", 0, 512, 0, C.byref(h)) != 0
+    assert lib.ghost_aei_create(b"unet", 2, 512, 7, C.byref(h)) != 0
+
+
+def _gemm_conv(x, wp, cout, k, stride, pad):
+    """Replay the implicit GEMM on CPU: rows = output pixels, K = (ky, kx, c)."""
+    B, Cin, H, W = x.shape
+    cols = F.unfold(x, k, padding=pad, stride=stride)          # [B, Cin*k*k, L] with (c, ky, kx) order
+    L = cols.shape[-1]
+    cols = cols.reshape(B, Cin, k * k, L).permute(0, 3, 2, 1).reshape(B, L, k * k * Cin)  # (ky,kx,c)
+    y = cols @ wp[:cout, :k * k * Cin].t()
+    Ho = (H + 2 * pad - k) // stride + 1
+    return y.reshape(B, Ho, -1, cout).permute(0, 3, 1, 2)
+
+
+def test_pack_conv_layout():
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 32, 12, 12, generator=g, dtype=torch.float64)
+    for (co, k, s, p) in [(40, 4, 2, 1), (24, 3, 1, 1), (16, 1, 1, 0)]:
+        w = torch.randn(co, 32, k, k, generator=g, dtype=torch.float64)
+        wp = pack.pack_conv(w, torch.float64)
+        assert wp.shape == (pack.rup(co, 128), pack.rup(32 * k * k, 32))
+        torch.testing.assert_close(_gemm_conv(x, wp, co, k, s, p), F.conv2d(x, w, stride=s, padding=p))
+
+
+def test_pack_convT_subpixel_layout():
+    g = torch.Generator().manual_seed(1)
+    ci, co, H = 16, 24, 5
+    x = torch.randn(2, ci, H, H, generator=g, dtype=torch.float64)
+    w = torch.randn(ci, co, 4, 4, generator=g, dtype=torch.float64)
+    wp = pack.pack_convT4x4(w, torch.float64)
+    ref = F.conv_transpose2d(x, w, stride=2, padding=1)
+    out = torch.zeros_like(ref)
+    xp = F.pad(x, (1, 1, 1, 1))
+    for py in range(2):
+        for px in range(2):
+            acc = torch.zeros(2, co, H, H, dtype=torch.float64)
+            for ty in range(2):
+                for tx in range(2):
+                    dy, dx = py - ty, px - tx           # input offset = parity - tap (kernel tbase/tsign)
+                    patch = xp[:, :, 1 + dy:1 + dy + H, 1 + dx:1 + dx + H]
+                    wt = wp[2 * py + px, :co, (ty * 2 + tx) * ci:(ty * 2 + tx + 1) * ci]
+                    acc += torch.einsum("bchw,oc->bohw", patch, wt)
+            out[:, :, py::2, px::2] = acc
+    torch.testing.assert_close(out, ref)
+
+
+def test_pack_aad_interleave_and_bn_fold():
+    sd = aei_ref.make_weights(aei_ref.param_specs("unet", 2))
+    pre = "generator.AADBlk6.add_blocks.0"
+    p = pack.pack_aad(sd, pre, torch.float32)
+    c = sd[f"{pre}.conv1.weight"].shape[0]
+    for col in range(2 * c):
+        grp, r = divmod(col, 16)
+        ch = (grp // 2) * 16 + r
+        src = "conv1" if grp % 2 == 0 else "conv2"
+        ca = sd[f"{pre}.conv1.weight"].shape[1]
+        torch.testing.assert_close(p["gbw"][col, :ca],
+                                   sd[f"{pre}.{src}.weight"][ch, :, 0, 0])
+        assert float(p["gbb"][col]) == float(sd[f"{pre}.{src}.bias"][ch])
+    s, t = pack.bn_fold(sd, "encoder.conv3.1", 128)
+    x = torch.randn(4, 128, 3, 3)
+    bn = F.batch_norm(x, sd["encoder.conv3.1.running_mean"], sd["encoder.conv3.1.running_var"],
+                      sd["encoder.conv3.1.weight"], sd["encoder.conv3.1.bias"], False, 0.0, 1e-5)
+    torch.testing.assert_close(x * s.view(1, -1, 1, 1) + t.view(1, -1, 1, 1), bn, atol=1e-5, rtol=1e-5)
+
+
+def test_pack_up1_and_identity_table():
+    sd = aei_ref.make_weights(aei_ref.param_specs("unet", 2))
+    slots = pack.pack_all(sd, "unet", 2, 512, torch.float32)
+    z = torch.randn(3, 512)
+    ref = F.conv_transpose2d(z.reshape(3, 512, 1, 1), sd["generator.up1.weight"], sd["generator.up1.bias"])
+    got = (z @ slots["gen.up1.w"][:, :512].t() + slots["gen.up1.shift"]).reshape(3, 2, 2, 1024).permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-5)
+    tab = z @ slots["gen.id.w"][:, :512].t() + slots["gen.id.shift"]
+    off = 0
+    for _, pre in pack.aad_plan("unet", 2):
+        c = sd[f"{pre}.fc1.weight"].shape[0]
+        torch.testing.assert_close(tab[:, off:off + c], F.linear(z, sd[f"{pre}.fc1.weight"], sd[f"{pre}.fc1.bias"]),
+                                   atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(tab[:, off + c:off + 2 * c],
+                                   F.linear(z, sd[f"{pre}.fc2.weight"], sd[f"{pre}.fc2.bias"]), atol=1e-5, rtol=1e-5)
+        off += 2 * c
+
+
+def test_module_state_dict_matches_reference_keys():
+    from ghost_amd.network import AEI_Net
+    for backbone, nb in [("unet", 2), ("linknet", 3), ("unet", 1)]:
+        G = AEI_Net(backbone, num_blocks=nb, c_id=512)
+        mine = [(k, tuple(v.shape)) for k, v in G.state_dict().items()]
+        ref = [(k, tuple(s)) for k, s, _ in aei_ref.param_specs(backbone, nb)]
+        assert mine == ref
+        G.load_state_dict(aei_ref.make_weights(aei_ref.param_specs(backbone, nb)), strict=True)
+
+
+def test_product_refuses_cpu_tensors():
+    from ghost_amd.network import AEI_Net
+    G = AEI_Net("unet", num_blocks=2, c_id=512).eval()
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        G(torch.zeros(1, 3, 256, 256), torch.zeros(1, 512))
+    with pytest.raises(NotImplementedError):
+        G.generator.AADBlk1(torch.zeros(1), None, None)
