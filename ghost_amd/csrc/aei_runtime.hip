@@ -108,8 +108,14 @@ struct Ctx {
     }
   }
   const void* W(const std::string& name) {
-    if (dry) return reinterpret_cast<const void*>(uintptr_t(0x1000));  // sizing needs no weights
     auto it = h->slots.find(name);
+    if (dry) {  // sizing needs no weights, but every slot the plan reads must be declared
+      if (it == h->slots.end() && rc == 0) {
+        rc = GHOST_EINVAL;
+        where = "plan reads undeclared slot " + name;
+      }
+      return reinterpret_cast<const void*>(uintptr_t(0x1000));
+    }
     if (it == h->slots.end() || !it->second) {
       if (rc == 0) {
         rc = GHOST_ENOTREADY;
@@ -356,7 +362,7 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
         aad(c, an, x, cin, stat_x, za, Ca, Ca, B, n, cin, id_off, idgb, a, cin);
         id_off += 2 * cin;
         void* xn = c.alloc(P * cin * es);
-        conv3x3(c, cn, a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr);
+        conv3x3(c, cn + ".w", a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr);
         float* st = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
         run_stats(c, xn, cin, B, n * n, cin, st);
         x = xn;
@@ -365,7 +371,7 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
         void* a = c.alloc(P * cin * es);
         aad(c, an, x, cin, stat_x, za, Ca, Ca, B, n, cin, id_off, idgb, a, cin);
         id_off += 2 * cin;
-        conv3x3(c, cn, a, cin, cin, B, n, cout, y, ldy, m, cin, last_k, last_k ? u8 : nullptr);
+        conv3x3(c, cn + ".w", a, cin, cin, B, n, cout, y, ldy, m, cin, last_k, last_k ? u8 : nullptr);
       } else {
         // x-branch and h'-branch share the output: conv(cat(a_x, a_h), [W_x | W_h]) = x + h'
         void* cat = c.alloc(P * 2 * cin * es);
@@ -373,7 +379,7 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
         id_off += 2 * cin;
         aad(c, blk + ".aadlast", m, cin, stat_m, za, Ca, Ca, B, n, cin, id_off, idgb,
             (char*)cat + (size_t)cin * es, 2 * cin);
-        conv3x3(c, cn, cat, 2 * cin, 2 * cin, B, n, cout, y, ldy, nullptr, 0, last_k, last_k ? u8 : nullptr);
+        conv3x3(c, cn + ".w", cat, 2 * cin, 2 * cin, B, n, cout, y, ldy, nullptr, 0, last_k, last_k ? u8 : nullptr);
       }
     }
     if (cin != cout) id_off += 2 * cin;  // last_add_block's AADLayer

@@ -169,7 +169,8 @@ int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* 
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ void __launch_bounds__(256)
-upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, int B, int H, int W, int C) {
+upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, int B, int H, int W, int C, float sh,
+                  float sw) {
   constexpr int VEC = Vec16<T>::N;
   const int nch = C / VEC;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
@@ -181,8 +182,6 @@ upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, 
   const int ox = (int)(op % Wo);
   const int oy = (int)((op / Wo) % Ho);
   const int b = (int)(op / ((long)Wo * Ho));
-  const float sh = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
-  const float sw = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
   const float ry = sh * (float)oy, rx = sw * (float)ox;
   const int y0 = (int)ry, x0 = (int)rx;
   const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
@@ -204,10 +203,15 @@ int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, i
   if (C % vec || ldx % vec || ldy % vec || (uintptr_t)x % 16 || (uintptr_t)y % 16) return -1;
   const long total = (long)B * 4 * H * W * (C / vec);
   dim3 grid((unsigned)((total + 255) / 256));
+  // source scale (in-1)/(out-1) rounded once on the host, as PyTorch's area_pixel_compute_scale
+  const float sh = H > 0 ? (float)(H - 1) / (float)(2 * H - 1) : 0.f;
+  const float sw = W > 0 ? (float)(W - 1) / (float)(2 * W - 1) : 0.f;
   if (dt == GHOST_F32)
-    hipLaunchKernelGGL(upsample2x_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, B, H, W, C);
+    hipLaunchKernelGGL(upsample2x_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, B, H, W, C,
+                       sh, sw);
   else if (dt == GHOST_BF16)
-    hipLaunchKernelGGL(upsample2x_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, B, H, W, C);
+    hipLaunchKernelGGL(upsample2x_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, B, H, W, C,
+                       sh, sw);
   else
     return -1;
   return (int)hipGetLastError();
