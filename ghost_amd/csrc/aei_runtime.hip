@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/ghost_amd.h"
+#include "aad_fused.h"
 #include "conv_igemm.h"
 #include "ghost_common.h"
 #include "ops.h"
@@ -279,21 +280,40 @@ struct GenShared {
 void aad(Ctx& c, const std::string& name, const void* hin, int ldh, const float* stat, const void* za, int lda,
          int Ca, int B, int n, int C, int id_off, const float* idgb, void* out, int ldo) {
   ghost_aei* h = c.h;
+  const double P = (double)B * n * n;
+  const double bytes = P * (2.0 * C + Ca) * (double)h->esz;   // |h_in| + |z_attr| + |out|
+  const double flops = 2.0 * P * 2.0 * C * Ca;
+  const void* gbw = c.W(name + ".gbw");
+  const float* gbb = (const float*)c.W(name + ".gbb");
+  const float* wh = (const float*)c.W(name + ".wh");
+  const float* bh = (const float*)c.W(name + ".bh");
+  if (aad_fused_supported(h->dt, B, n * n, C, Ca, lda, ldh, ldo)) {
+    if (!c.ok() || c.dry) return;
+    const bool big = n == 256;
+    int e_all = c.prof_begin(0);
+    int e_big = big ? c.prof_begin(1) : -1;
+    c.check(aad_fused(h->dt, za, lda, Ca, gbw, rup(Ca, 32), gbb, hin, ldh, stat, wh, bh, idgb + id_off, h->id_total,
+                      out, ldo, B, n * n, C, 0.0f, c.s),
+            "aad_fused");
+    if (e_big >= 0) c.prof_end(1, e_big, bytes, flops);
+    if (e_all >= 0) c.prof_end(0, e_all, bytes, flops);
+    return;
+  }
   float* mask = (float*)c.alloc((size_t)B * n * n * sizeof(float));
-  run_mask(c, hin, ldh, B, n * n, C, stat, (const float*)c.W(name + ".wh"), (const float*)c.W(name + ".bh"), mask);
+  run_mask(c, hin, ldh, B, n * n, C, stat, wh, bh, mask);
   ConvDesc d;
   d.ti = d.to = h->dt;
   d.x = za; d.B = B; d.Hi = n; d.Wi = n; d.Cin = Ca; d.ldx = lda;
-  d.w = c.W(name + ".gbw");
+  d.w = gbw;
   d.N = 2 * C; d.Npad = rup(2 * C, 128); d.Kpad = rup(Ca, 32);
   d.kind = CONV_FWD; d.kh = d.kw = 1; d.stride = 1; d.pad = 0;
   d.y = out; d.ldy = ldo;
-  d.shift = (const float*)c.W(name + ".gbb");
+  d.shift = gbb;
   d.slope = 0.0f;  // the ReLU that follows every AADLayer in AddBlocksSequential
   d.epi = EPI_AAD;
   d.hin = hin; d.ldh = ldh; d.stat = stat;
   d.idgb = idgb ? idgb + id_off : nullptr; d.id_ld = h->id_total; d.mask = mask; d.C_aad = C;
-  run_conv(c, d, 0, 1, 2.0 * B * n * n * 2.0 * C * Ca);
+  run_conv(c, d, 0, 1, flops);
 }
 
 void conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, int B, int n, int Cout, void* y,
@@ -734,6 +754,11 @@ extern "C" int ghost_aad_layer_nhwc(int dtype, const void* h_in, int ldh, const 
   char* scratch = base + stat_b + mask_b;
   int rc = in_stats(dtype, h_in, ldh, B, HW, C, stat, scratch, sc, s);
   if (rc) return fail(rc, "aad_layer: in_stats failed");
+  if (aad_fused_supported(dtype, B, HW, C, Ca, lda, ldh, ldo)) {
+    rc = aad_fused(dtype, z_attr, lda, Ca, gbw_packed, Kpad, gbb, h_in, ldh, stat, wh, bh, idgb, id_ld, out, ldo, B, HW, C,
+                   slope, s);
+    return rc ? fail(rc, "aad_layer: fused kernel failed") : 0;
+  }
   rc = aad_mask(dtype, h_in, ldh, B, HW, C, stat, wh, bh, mask, s);
   if (rc) return fail(rc, "aad_layer: mask failed");
   d.stat = stat; d.mask = mask;

@@ -311,3 +311,30 @@ def test_strided_half_input_view(lib):
     Y1, _ = G(t, z.to(DEV))
     Y2, _ = G(t.contiguous().float(), z.to(DEV))
     assert torch.equal(Y1, Y2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("c_x,c_a,n,B", [(64, 64, 256, 2), (128, 128, 128, 2), (256, 256, 64, 8), (64, 32, 128, 4)])
+def test_aad_layer_fused_path_vs_oracle(lib, dt, c_x, c_a, n, B):
+    """The fused AAD kernel (mask pre-pass + MFMA gamma/beta + LDS-staged blend) at pipeline sizes."""
+    from ghost_amd.network import AADLayer
+    layer = AADLayer(c_x, c_a, 512)
+    specs = [(f"fz.{k}", tuple(v.shape), "lin_w" if k.startswith("fc") and k.endswith("weight")
+              else ("bias" if k.endswith("bias") else "conv")) for k, v in layer.state_dict().items()]
+    w = aei_ref.make_weights(specs)
+    sd = {k.split(".", 1)[1]: v for k, v in w.items()}
+    layer.load_state_dict(sd)
+    if dt == torch.bfloat16:
+        layer = layer.to(torch.bfloat16)
+    layer = layer.to(DEV)
+    g = torch.Generator().manual_seed(c_x + n)
+    h = torch.randn(B, c_x, n, n, generator=g) * 1.5 + 0.7
+    za = torch.randn(B, c_a, n, n, generator=g)
+    zi = torch.randn(B, 512, generator=g)
+    out = layer(h.to(DEV), za.to(DEV), zi.to(DEV)).float().cpu()
+    p = {f"l.{k}": v.to(dt).float() for k, v in sd.items()}      # the module rounds its params to dt
+    h, za = h.to(dt).float(), za.to(dt).float()
+    ref = aei_ref.aad_layer(h, za, zi, p, "l")
+    scale = max(1.0, float(ref.abs().max()))
+    err = float((out - ref).abs().max())
+    assert err <= (1e-4 if dt == torch.float32 else 4e-2) * scale, err
