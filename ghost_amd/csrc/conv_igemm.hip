@@ -82,6 +82,12 @@ GHOST_DEV float epi_aad(const ConvArgs& a, float ga, float ba, int c, long m) {
   return out > 0.f ? out : out * a.slope;
 }
 
+GHOST_DEV int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
 GHOST_DEV long out_pixel(const ConvArgs& a, long m, int py, int px) {
   if (!a.deconv) return m;
   const int HW = a.Ho * a.Wo;
@@ -112,8 +118,12 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
   __shared__ __attribute__((aligned(16))) TI smem[2 * (BM + BN) * LDR];
 
   const int tid = threadIdx.x;
-  const int nt = blockIdx.x % a.nNt;
-  const int mt = blockIdx.x / a.nNt;
+  // XCD-aware remap: workgroups are dealt round-robin over the 8 XCDs; give each XCD a
+  // contiguous run of tiles so the 3x3/4x4 halo rows a tile shares with its neighbours
+  // are re-read from that XCD's L2 instead of HBM (cdna_hip_programming.md T1, bijective form)
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = tile % a.nNt;
+  const int mt = tile / a.nNt;
   const int m0 = mt * BM, n0 = nt * BN;
   const int split = blockIdx.y;
   const int par = blockIdx.z;

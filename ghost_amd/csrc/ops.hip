@@ -182,8 +182,10 @@ upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, 
   const int ox = (int)(op % Wo);
   const int oy = (int)((op / Wo) % Ho);
   const int b = (int)(op / ((long)Wo * Ho));
-  // __fmul_rn: keep the rounded source coordinate (no fma contraction into the lambda), as PyTorch
-  const float ry = __fmul_rn(sh, (float)oy), rx = __fmul_rn(sw, (float)ox);
+  // keep the rounded source coordinate, as PyTorch does: the empty asm stops hipcc from
+  // re-forming sh*oy - y0 as one fma (which would skip the product's rounding)
+  float ry = sh * (float)oy, rx = sw * (float)ox;
+  asm volatile("" : "+v"(ry), "+v"(rx));
   const int y0 = (int)ry, x0 = (int)rx;
   const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
   const float ly1 = ry - (float)y0, ly0 = 1.f - ly1;
