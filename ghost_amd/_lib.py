@@ -55,6 +55,8 @@ _SIGS = {
     "ghost_nhwc_to_nchw": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp]),
     "ghost_crops_to_input_nhwc": (i32, [vp, i64, i32, i32, i32, i32, vp, vp]),
     "ghost_set_split_k": (i32, [i32]),
+    "ghost_conv3x3_narrow_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, vp, i32, i32, vp, i32, vp,
+                                        vp]),
 }
 
 

@@ -16,6 +16,7 @@
 #include "../../include/ghost_amd.h"
 #include "aad_fused.h"
 #include "conv_igemm.h"
+#include "conv_narrow.h"
 #include "ghost_common.h"
 #include "ops.h"
 
@@ -318,6 +319,18 @@ void aad(Ctx& c, const std::string& name, const void* hin, int ldh, const float*
 
 void conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, int B, int n, int Cout, void* y,
              int ldy, const void* res, int ldres, int tanh_out, uint8_t* u8) {
+  const double flops = 2.0 * B * n * n * Cout * 9.0 * Cin;
+  if (Cout <= 3 && conv3x3_narrow_supported(c.h->dt, n, n, Cin, ldx, Cout)) {
+    const void* wn = c.W(wname + "n");   // "...conv{i}.w" + "n" = the narrow layout slot
+    if (!c.ok() || c.dry) return;
+    int e_all = c.prof_begin(2);
+    int e_big = n == 256 ? c.prof_begin(3) : -1;
+    c.check(conv3x3_narrow(c.h->dt, x, B, n, n, Cin, ldx, wn, rup(Cin, 32), Cout, res, ldres, tanh_out, y, ldy, u8, c.s),
+            "conv3x3_narrow");
+    if (e_big >= 0) c.prof_end(3, e_big, 0, flops);
+    if (e_all >= 0) c.prof_end(2, e_all, 0, flops);
+    return;
+  }
   ConvDesc d;
   d.ti = d.to = c.h->dt;
   d.x = x; d.B = B; d.Hi = n; d.Wi = n; d.Cin = Cin; d.ldx = ldx;
@@ -327,7 +340,7 @@ void conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, 
   d.y = y; d.ldy = ldy;
   d.res = res; d.ldres = ldres;
   d.tanh_out = tanh_out; d.u8 = u8;
-  run_conv(c, d, 2, 3, 2.0 * B * n * n * Cout * 9.0 * Cin);
+  run_conv(c, d, 2, 3, flops);
 }
 
 void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, void* y_out, uint8_t* u8) {
@@ -439,6 +452,7 @@ void declare_slots(ghost_aei* h) {
       const std::string an = blk + ".aad" + std::to_string(i);
       add(an + ".gbw"); add(an + ".gbb"); add(an + ".wh"); add(an + ".bh");
       add(blk + ".conv" + std::to_string(i) + ".w");
+      if (i == h->nb - 1 && cout <= 3) add(blk + ".conv" + std::to_string(i) + ".wn");
       h->id_total += 2 * cin;
     }
     if (cin != cout) {
@@ -782,4 +796,12 @@ extern "C" int ghost_crops_to_input_nhwc(const uint8_t* crops, int64_t crop_batc
                                          void* y, void* stream) {
   int rc = crops_u8_to_input(crops, crop_batch_stride, B, H, W, dtype, y, (hipStream_t)stream);
   return rc ? fail(rc, "crops_to_input failed") : 0;
+}
+
+extern "C" int ghost_conv3x3_narrow_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx,
+                                         const void* w_narrow, int Kpad, int Cout, const void* res, int ldres,
+                                         int tanh_out, void* y, int ldy, uint8_t* u8, void* stream) {
+  int rc = conv3x3_narrow(dtype, x, B, H, W, Cin, ldx, w_narrow, Kpad, Cout, res, ldres, tanh_out, y, ldy, u8,
+                          (hipStream_t)stream);
+  return rc ? fail(rc, "conv3x3_narrow failed (H % 8, W % 32, Cin % 32 and Cout <= 3 required)") : 0;
 }

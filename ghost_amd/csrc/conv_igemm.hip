@@ -8,6 +8,9 @@
 // at the borders; when Cin % 32 == 0 a 32-deep K slice lies inside one tap, so every
 // row is one contiguous 64 B (bf16) / 128 B (fp32) run loaded as 16 B vectors.
 // Staging: global -> registers -> LDS, double-buffered, one barrier per K step.
+#include <cstdio>
+#include <cstdlib>
+
 #include "conv_igemm.h"
 #include "ghost_common.h"
 
@@ -102,18 +105,23 @@ GHOST_DEV long out_pixel(const ConvArgs& a, long m, int py, int px) {
 // ---------------------------------------------------------------------------
 enum { KEPI_STD = 0, KEPI_AAD = 1, KEPI_SPLIT = 2 };
 
-template <typename TI, typename TO, int BM, int BN, int EPI, bool FAST>
+// wave layout: 4 waves as 2x2 (BM <= 128, BN >= 32) or 4x1 (BM = 256 or a 16-wide N tile)
+template <int BM, int BN> struct WaveGrid { static constexpr int WN = (BM <= 128 && BN >= 32) ? 2 : 1, WM = 4 / WN; };
+
+template <typename TI, typename TO, int BM, int BN, int BK, int EPI, bool FAST>
 __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
-  constexpr int BK = 32;
   constexpr int VEC = Vec16<TI>::N;
   constexpr int CPR = BK / VEC;   // 16 B chunks per tile row
   constexpr int RPP = 256 / CPR;  // tile rows covered per load pass
   constexpr int AP = BM / RPP;
   constexpr int BP = (BN + RPP - 1) / RPP;   // BN may be smaller than one pass
   constexpr int LDR = BK + VEC;   // padded LDS row, elements
-  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int WM = WaveGrid<BM, BN>::WM, WN = WaveGrid<BM, BN>::WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(TM >= 1 && TN >= 1 && BK % 32 == 0, "tile shape");
   static_assert(BM % RPP == 0 && (BN % RPP == 0 || RPP % BN == 0), "tile/load mismatch");
-  static_assert(EPI != KEPI_AAD || (TN % 2 == 0), "AAD epilogue needs gamma/beta tile pairs");
+  static_assert(EPI != KEPI_AAD || (TN % 2 == 0 && WTN % 32 == 0), "AAD epilogue needs gamma/beta tile pairs");
 
   __shared__ __attribute__((aligned(16))) TI smem[2 * (BM + BN) * LDR];
 
@@ -135,41 +143,59 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
   const int kt0 = split * a.kt_per_split;
   const int kt1 = min(nk, kt0 + a.kt_per_split);
 
-  // per-thread rows of the A tile
+  // per-thread rows of the A tile, decoded once per tile: element offset of the tap-origin
+  // pixel and a bitmask of the taps that land inside the image (the rest read as the zero
+  // padding).  Per K step only a scalar tap offset and one bit test per row remain.
   const int crow = tid / CPR, cch = tid % CPR;
   const int HoWo = a.Ho * a.Wo;
-  int a_base[AP], a_iy[AP], a_ix[AP];
-  bool a_ok[AP];
+  const int tby = a.deconv ? py : a.tbase;
+  const int tbx = a.deconv ? px : a.tbase;
+  const int nty = a.K / (a.Cin * a.ntx);
+  long a_off[AP];
+  unsigned a_mask[AP];
 #pragma unroll
   for (int p = 0; p < AP; ++p) {
     const int m = m0 + crow + p * RPP;
-    a_ok[p] = m < a.M;
-    const int mm = a_ok[p] ? m : 0;
-    const int b = mm / HoWo;
-    const int r = mm - b * HoWo;
-    const int oy = r / a.Wo, ox = r - oy * a.Wo;
-    a_base[p] = b * a.Hi * a.Wi;
-    a_iy[p] = oy * a.stride;
-    a_ix[p] = ox * a.stride;
+    a_off[p] = 0;
+    a_mask[p] = 0u;
+    if (m < a.M) {
+      const int b = m / HoWo;
+      const int r = m - b * HoWo;
+      const int oy = r / a.Wo, ox = r - oy * a.Wo;
+      const int iyb = oy * a.stride + tby, ixb = ox * a.stride + tbx;
+      a_off[p] = ((long)(b * a.Hi + iyb) * a.Wi + ixb) * a.ldx;
+      unsigned mk = 0u;
+      for (int ty = 0; ty < nty; ++ty) {
+        const int iy = iyb + a.tsign * ty;
+        if (iy < 0 || iy >= a.Hi) continue;
+        for (int tx = 0; tx < a.ntx; ++tx) {
+          const int ix = ixb + a.tsign * tx;
+          if (ix >= 0 && ix < a.Wi) mk |= 1u << (ty * a.ntx + tx);
+        }
+      }
+      a_mask[p] = mk;
+    }
   }
-  const int tby = a.deconv ? py : a.tbase;
-  const int tbx = a.deconv ? px : a.tbase;
+  const TI* wrow[BP];
+#pragma unroll
+  for (int p = 0; p < BP; ++p) {
+    // BN < RPP: the surplus threads re-load an in-tile row and do not store it
+    const int n = n0 + (BN >= RPP ? crow + p * RPP : crow % BN);
+    wrow[p] = w + (long)n * a.Kpad + cch * VEC;
+  }
 
   u32x4 ra[AP], rb[BP];
 
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK;
     if constexpr (FAST) {
-      const int tap = k0 / a.Cin;
-      const int c = k0 - tap * a.Cin + cch * VEC;
+      const int tap = k0 / a.Cin;                       // the BK slice lies inside one tap
       const int ty = tap / a.ntx, tx = tap - ty * a.ntx;
-      const int dy = tby + a.tsign * ty, dx = tbx + a.tsign * tx;
+      const long toff = ((long)a.tsign * ty * a.Wi + a.tsign * tx) * a.ldx + (k0 - tap * a.Cin) + cch * VEC;
 #pragma unroll
       for (int p = 0; p < AP; ++p) {
-        const int iy = a_iy[p] + dy, ix = a_ix[p] + dx;
-        const bool ok = a_ok[p] && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
-        if (ok)
-          ra[p] = *reinterpret_cast<const u32x4*>(x + (long)(a_base[p] + iy * a.Wi + ix) * a.ldx + c);
+        if ((a_mask[p] >> tap) & 1u)
+          ra[p] = *reinterpret_cast<const u32x4*>(x + a_off[p] + toff);
         else
           ra[p] = u32x4{0u, 0u, 0u, 0u};
       }
@@ -181,24 +207,19 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
         for (int j = 0; j < VEC; ++j) {
           const int k = k0 + cch * VEC + j;
           float v = 0.f;
-          if (a_ok[p] && k < a.K) {
+          if (k < a.K) {
             const int tap = k / a.Cin;
             const int c = k - tap * a.Cin;
             const int ty = tap / a.ntx, tx = tap - ty * a.ntx;
-            const int iy = a_iy[p] + tby + a.tsign * ty, ix = a_ix[p] + tbx + a.tsign * tx;
-            if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi)
-              v = to_f(x[(long)(a_base[p] + iy * a.Wi + ix) * a.ldx + c]);
+            if ((a_mask[p] >> tap) & 1u)
+              v = to_f(x[a_off[p] + ((long)a.tsign * ty * a.Wi + a.tsign * tx) * a.ldx + c]);
           }
           e[j] = from_f<TI>(v);
         }
       }
     }
 #pragma unroll
-    for (int p = 0; p < BP; ++p) {
-      // BN < RPP: the surplus threads re-load an in-tile row and do not store it
-      const int n = n0 + (BN >= RPP ? crow + p * RPP : crow % BN);
-      rb[p] = *reinterpret_cast<const u32x4*>(w + (long)n * a.Kpad + k0 + cch * VEC);
-    }
+    for (int p = 0; p < BP; ++p) rb[p] = *reinterpret_cast<const u32x4*>(wrow[p] + k0);
   };
   auto store_tile = [&](int buf) {
     TI* As = smem + buf * (BM + BN) * LDR;
@@ -211,7 +232,7 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
   };
 
   const int wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -222,22 +243,25 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
   auto compute = [&](int buf) {
     const TI* As = smem + buf * (BM + BN) * LDR;
     const TI* Bs = As + BM * LDR;
-    const TI* Ab = As + (wm * (BM / 2) + lr) * LDR;
-    const TI* Bb = Bs + (wn * (BN / 2) + lr) * LDR;
+    const TI* Ab = As + (wm * WTM + lr) * LDR;
+    const TI* Bb = Bs + (wn * WTN + lr) * LDR;
     if constexpr (sizeof(TI) == 2) {
-      bf16x8 af[TM], bfv[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * LDR + lq * 8);
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8 af[TM], bfv[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * LDR + lq * 8);
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * LDR + ks * 32 + lq * 8);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * LDR + ks * 32 + lq * 8);
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < BK / 16; ++h) {
         f32x4 af[TM], bfv[TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const f32x4*>(Ab + i * 16 * LDR + h * 16 + lq * 4);
@@ -270,23 +294,23 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm * (BM / 2) + i * 16 + lq * 4 + r;
+      const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
       if (m >= a.M) continue;
       if constexpr (EPI == KEPI_SPLIT) {
         float* dst = a.partial + (((long)par * a.nsplit + split) * a.M + m) * a.NT;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) dst[n0 + wn * (BN / 2) + j * 16 + lr] = acc[i][j][r];
+        for (int j = 0; j < TN; ++j) dst[n0 + wn * WTN + j * 16 + lr] = acc[i][j][r];
       } else if constexpr (EPI == KEPI_STD) {
         const long op = out_pixel(a, m, py, px);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const int n = n0 + wn * (BN / 2) + j * 16 + lr;
+          const int n = n0 + wn * WTN + j * 16 + lr;
           if (n < a.N) store_std<TO>(a, epi_std<TO>(a, acc[i][j][r], n, op), n, op);
         }
       } else {  // AAD: column tiles (2jp, 2jp+1) = (gamma, beta) of the same 16 channels
 #pragma unroll
         for (int jp = 0; jp < TN / 2; ++jp) {
-          const int ng = n0 + wn * (BN / 2) + (2 * jp) * 16 + lr;
+          const int ng = n0 + wn * WTN + (2 * jp) * 16 + lr;
           const int c = (ng >> 5) * 16 + lr;
           if (c < a.C_aad) {
             const float ga = acc[i][2 * jp][r] + a.shift[ng];
@@ -336,11 +360,17 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a) {
 namespace {
 
 struct Plan {
-  int BM, BN, nNt, nMt, npar, nsplit, kt_per_split, NT, M, Ho, Wo;
+  int BM, BN, BK, nNt, nMt, npar, nsplit, kt_per_split, NT, M, Ho, Wo;
   bool fast;
 };
 
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
 Plan make_plan(const ConvDesc& d) {
+  static const int force_bk = env_int("GHOST_CONV_BK", 0);   // tuning knob (0 = heuristic)
   Plan p{};
   p.npar = d.kind == CONV_T4S2 ? 4 : 1;
   if (d.kind == CONV_T4S2) {
@@ -351,18 +381,39 @@ Plan make_plan(const ConvDesc& d) {
     p.Wo = (d.Wi + 2 * d.pad - d.kw) / d.stride + 1;
   }
   p.M = d.B * p.Ho * p.Wo;
-  const int vec = d.ti == GHOST_BF16 ? 8 : 4;
+  const bool bf = d.ti == GHOST_BF16;
+  const int vec = bf ? 8 : 4;
   p.fast = (d.Cin % 32 == 0) && (d.ldx % vec == 0) && ((uintptr_t)d.x % 16 == 0);
-  if (d.epi == EPI_AAD)
-    p.BN = d.N > 64 ? 128 : 64;
-  else
-    p.BN = d.N <= 32 ? 32 : (d.N <= 64 ? 64 : 128);
+  // BK = 64 pays only on deep reductions (measured: 256x64 tiles lose 2x at BK 64 from LDS occupancy)
+  const bool bk64_ok = bf && p.fast && d.Cin % 64 == 0 && d.Kpad % 64 == 0;
+  p.BK = (bk64_ok && d.Kpad >= 4608) ? 64 : 32;
+  if (force_bk == 32 || (force_bk == 64 && bk64_ok)) p.BK = force_bk;
+  if (!p.fast) {
+    p.BN = d.N <= 32 ? 32 : 64;
+    p.BM = d.N <= 32 ? 256 : 64;
+  } else if (d.epi == EPI_AAD) {
+    p.BN = 128;
+    p.BM = ((p.M + 127) / 128) * ((d.N + 127) / 128) * p.npar >= 512 ? 128 : 64;
+  } else if (d.N <= 16) {
+    p.BN = 16; p.BM = 256;
+  } else if (d.N <= 32) {
+    p.BN = 32; p.BM = 256;
+  } else if (d.N <= 64) {
+    p.BN = 64; p.BM = 256;
+  } else {
+    p.BN = 128;
+    p.BM = ((p.M + 127) / 128) * ((d.N + 127) / 128) * p.npar >= 512 ? 128 : 64;
+  }
+  if (!p.fast || p.BM >= 256) p.BK = force_bk == 64 && bk64_ok ? 64 : 32;
+  static const char* force_tile = getenv("GHOST_CONV_TILE");   // tuning knob "BMxBN"
+  if (force_tile && p.fast && d.epi != EPI_AAD) {
+    int bm = 0, bn = 0;
+    if (sscanf(force_tile, "%dx%d", &bm, &bn) == 2 && bn >= d.N / 2 && bm > 0) { p.BM = bm; p.BN = bn; }
+  }
   p.nNt = (d.N + p.BN - 1) / p.BN;
-  const int tiles128 = ((p.M + 127) / 128) * p.nNt * p.npar;
-  p.BM = (tiles128 >= 512 || !p.fast) ? 128 : 64;
   p.nMt = (p.M + p.BM - 1) / p.BM;
   p.NT = p.nNt * p.BN;
-  const int nk = d.Kpad / 32;
+  const int nk = d.Kpad / p.BK;
   const int tiles = p.nMt * p.nNt * p.npar;
   int s = 1;
   if (d.force_split > 0) {
@@ -399,26 +450,46 @@ ConvArgs make_args(const ConvDesc& d, const Plan& p, float* partial) {
   return a;
 }
 
-template <typename TI, typename TO, int BM, int BN, int EPI, bool FAST>
+template <typename TI, typename TO, int BM, int BN, int BK, int EPI, bool FAST>
 void launch_gemm(const ConvArgs& a, const Plan& p, hipStream_t s) {
   dim3 grid(p.nMt * p.nNt, p.nsplit, p.npar);
-  hipLaunchKernelGGL((conv_igemm_kernel<TI, TO, BM, BN, EPI, FAST>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<TI, TO, BM, BN, BK, EPI, FAST>), grid, dim3(256), 0, s, a);
 }
 
+// instantiated configurations (BM x BN x BK); anything else is rejected by the plan
 template <typename TI, typename TO, int EPI, bool FAST>
 int dispatch_tile(const ConvArgs& a, const Plan& p, hipStream_t s) {
-  if (p.BM == 128 && p.BN == 128) launch_gemm<TI, TO, 128, 128, EPI, FAST>(a, p, s);
-  else if (p.BM == 128 && p.BN == 64) launch_gemm<TI, TO, 128, 64, EPI, FAST>(a, p, s);
-  else if (p.BM == 64 && p.BN == 128) launch_gemm<TI, TO, 64, 128, EPI, FAST>(a, p, s);
-  else if (p.BM == 64 && p.BN == 64) launch_gemm<TI, TO, 64, 64, EPI, FAST>(a, p, s);
-  else {
+  const int key = p.BM * 100000 + p.BN * 100 + p.BK;
+#define GHOST_TILE(bm, bn, bk) \
+  case bm * 100000 + bn * 100 + bk: launch_gemm<TI, TO, bm, bn, bk, EPI, FAST>(a, p, s); return 0;
+  if constexpr (!FAST) {
     if constexpr (EPI != KEPI_AAD) {
-      if (p.BM == 128 && p.BN == 32) { launch_gemm<TI, TO, 128, 32, EPI, FAST>(a, p, s); return 0; }
-      if (p.BM == 64 && p.BN == 32) { launch_gemm<TI, TO, 64, 32, EPI, FAST>(a, p, s); return 0; }
+      switch (key) { GHOST_TILE(256, 32, 32) GHOST_TILE(64, 64, 32) default: break; }
+    }
+    return -1;
+  } else if constexpr (sizeof(TI) == 2) {
+    if constexpr (EPI == KEPI_AAD) {
+      switch (key) { GHOST_TILE(128, 128, 32) GHOST_TILE(128, 128, 64) GHOST_TILE(64, 128, 32)
+                     GHOST_TILE(64, 128, 64) default: break; }
+    } else {
+      switch (key) { GHOST_TILE(128, 128, 32) GHOST_TILE(128, 128, 64) GHOST_TILE(64, 128, 32)
+                     GHOST_TILE(64, 128, 64) GHOST_TILE(256, 64, 32) GHOST_TILE(256, 64, 64)
+                     GHOST_TILE(256, 32, 32) GHOST_TILE(256, 32, 64) GHOST_TILE(256, 16, 32)
+                     GHOST_TILE(256, 16, 64) GHOST_TILE(128, 64, 32) GHOST_TILE(128, 64, 64)
+                     GHOST_TILE(64, 64, 32) GHOST_TILE(64, 64, 64) GHOST_TILE(128, 32, 32)
+                     GHOST_TILE(128, 16, 32) default: break; }
+    }
+    return -1;
+  } else {
+    if constexpr (EPI == KEPI_AAD) {
+      switch (key) { GHOST_TILE(128, 128, 32) GHOST_TILE(64, 128, 32) default: break; }
+    } else {
+      switch (key) { GHOST_TILE(128, 128, 32) GHOST_TILE(64, 128, 32) GHOST_TILE(256, 64, 32)
+                     GHOST_TILE(256, 32, 32) GHOST_TILE(256, 16, 32) default: break; }
     }
     return -1;
   }
-  return 0;
+#undef GHOST_TILE
 }
 
 template <typename TI, typename TO>

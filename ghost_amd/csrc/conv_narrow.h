@@ -1,0 +1,13 @@
+// ghost_amd — 3x3 / pad 1 convolution to <= 3 output channels (the generator's RGB output).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ghost {
+
+bool conv3x3_narrow_supported(int dt, int H, int W, int Cin, int ldx, int NO);
+// w_narrow: [32][Kpad] with row n = tap*NO + o (tap = ky*3 + kx), K = input channel (zero rows >= 9*NO)
+int conv3x3_narrow(int dt, const void* x, int B, int H, int W, int Cin, int ldx, const void* w_narrow, int Kpad, int NO,
+                   const void* res, int ldres, int tanh_out, void* y, int ldy, uint8_t* u8, hipStream_t s);
+
+}  // namespace ghost

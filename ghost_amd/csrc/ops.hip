@@ -169,19 +169,17 @@ int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* 
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ void __launch_bounds__(256)
-upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, int B, int H, int W, int C, float sh,
+upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, int H, int W, int C, float sh,
                   float sw) {
+  // grid: x = chunks of one output row (2W * C/VEC work items), y = b * 2H + oy; 32-bit index math only
   constexpr int VEC = Vec16<T>::N;
   const int nch = C / VEC;
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  const int Ho = 2 * H, Wo = 2 * W;
-  const long total = (long)B * Ho * Wo * nch;
-  if (idx >= total) return;
-  const int ci = (int)(idx % nch);
-  const long op = idx / nch;
-  const int ox = (int)(op % Wo);
-  const int oy = (int)((op / Wo) % Ho);
-  const int b = (int)(op / ((long)Wo * Ho));
+  const int Wo = 2 * W, Ho = 2 * H;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Wo * nch) return;
+  const int row = blockIdx.y;
+  const int b = row / Ho, oy = row - b * Ho;
+  const int ox = i / nch, ci = i - ox * nch;
   // keep the rounded source coordinate, as PyTorch does: the empty asm stops hipcc from
   // re-forming sh*oy - y0 as one fma (which would skip the product's rounding)
   float ry = sh * (float)oy, rx = sw * (float)ox;
@@ -192,28 +190,27 @@ upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, 
   const float lx1 = rx - (float)x0, lx0 = 1.f - lx1;
   const T* xb = x + (long)b * H * W * ldx + ci * VEC;
   float v00[VEC], v01[VEC], v10[VEC], v11[VEC], o[VEC];
-  load16_f(xb + ((long)y0 * W + x0) * ldx, v00);
-  load16_f(xb + ((long)y0 * W + x1) * ldx, v01);
-  load16_f(xb + ((long)y1 * W + x0) * ldx, v10);
-  load16_f(xb + ((long)y1 * W + x1) * ldx, v11);
+  load16_f(xb + (long)(y0 * W + x0) * ldx, v00);
+  load16_f(xb + (long)(y0 * W + x1) * ldx, v01);
+  load16_f(xb + (long)(y1 * W + x0) * ldx, v10);
+  load16_f(xb + (long)(y1 * W + x1) * ldx, v11);
 #pragma unroll
   for (int e = 0; e < VEC; ++e) o[e] = ly0 * (lx0 * v00[e] + lx1 * v01[e]) + ly1 * (lx0 * v10[e] + lx1 * v11[e]);
-  store16_f(y + op * ldy + ci * VEC, o);
+  store16_f(y + ((long)row * Wo + ox) * ldy + ci * VEC, o);
 }
 
 int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C, hipStream_t s) {
   const int vec = dt == GHOST_F32 ? 4 : 8;
   if (C % vec || ldx % vec || ldy % vec || (uintptr_t)x % 16 || (uintptr_t)y % 16) return -1;
-  const long total = (long)B * 4 * H * W * (C / vec);
-  dim3 grid((unsigned)((total + 255) / 256));
+  dim3 grid((unsigned)((2 * W * (C / vec) + 255) / 256), (unsigned)(B * 2 * H));
   // source scale (in-1)/(out-1) rounded once on the host, as PyTorch's area_pixel_compute_scale
   const float sh = H > 0 ? (float)(H - 1) / (float)(2 * H - 1) : 0.f;
   const float sw = W > 0 ? (float)(W - 1) / (float)(2 * W - 1) : 0.f;
   if (dt == GHOST_F32)
-    hipLaunchKernelGGL(upsample2x_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, B, H, W, C,
+    hipLaunchKernelGGL(upsample2x_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, H, W, C,
                        sh, sw);
   else if (dt == GHOST_BF16)
-    hipLaunchKernelGGL(upsample2x_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, B, H, W, C,
+    hipLaunchKernelGGL(upsample2x_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, H, W, C,
                        sh, sw);
   else
     return -1;

@@ -6,6 +6,7 @@ Slot names are the ones ``ghost_aei_bind`` accepts (see aei_runtime.hip
 
 Layouts (Npad = Cout rounded up to 128, Kpad = K rounded up to 32, zero padded):
   conv  [Cout,Cin,kh,kw]      -> [Npad][Kpad], K = (ky*kw + kx)*Cin + c
+  conv3x3 to <= 3 channels    -> also [32][Kpad], row = (ky*3 + kx)*Cout + o, K = c  (narrow kernel)
   convT [Cin,Cout,4,4] (s2p1) -> [4][Npad][Kpad], phase = 2*py+px, K = (ty*2+tx)*Cin + c,
                                  kernel tap ky = ((1,3),(0,2))[py][ty]  (sub-pixel decomposition)
   AAD conv1/conv2 (1x1)       -> [Npad][Kpad] rows interleaved per 16 channels: gamma c0..15,
@@ -43,6 +44,15 @@ def pack_conv(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     k = kh * kw * ci
     out = torch.zeros(rup(co, 128), rup(k, 32), dtype=dtype, device=w.device)
     out[:co, :k] = w.permute(0, 2, 3, 1).reshape(co, k).to(dtype)
+    return out
+
+
+def pack_conv3x3_narrow(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """[Cout<=3, Cin, 3, 3] -> [32][Kpad]: row n = (ky*3 + kx)*Cout + o, K = input channel."""
+    co, ci = w.shape[:2]
+    assert co <= 3 and w.shape[2:] == (3, 3)
+    out = torch.zeros(32, rup(ci, 32), dtype=dtype, device=w.device)
+    out[:9 * co, :ci] = w.permute(2, 3, 0, 1).reshape(9 * co, ci).to(dtype)
     return out
 
 
@@ -144,4 +154,6 @@ def pack_all(sd: Dict[str, torch.Tensor], backbone: str, num_blocks: int, c_id: 
             if i == num_blocks - 1 and cin != cout:
                 w = torch.cat([w, sd[f"generator.AADBlk{k}.last_add_block.2.weight"]], 1)
             slots[f"gen.blk{k}.conv{i}.w"] = pack_conv(w, dtype)
+            if w.shape[0] <= 3:
+                slots[f"gen.blk{k}.conv{i}.wn"] = pack_conv3x3_narrow(w, dtype)
     return {k: v.contiguous() for k, v in slots.items()}

@@ -91,6 +91,11 @@ int ghost_conv2d_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, in
                       int Npad, int Kpad, int kh, int kw, int stride, int pad, const float* scale, const float* shift,
                       float slope, const void* res, int ldres, int tanh_out, void* y, int ldy, void* ws,
                       int64_t ws_bytes, void* stream);
+/* Conv2d 3x3/p1 to Cout <= 3 channels (the generator's RGB output): halo-tiled per-tap partial
+ * sums; w_narrow [32][Kpad], row (ky*3+kx)*Cout + o; optional residual, tanh and BGR uint8 copy. */
+int ghost_conv3x3_narrow_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx, const void* w_narrow,
+                              int Kpad, int Cout, const void* res, int ldres, int tanh_out, void* y, int ldy,
+                              uint8_t* u8, void* stream);
 /* ConvTranspose2d 4x4/s2/p1 as four 2x2 sub-pixel phases; w_packed: [4][Npad][Kpad],
  * phase = 2*py + px, K index (ty*2 + tx)*Cin + c. */
 int ghost_conv_transpose4x4s2_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx,

@@ -338,3 +338,33 @@ def test_aad_layer_fused_path_vs_oracle(lib, dt, c_x, c_a, n, B):
     scale = max(1.0, float(ref.abs().max()))
     err = float((out - ref).abs().max())
     assert err <= (1e-4 if dt == torch.float32 else 4e-2) * scale, err
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,H,W,use_res", [(128, 3, 32, 64, False), (64, 3, 16, 32, True), (96, 1, 8, 96, False)])
+def test_conv3x3_narrow_op(lib, dt, cin, cout, H, W, use_res):
+    """The generator's RGB-output conv: per-tap partial sums on a halo tile, tanh and BGR uint8 epilogue."""
+    from ghost_amd import _lib
+    from ghost_amd.network.pack import pack_conv3x3_narrow
+    g = torch.Generator().manual_seed(cin + W)
+    x = torch.randn(2, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) * (1.0 / (cin * 9)) ** 0.5
+    res = torch.randn(2, cout, H, W, generator=g) * 0.3
+    ref = F.conv2d(x.to(dt).float(), w.to(dt).float(), padding=1)
+    if use_res:
+        ref = ref + res.to(dt).float()
+    ref = torch.tanh(ref)
+    wn = pack_conv3x3_narrow(w, dt).to(DEV)
+    xd = nhwc(x).to(dt).to(DEV)
+    rd = nhwc(res).to(dt).to(DEV)
+    y = torch.empty(2, H, W, cout, dtype=dt, device=DEV)
+    u8 = torch.zeros(2, H, W, 3, dtype=torch.uint8, device=DEV)
+    _lib.check(lib.ghost_conv3x3_narrow_nhwc(_lib.gdtype(dt), xd.data_ptr(), 2, H, W, cin, cin, wn.data_ptr(),
+                                             wn.shape[1], cout, rd.data_ptr() if use_res else None, cout, 1,
+                                             y.data_ptr(), cout, u8.data_ptr(), stream(lib)))
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    assert float((got - ref).abs().max()) <= tol
+    ref_u8 = ((ref.permute(0, 2, 3, 1) * 0.5 + 0.5) * 255).type(torch.uint8)
+    got_u8 = u8.cpu()[..., [2, 1, 0]][..., :cout] if cout == 3 else u8.cpu()[..., 2:3]
+    assert int((got_u8.int() - ref_u8[..., :cout].int()).abs().max()) <= (1 if dt == torch.float32 else 3)

@@ -1,0 +1,133 @@
+"""Micro-benchmarks of the individual gfx950 kernels at the generator's B=64 shapes.
+
+    python tools/bench_ops.py [--only conv|aad|up|stats] [--iters 20]
+
+Each case is timed with HIP events around `iters` back-to-back launches on one stream
+(after 3 warm-ups) and reported as us/launch, TFLOP/s (convs) or algorithmic GB/s.
+Used to A/B kernel variants quickly (cdna_hip_programming.md §5.4 rule 24: same process).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from ghost_amd import _lib  # noqa: E402
+from ghost_amd.network.pack import pack_conv, pack_convT4x4, rup  # noqa: E402
+
+DEV = torch.device("cuda:0")
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3   # us
+
+
+def conv_cases(lib, iters, dt=torch.bfloat16):
+    B = 64
+    ws = torch.empty(512 << 20, dtype=torch.uint8, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    # (name, H, Cin, Cout, k, stride, pad)
+    cases = [("gen256 64->64", 256, 64, 64, 3, 1, 1), ("gen256 cat128->3", 256, 128, 3, 3, 1, 1),
+             ("gen128 128->128", 128, 128, 128, 3, 1, 1), ("gen128 cat256->64", 128, 256, 64, 3, 1, 1),
+             ("gen64 256->256", 64, 256, 256, 3, 1, 1), ("gen64 cat512->128", 64, 512, 128, 3, 1, 1),
+             ("gen32 512->512", 32, 512, 512, 3, 1, 1), ("gen16 1024->1024", 16, 1024, 1024, 3, 1, 1),
+             ("gen4 1024->1024", 4, 1024, 1024, 3, 1, 1),
+             ("enc conv2 32->64", 128, 32, 64, 4, 2, 1), ("enc conv1 3->32", 256, 3, 32, 4, 2, 1)]
+    for name, H, ci, co, k, s, p in cases:
+        x = torch.randn(B, H, H, ci, device=DEV).to(dt)
+        w = pack_conv(torch.randn(co, ci, k, k, device=DEV) * 0.05, dt)
+        Ho = (H + 2 * p - k) // s + 1
+        y = torch.empty(B, Ho, Ho, co, dtype=dt, device=DEV)
+
+        def run():
+            _lib.check(lib.ghost_conv2d_nhwc(_lib.gdtype(dt), x.data_ptr(), B, H, H, ci, ci, w.data_ptr(), co,
+                                             w.shape[0], w.shape[1], k, k, s, p, None, None, 1.0, None, 0, 0,
+                                             y.data_ptr(), co, ws.data_ptr(), ws.numel(), st))
+        us = timeit(run, iters)
+        fl = 2.0 * B * Ho * Ho * co * ci * k * k
+        by = (x.numel() + y.numel()) * x.element_size()
+        print(f"conv  {name:22s} {us:9.1f} us  {fl / us / 1e6:7.1f} TF/s  {by / us / 1e3:7.1f} GB/s(io)", flush=True)
+
+
+def aad_cases(lib, iters, dt=torch.bfloat16):
+    B = 64
+    st = torch.cuda.current_stream().cuda_stream
+    ws = torch.empty(512 << 20, dtype=torch.uint8, device=DEV)
+    for C, Ca, n in [(64, 64, 256), (128, 128, 128), (256, 256, 64), (512, 512, 32), (1024, 512, 16)]:
+        h = torch.randn(B, n, n, C, device=DEV).to(dt)
+        za = torch.randn(B, n, n, Ca, device=DEV).to(dt)
+        out = torch.empty_like(h)
+        gbw = torch.randn(rup(2 * C, 128), rup(Ca, 32), device=DEV).to(dt) * 0.05
+        gbb = torch.zeros(rup(2 * C, 128), device=DEV)
+        wh = torch.randn(C, device=DEV) * 0.05
+        bh = torch.zeros(1, device=DEV)
+        idgb = torch.randn(B, 2 * C, device=DEV)
+
+        def run():
+            _lib.check(lib.ghost_aad_layer_nhwc(_lib.gdtype(dt), h.data_ptr(), C, za.data_ptr(), Ca, B, n, n, C, Ca,
+                                                gbw.data_ptr(), gbw.shape[0], gbw.shape[1], gbb.data_ptr(),
+                                                wh.data_ptr(), bh.data_ptr(), idgb.data_ptr(), 2 * C, 0.0,
+                                                out.data_ptr(), C, ws.data_ptr(), ws.numel(), st))
+        us = timeit(run, iters)
+        by = (h.numel() * 2 + za.numel()) * h.element_size()
+        print(f"aad   C={C:4d} Ca={Ca:4d} n={n:3d} (stats+mask/fused) {us:9.1f} us  {by / us / 1e3:7.1f} GB/s(alg)",
+              flush=True)
+
+
+def up_cases(lib, iters, dt=torch.bfloat16):
+    B = 64
+    st = torch.cuda.current_stream().cuda_stream
+    for C, n in [(64, 128), (128, 64)]:
+        x = torch.randn(B, n, n, C, device=DEV).to(dt)
+        y = torch.empty(B, 2 * n, 2 * n, C, dtype=dt, device=DEV)
+        us = timeit(lambda: _lib.check(lib.ghost_upsample2x_nhwc(_lib.gdtype(dt), x.data_ptr(), C, y.data_ptr(), C,
+                                                                 B, n, n, C, st)), iters)
+        by = (x.numel() + y.numel()) * x.element_size()
+        print(f"up2x  C={C} {n}->{2 * n} {us:9.1f} us  {by / us / 1e3:7.1f} GB/s", flush=True)
+
+
+def stats_cases(lib, iters, dt=torch.bfloat16):
+    B = 64
+    st = torch.cuda.current_stream().cuda_stream
+    ws = torch.empty(256 << 20, dtype=torch.uint8, device=DEV)
+    for C, n in [(64, 256), (128, 128)]:
+        x = torch.randn(B, n, n, C, device=DEV).to(dt)
+        stat = torch.empty(B, C, 2, device=DEV)
+        us = timeit(lambda: _lib.check(lib.ghost_instnorm_stats_nhwc(_lib.gdtype(dt), x.data_ptr(), B, n * n, C, C,
+                                                                     stat.data_ptr(), ws.data_ptr(), ws.numel(), st)),
+                    iters)
+        print(f"stats C={C} n={n} {us:9.1f} us  {x.numel() * x.element_size() / us / 1e3:7.1f} GB/s", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    lib = _lib.load()
+    print("env:", {k: v for k, v in os.environ.items() if k.startswith("GHOST_")})
+    if a.only in ("", "conv"):
+        conv_cases(lib, a.iters)
+    if a.only in ("", "aad"):
+        aad_cases(lib, a.iters)
+    if a.only in ("", "up"):
+        up_cases(lib, a.iters)
+    if a.only in ("", "stats"):
+        stats_cases(lib, a.iters)
+
+
+if __name__ == "__main__":
+    main()
