@@ -1,0 +1,198 @@
+// ghost_amd — AADLayer kernel for the high-resolution stages (C in {64, 128}, bf16).
+//
+// AADLayer.py:20-38 (+ the following ReLU) for up to two AADLayers that read the same
+// h_in and z_attr (AAD_ResBlk's first add_block layer and its last_add_block layer,
+// AADLayer.py:53-79), sharing every byte of input traffic:
+//
+//   per 16-pixel tile and wave:
+//     h  = (h_in - mu) * rstd                                   (16 channels per lane, fp32)
+//     M_l = sigmoid(sum_c wh_l[c] h[c] + bh_l)                   (lane partials + 2 xor-shuffles)
+//     [gamma|beta]_l^T = W_l . z_attr^T + b_l                    (MFMA 16x16x32, W_l in LDS,
+//                                                                 z_attr fragments straight from HBM)
+//     out_l = relu((1 - M_l)(gamma h + beta) + M_l (gi h + bi))  (16-byte stores)
+//
+// The GEMM is computed transposed (rows = weight rows, columns = pixels) with the weight
+// rows permuted (pack.py pack_aad_v3) so that the accumulator a lane holds is gamma and
+// beta of 16 *contiguous-in-pairs-of-8* channels of ONE pixel: the blend needs no LDS
+// round trip and every global access is a 16-byte vector along channels.
+// HBM bytes per launch = |h_in| + |z_attr| + L * |out|  (the algorithmic minimum).
+#include "aad_v3.h"
+#include "ghost_common.h"
+
+namespace ghost {
+
+struct AadV3Args {
+  const bf16* za;
+  const bf16* hin;
+  const float* stat;
+  const bf16* w3[2];
+  const float* b3[2];
+  const float* wh[2];
+  const float* bh[2];
+  const float* idgb[2];
+  bf16* out[2];
+  int ldo[2];
+  int lda, ldh, id_ld, HW, PPW;
+  float slope;
+};
+
+static constexpr int kWaves = 8;
+
+template <int C, int CA, int L>
+__global__ void __launch_bounds__(512) aad_v3_kernel(const AadV3Args a) {
+  constexpr int CT = C / 64;          // 64-channel tiles
+  constexpr int KS = CA / 32;         // MFMA k-steps
+  constexpr int WLD = CA + 8;         // padded LDS weight row (bf16 elements)
+  constexpr int NH = CT * 2;          // 16-byte h_in chunks per lane (8 channels each)
+  __shared__ __attribute__((aligned(16))) bf16 s_w[L * CT * 128 * WLD];
+  __shared__ __attribute__((aligned(16))) float s_b[L * CT * 128];
+  __shared__ __attribute__((aligned(16))) float s_rs[C];
+  __shared__ __attribute__((aligned(16))) float s_nm[C];
+  __shared__ __attribute__((aligned(16))) float s_wh[L * C];
+  __shared__ __attribute__((aligned(16))) float s_gi[L * C];
+  __shared__ __attribute__((aligned(16))) float s_bi[L * C];
+
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const long p_begin = (long)blockIdx.x * a.PPW;
+  const int b = (int)(p_begin / a.HW);     // PPW divides HW: one sample per workgroup
+
+  // ---- resident weights, biases and per-channel tables ----
+  for (int l = 0; l < L; ++l) {
+    for (int idx = tid; idx < CT * 128 * (CA / 8); idx += kWaves * 64) {
+      const int row = idx / (CA / 8), kc = idx - row * (CA / 8);
+      *reinterpret_cast<u32x4*>(&s_w[(l * CT * 128 + row) * WLD + kc * 8]) =
+          *reinterpret_cast<const u32x4*>(a.w3[l] + (long)row * CA + kc * 8);
+    }
+    for (int idx = tid; idx < CT * 128; idx += kWaves * 64) s_b[l * CT * 128 + idx] = a.b3[l][idx];
+    for (int c = tid; c < C; c += kWaves * 64) {
+      s_wh[l * C + c] = a.wh[l][c];
+      s_gi[l * C + c] = a.idgb[l][(long)b * a.id_ld + c];
+      s_bi[l * C + c] = a.idgb[l][(long)b * a.id_ld + C + c];
+    }
+  }
+  for (int c = tid; c < C; c += kWaves * 64) {
+    const float mu = a.stat[((long)b * C + c) * 2], rs = a.stat[((long)b * C + c) * 2 + 1];
+    s_rs[c] = rs;
+    s_nm[c] = -mu * rs;
+  }
+  __syncthreads();
+
+  float bh[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) bh[l] = a.bh[l][0];
+
+  // one 16-pixel tile per wave iteration; latency is hidden by the 8 waves of the workgroup
+  // and the co-resident workgroups (no software prefetch: it would cost the occupancy)
+  const int ntiles = a.PPW / 16;
+  for (int t = wid; t < ntiles; t += kWaves) {
+    // compiler memory barrier: keeps the per-channel LDS tables from being hoisted out of the
+    // loop into (hundreds of) registers; re-reading them from LDS each tile is cheap
+    asm volatile("" ::: "memory");
+    const long p = p_begin + t * 16 + lr;
+    u32x4 zc[KS], hc[NH];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + ks * 32 + lq * 8);
+#pragma unroll
+    for (int j = 0; j < NH; ++j)   // chunk j = (ct, s): channels ct*64 + 32s + 8lq .. +7
+      hc[j] = *reinterpret_cast<const u32x4*>(a.hin + p * a.ldh + (j >> 1) * 64 + (j & 1) * 32 + lq * 8);
+
+    // mask partials of every layer over this lane's 8*NH channels, then across the 4 lanes of the pixel
+    float ms[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) ms[l] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NH; ++j) {
+      const int c0 = (j >> 1) * 64 + (j & 1) * 32 + lq * 8;
+      const bf16* hv = reinterpret_cast<const bf16*>(&hc[j]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float hh = fmaf((float)hv[e], s_rs[c0 + e], s_nm[c0 + e]);
+#pragma unroll
+        for (int l = 0; l < L; ++l) ms[l] = fmaf(s_wh[l * C + c0 + e], hh, ms[l]);
+      }
+    }
+    float Mk[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      float sm = ms[l];
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      Mk[l] = sigmoidf_ref(sm + bh[l]);
+    }
+
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const bf16* W = s_w + (l * CT + ct) * 128 * WLD;
+        f32x4 acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          acc[i] = *reinterpret_cast<const f32x4*>(&s_b[(l * CT + ct) * 128 + i * 16 + lq * 4]);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          bf16x8 bfrag;
+          __builtin_memcpy(&bfrag, &zc[ks], 16);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&W[(i * 16 + lr) * WLD + ks * 32 + lq * 8]);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i], 0, 0, 0);
+          }
+        }
+        // lane holds gamma (row tiles 2s + e/4) and beta (4 + 2s + e/4) of channels ct*64 + 32s + 8lq + e
+#pragma unroll
+        for (int sh = 0; sh < 2; ++sh) {
+          const int j = ct * 2 + sh;
+          const int c0 = ct * 64 + sh * 32 + lq * 8;
+          const bf16* hv = reinterpret_cast<const bf16*>(&hc[j]);
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float hh = fmaf((float)hv[e], s_rs[c0 + e], s_nm[c0 + e]);
+            const float g = acc[2 * sh + (e >> 2)][e & 3];
+            const float be = acc[4 + 2 * sh + (e >> 2)][e & 3];
+            const float A = fmaf(g, hh, be);
+            const float I = fmaf(s_gi[l * C + c0 + e], hh, s_bi[l * C + c0 + e]);
+            const float v = (1.0f - Mk[l]) * A + Mk[l] * I;
+            o[e] = v > 0.f ? v : v * a.slope;
+          }
+          store16_f(a.out[l] + p * a.ldo[l] + c0, o);
+        }
+      }
+    }
+  }
+}
+
+bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo) {
+  if (dt != GHOST_BF16) return false;
+  const bool shape = (C == 64 && (Ca == 64 || Ca == 32)) || (C == 128 && (Ca == 128 || Ca == 64));
+  if (!shape || lda % 8 || ldh % 8 || ldo % 8) return false;
+  const int ppw = HW >= 65536 ? 1024 : 512;
+  return HW % ppw == 0 && (long)B * HW / ppw >= 32;
+}
+
+int aad_v3(const AadV3Desc& d, hipStream_t s) {
+  if (!aad_v3_supported(GHOST_BF16, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo[0])) return -1;
+  if (d.L == 2 && d.ldo[1] % 8) return -1;
+  if (d.L < 1 || d.L > 2 || (d.L == 2 && d.C != 64)) return -1;   // two layers' weights must fit LDS
+  AadV3Args a{};
+  a.za = (const bf16*)d.za; a.hin = (const bf16*)d.hin; a.stat = d.stat;
+  for (int l = 0; l < d.L; ++l) {
+    a.w3[l] = (const bf16*)d.w3[l]; a.b3[l] = d.b3[l]; a.wh[l] = d.wh[l]; a.bh[l] = d.bh[l];
+    a.idgb[l] = d.idgb[l]; a.out[l] = (bf16*)d.out[l]; a.ldo[l] = d.ldo[l];
+  }
+  a.lda = d.lda; a.ldh = d.ldh; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
+  a.PPW = d.HW >= 65536 ? 1024 : 512;
+  dim3 grid((unsigned)((long)d.B * d.HW / a.PPW));
+#define GHOST_V3(c, ca, l)                                                              \
+  if (d.C == c && d.Ca == ca && d.L == l) {                                             \
+    hipLaunchKernelGGL((aad_v3_kernel<c, ca, l>), grid, dim3(kWaves * 64), 0, s, a);            \
+    return (int)hipGetLastError();                                                      \
+  }
+  GHOST_V3(64, 64, 1) GHOST_V3(64, 64, 2) GHOST_V3(64, 32, 1) GHOST_V3(64, 32, 2)
+  GHOST_V3(128, 128, 1) GHOST_V3(128, 64, 1)
+#undef GHOST_V3
+  return -1;
+}
+
+}  // namespace ghost

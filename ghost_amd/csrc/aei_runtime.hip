@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <string>
@@ -15,6 +16,7 @@
 
 #include "../../include/ghost_amd.h"
 #include "aad_fused.h"
+#include "aad_v3.h"
 #include "conv_igemm.h"
 #include "conv_narrow.h"
 #include "ghost_common.h"
@@ -317,6 +319,52 @@ void aad(Ctx& c, const std::string& name, const void* hin, int ldh, const float*
   run_conv(c, d, 0, 1, flops);
 }
 
+struct AadOut {
+  std::string name;
+  int id_off;
+  void* out;
+  int ldo;
+};
+
+// AADLayers that read the same h_in / z_attr: the register-epilogue kernel takes up to two at
+// once (one pass over the inputs); other shapes run one fused / split AAD kernel per layer
+void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, const float* stat, const void* za,
+               int lda, int Ca, int B, int n, int C, const float* idgb) {
+  ghost_aei* h = c.h;
+  bool v3 = aad_v3_supported(h->dt, B, n * n, C, Ca, lda, ldh, 8);
+  for (auto& l : ls) v3 = v3 && l.ldo % 8 == 0;
+  if (!v3) {
+    for (auto& l : ls) aad(c, l.name, hin, ldh, stat, za, lda, Ca, B, n, C, l.id_off, idgb, l.out, l.ldo);
+    return;
+  }
+  const size_t lmax = C == 64 ? 2 : 1;
+  for (size_t i0 = 0; i0 < ls.size(); i0 += lmax) {
+    AadV3Desc d;
+    d.za = za; d.lda = lda; d.Ca = Ca; d.hin = hin; d.ldh = ldh; d.stat = stat;
+    d.B = B; d.HW = n * n; d.C = C; d.id_ld = h->id_total; d.slope = 0.0f;   // + the ReLU that follows
+    d.L = (int)std::min(lmax, ls.size() - i0);
+    for (int l = 0; l < d.L; ++l) {
+      const AadOut& o = ls[i0 + l];
+      d.w3[l] = c.W(o.name + ".w3");
+      d.b3[l] = (const float*)c.W(o.name + ".b3");
+      d.wh[l] = (const float*)c.W(o.name + ".wh");
+      d.bh[l] = (const float*)c.W(o.name + ".bh");
+      d.idgb[l] = idgb ? idgb + o.id_off : nullptr;
+      d.out[l] = o.out;
+      d.ldo[l] = o.ldo;
+    }
+    if (!c.ok() || c.dry) continue;
+    const double Pn = (double)B * n * n;
+    const double bytes = Pn * (C + Ca + (double)d.L * C) * h->esz;   // |h_in| + |z_attr| + L |out|
+    const double flops = 2.0 * Pn * 2.0 * C * Ca * d.L;
+    int e_all = c.prof_begin(0);
+    int e_big = n == 256 ? c.prof_begin(1) : -1;
+    c.check(aad_v3(d, c.s), "aad_v3");
+    if (e_big >= 0) c.prof_end(1, e_big, bytes, flops);
+    if (e_all >= 0) c.prof_end(0, e_all, bytes, flops);
+  }
+}
+
 void conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, int B, int n, int Cout, void* y,
              int ldy, const void* res, int ldres, int tanh_out, uint8_t* u8) {
   const double flops = 2.0 * B * n * n * Cout * 9.0 * Cin;
@@ -379,46 +427,43 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     const void* za = attr[k - 1];
     const std::string blk = "gen.blk" + std::to_string(k);
     const size_t P = (size_t)B * n * n;
+    const bool last_k = k == 8;
+    const bool split = cin != cout;          // AAD_ResBlk has a last_add_block (AADLayer.py:68-72)
+    const int base = id_off;                  // idgb offset of this block's first AADLayer
     float* stat_m = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
     run_stats(c, m, cin, B, n * n, cin, stat_m);
+    void* y = last_k ? y_out : c.alloc(P * cout * es);
+    // x-branch and h'-branch share the output conv: conv(cat(a_x, a_h), [W_x | W_h]) = x + h'
+    void* cat = split ? c.alloc(P * 2 * cin * es) : nullptr;
     const void* x = m;
     const float* stat_x = stat_m;
-    const bool last_k = k == 8;
-    void* y = last_k ? y_out : c.alloc(P * cout * es);
-    const int ldy = cout;
     for (int i = 0; i < nb; ++i) {
       const bool last = i == nb - 1;
-      const std::string an = blk + ".aad" + std::to_string(i);
-      const std::string cn = blk + ".conv" + std::to_string(i);
+      const std::string cn = blk + ".conv" + std::to_string(i) + ".w";
+      std::vector<AadOut> group;
+      void* a = (last && split) ? cat : c.alloc(P * cin * es);
+      const int lda_out = (last && split) ? 2 * cin : cin;
+      group.push_back({blk + ".aad" + std::to_string(i), base + 2 * cin * i, a, lda_out});
+      if (i == 0 && split)   // last_add_block's AADLayer reads the block input m as well
+        group.push_back({blk + ".aadlast", base + 2 * cin * nb, (char*)cat + (size_t)cin * es, 2 * cin});
+      aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb);
       if (!last) {
-        void* a = c.alloc(P * cin * es);
-        aad(c, an, x, cin, stat_x, za, Ca, Ca, B, n, cin, id_off, idgb, a, cin);
-        id_off += 2 * cin;
         void* xn = c.alloc(P * cin * es);
-        conv3x3(c, cn + ".w", a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr);
+        conv3x3(c, cn, a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr);
         float* st = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
         run_stats(c, xn, cin, B, n * n, cin, st);
         x = xn;
         stat_x = st;
-      } else if (cin == cout) {
-        void* a = c.alloc(P * cin * es);
-        aad(c, an, x, cin, stat_x, za, Ca, Ca, B, n, cin, id_off, idgb, a, cin);
-        id_off += 2 * cin;
-        conv3x3(c, cn + ".w", a, cin, cin, B, n, cout, y, ldy, m, cin, last_k, last_k ? u8 : nullptr);
+      } else if (!split) {
+        conv3x3(c, cn, a, cin, cin, B, n, cout, y, cout, m, cin, last_k, last_k ? u8 : nullptr);
       } else {
-        // x-branch and h'-branch share the output: conv(cat(a_x, a_h), [W_x | W_h]) = x + h'
-        void* cat = c.alloc(P * 2 * cin * es);
-        aad(c, an, x, cin, stat_x, za, Ca, Ca, B, n, cin, id_off, idgb, cat, 2 * cin);
-        id_off += 2 * cin;
-        aad(c, blk + ".aadlast", m, cin, stat_m, za, Ca, Ca, B, n, cin, id_off, idgb,
-            (char*)cat + (size_t)cin * es, 2 * cin);
-        conv3x3(c, cn + ".w", cat, 2 * cin, 2 * cin, B, n, cout, y, ldy, nullptr, 0, last_k, last_k ? u8 : nullptr);
+        conv3x3(c, cn, cat, 2 * cin, 2 * cin, B, n, cout, y, cout, nullptr, 0, last_k, last_k ? u8 : nullptr);
       }
     }
-    if (cin != cout) id_off += 2 * cin;  // last_add_block's AADLayer
+    id_off = base + 2 * cin * nb + (split ? 2 * cin : 0);
     if (!last_k) {
       void* mn = c.alloc((size_t)B * 4 * n * n * cout * es);
-      run_up(c, y, ldy, mn, cout, B, n, n, cout);
+      run_up(c, y, cout, mn, cout, B, n, n, cout);
       m = mn;
     }
   }
@@ -448,9 +493,11 @@ void declare_slots(ghost_aei* h) {
   for (int k = 1; k <= 8; ++k) {
     const int cin = h->gen()[k - 1][0], cout = h->gen()[k - 1][1];
     const std::string blk = "gen.blk" + std::to_string(k);
+    const bool v3 = h->dt == GHOST_BF16 && (cin == 64 || cin == 128);   // register-epilogue AAD layouts
     for (int i = 0; i < h->nb; ++i) {
       const std::string an = blk + ".aad" + std::to_string(i);
       add(an + ".gbw"); add(an + ".gbb"); add(an + ".wh"); add(an + ".bh");
+      if (v3) { add(an + ".w3"); add(an + ".b3"); }
       add(blk + ".conv" + std::to_string(i) + ".w");
       if (i == h->nb - 1 && cout <= 3) add(blk + ".conv" + std::to_string(i) + ".wn");
       h->id_total += 2 * cin;
@@ -458,6 +505,7 @@ void declare_slots(ghost_aei* h) {
     if (cin != cout) {
       const std::string an = blk + ".aadlast";
       add(an + ".gbw"); add(an + ".gbb"); add(an + ".wh"); add(an + ".bh");
+      if (v3) { add(an + ".w3"); add(an + ".b3"); }
       h->id_total += 2 * cin;
     }
   }
@@ -804,4 +852,33 @@ extern "C" int ghost_conv3x3_narrow_nhwc(int dtype, const void* x, int B, int H,
   int rc = conv3x3_narrow(dtype, x, B, H, W, Cin, ldx, w_narrow, Kpad, Cout, res, ldres, tanh_out, y, ldy, u8,
                           (hipStream_t)stream);
   return rc ? fail(rc, "conv3x3_narrow failed (H % 8, W % 32, Cin % 32 and Cout <= 3 required)") : 0;
+}
+
+extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, const void* z_attr, int lda, int B, int H, int W,
+                                        int C, int Ca, int L, const void* const w3[], const float* const b3[],
+                                        const float* const wh[], const float* const bh[], const float* const idgb[],
+                                        int id_ld, float slope, void* const out[], const int ldo[], void* ws,
+                                        int64_t ws_bytes, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int HW = H * W;
+  if (L < 1 || L > 2) return fail(GHOST_EINVAL, "aad_v3: L must be 1 or 2");
+  for (int l = 0; l < L; ++l)
+    if (!aad_v3_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[l]))
+      return fail(GHOST_EINVAL, "aad_v3: unsupported shape (bf16, C in {64,128}, enough pixels)");
+  const size_t stat_b = ((size_t)B * C * 2 * sizeof(float) + 255) & ~size_t(255);
+  const size_t sc = in_stats_workspace_bytes(B, HW, C);
+  char* base = (char*)(((uintptr_t)ws + 255) & ~uintptr_t(255));
+  if (!ws || (size_t)ws_bytes < stat_b + sc + 256) return fail(GHOST_ENOWS, "aad_v3: workspace too small");
+  float* stat = (float*)base;
+  int rc = in_stats(GHOST_BF16, h_in, ldh, B, HW, C, stat, base + stat_b, sc, s);
+  if (rc) return fail(rc, "aad_v3: in_stats failed");
+  AadV3Desc d;
+  d.za = z_attr; d.lda = lda; d.Ca = Ca; d.hin = h_in; d.ldh = ldh; d.stat = stat;
+  d.B = B; d.HW = HW; d.C = C; d.L = L; d.id_ld = id_ld; d.slope = slope;
+  for (int l = 0; l < L; ++l) {
+    d.w3[l] = w3[l]; d.b3[l] = b3[l]; d.wh[l] = wh[l]; d.bh[l] = bh[l]; d.idgb[l] = idgb[l];
+    d.out[l] = out[l]; d.ldo[l] = ldo[l];
+  }
+  rc = aad_v3(d, s);
+  return rc ? fail(rc, "aad_v3 launch failed") : 0;
 }

@@ -11,6 +11,8 @@ Layouts (Npad = Cout rounded up to 128, Kpad = K rounded up to 32, zero padded):
                                  kernel tap ky = ((1,3),(0,2))[py][ty]  (sub-pixel decomposition)
   AAD conv1/conv2 (1x1)       -> [Npad][Kpad] rows interleaved per 16 channels: gamma c0..15,
                                  beta c0..15, gamma c16..31, ...  (+ the same for the biases)
+                                 and, bf16 with C in {64,128}: [C/64*128][Ca] rows permuted for the
+                                 register-epilogue kernel (pack_aad_v3)
   all fc1/fc2 (Linear)        -> one fp32 [Npad][Kpad] = [gamma_l | beta_l] per AADLayer l in plan order
   up1 ConvT k2 on 1x1         -> fp32 [4096][Kpad], n = (y*2+x)*1024 + co
   BatchNorm (eval)            -> fp32 scale = g/sqrt(rv+eps), shift = b - rm*scale
@@ -101,6 +103,30 @@ def pack_aad(sd, prefix: str, dtype) -> Dict[str, torch.Tensor]:
             "bh": sd[f"{prefix}.conv_h.bias"].reshape(1).float().contiguous()}
 
 
+def pack_aad_v3(sd, prefix: str, dtype) -> Dict[str, torch.Tensor]:
+    """Weights of the register-epilogue AAD kernel (aad_v3.hip), C in {64, 128}.
+
+    Per 64-channel tile, row rho = 16*i + 4*q + r (i = MFMA row tile, q = lane group, r = register)
+    holds gamma (i < 4) or beta (i >= 4) of channel 32*((i>>1)&1) + 8*q + 4*(i&1) + r, so that a
+    lane's accumulators are gamma/beta of 16 channels (two runs of 8) of one pixel.
+    """
+    w1 = sd[f"{prefix}.conv1.weight"]
+    c, ca = w1.shape[:2]
+    dev = w1.device
+    rho = torch.arange(128, device=dev)
+    i, q, r = rho >> 4, (rho >> 2) & 3, rho & 3
+    gb = i >> 2
+    cl = 32 * ((i >> 1) & 1) + 8 * q + 4 * (i & 1) + r
+    W = [w1.reshape(c, ca), sd[f"{prefix}.conv2.weight"].reshape(c, ca)]
+    Bs = [sd[f"{prefix}.conv1.bias"].float(), sd[f"{prefix}.conv2.bias"].float()]
+    w3, b3 = [], []
+    for ct in range(c // 64):
+        ch = ct * 64 + cl
+        w3.append(torch.where((gb == 0)[:, None], W[0][ch], W[1][ch]))
+        b3.append(torch.where(gb == 0, Bs[0][ch], Bs[1][ch]))
+    return {"w3": torch.cat(w3, 0).to(dtype).contiguous(), "b3": torch.cat(b3, 0).contiguous()}
+
+
 def aad_plan(backbone: str, num_blocks: int) -> List[Tuple[str, str]]:
     """(slot prefix, state_dict prefix) of every AADLayer in the runtime's plan order."""
     out = []
@@ -138,6 +164,9 @@ def pack_all(sd: Dict[str, torch.Tensor], backbone: str, num_blocks: int, c_id: 
     for slot, pre in aad_plan(backbone, num_blocks):
         for k, v in pack_aad(sd, pre, dtype).items():
             slots[f"{slot}.{k}"] = v
+        if dtype == torch.bfloat16 and sd[f"{pre}.conv1.weight"].shape[0] in (64, 128):
+            for k, v in pack_aad_v3(sd, pre, dtype).items():
+                slots[f"{slot}.{k}"] = v
         ids_w += [sd[f"{pre}.fc1.weight"].float(), sd[f"{pre}.fc2.weight"].float()]
         ids_b += [sd[f"{pre}.fc1.bias"].float(), sd[f"{pre}.fc2.bias"].float()]
     wid = torch.cat(ids_w, 0)

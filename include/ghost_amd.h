@@ -116,6 +116,13 @@ int ghost_aad_layer_nhwc(int dtype, const void* h_in, int ldh, const void* z_att
                          int Ca, const void* gbw_packed, int Npad, int Kpad, const float* gbb, const float* wh,
                          const float* bh, const float* idgb, int id_ld, float slope, void* out, int ldo, void* ws,
                          int64_t ws_bytes, void* stream);
+/* One or two AADLayers (bf16, C in {64,128}) that read the same h_in and z_attr, in one pass:
+ * w3/b3 per layer in the permuted layout of pack.py pack_aad_v3; InstanceNorm statistics of h_in
+ * are computed into the workspace first. */
+int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, const void* z_attr, int lda, int B, int H, int W, int C,
+                             int Ca, int L, const void* const w3[], const float* const b3[], const float* const wh[],
+                             const float* const bh[], const float* const idgb[], int id_ld, float slope,
+                             void* const out[], const int ldo[], void* ws, int64_t ws_bytes, void* stream);
 int ghost_upsample2x_nhwc(int dtype, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C,
                           void* stream);
 int ghost_nhwc_to_nchw(int dtype, const void* x, int ldx, int B, int H, int W, int C, void* y, void* stream);

@@ -368,3 +368,48 @@ def test_conv3x3_narrow_op(lib, dt, cin, cout, H, W, use_res):
     ref_u8 = ((ref.permute(0, 2, 3, 1) * 0.5 + 0.5) * 255).type(torch.uint8)
     got_u8 = u8.cpu()[..., [2, 1, 0]][..., :cout] if cout == 3 else u8.cpu()[..., 2:3]
     assert int((got_u8.int() - ref_u8[..., :cout].int()).abs().max()) <= (1 if dt == torch.float32 else 3)
+
+
+@pytest.mark.parametrize("c_x,c_a,n,B,L", [(64, 64, 256, 2, 2), (64, 64, 256, 2, 1), (128, 128, 128, 2, 1),
+                                           (64, 32, 128, 4, 2), (128, 64, 64, 8, 1)])
+def test_aad_layers_v3_vs_oracle(lib, c_x, c_a, n, B, L):
+    """Register-epilogue AAD kernel (1 or 2 layers sharing h_in / z_attr) against the oracle AADLayer."""
+    import ctypes as C
+    from ghost_amd import _lib
+    from ghost_amd.network.pack import pack_aad_v3
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(c_x * 3 + n + L)
+    h = (torch.randn(B, c_x, n, n, generator=g) * 1.5 + 0.7).to(dt).float()
+    za = torch.randn(B, c_a, n, n, generator=g).to(dt).float()
+    zi = torch.randn(B, 512, generator=g)
+    hd, zad = nhwc(h).to(dt).to(DEV), nhwc(za).to(dt).to(DEV)
+    keep, w3s, b3s, whs, bhs, ids, outs, refs = [], [], [], [], [], [], [], []
+    for l in range(L):
+        specs = [(f"v3_{l}.{k}", shp, kind) for k, shp, kind in [
+            ("conv1.weight", (c_x, c_a, 1, 1), "conv"), ("conv1.bias", (c_x,), "bias"),
+            ("conv2.weight", (c_x, c_a, 1, 1), "conv"), ("conv2.bias", (c_x,), "bias"),
+            ("fc1.weight", (c_x, 512), "lin_w"), ("fc1.bias", (c_x,), "bias"),
+            ("fc2.weight", (c_x, 512), "lin_w"), ("fc2.bias", (c_x,), "bias"),
+            ("conv_h.weight", (1, c_x, 1, 1), "conv"), ("conv_h.bias", (1,), "bias")]]
+        p = {k: v.to(dt).float() for k, v in aei_ref.make_weights(specs).items()}
+        refs.append(F.relu(aei_ref.aad_layer(h, za, zi, p, f"v3_{l}")))
+        pk = pack_aad_v3({k: v.to(DEV) for k, v in p.items()}, f"v3_{l}", dt)
+        idgb = torch.cat([F.linear(zi, p[f"v3_{l}.fc1.weight"], p[f"v3_{l}.fc1.bias"]),
+                          F.linear(zi, p[f"v3_{l}.fc2.weight"], p[f"v3_{l}.fc2.bias"])], 1).to(DEV).contiguous()
+        wh = p[f"v3_{l}.conv_h.weight"].reshape(c_x).to(DEV).contiguous()
+        bh = p[f"v3_{l}.conv_h.bias"].reshape(1).to(DEV).contiguous()
+        out = torch.empty(B, n, n, c_x, dtype=dt, device=DEV)
+        keep += [pk, idgb, wh, bh, out]
+        w3s.append(pk["w3"].data_ptr()); b3s.append(pk["b3"].data_ptr()); whs.append(wh.data_ptr())
+        bhs.append(bh.data_ptr()); ids.append(idgb.data_ptr()); outs.append(out.data_ptr())
+    arr = lambda xs: (C.c_void_p * L)(*xs)  # noqa: E731
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=DEV)
+    _lib.check(lib.ghost_aad_layers_v3_nhwc(hd.data_ptr(), c_x, zad.data_ptr(), c_a, B, n, n, c_x, c_a, L, arr(w3s),
+                                            arr(b3s), arr(whs), arr(bhs), arr(ids), 2 * c_x, 0.0, arr(outs),
+                                            (C.c_int * L)(*([c_x] * L)), ws.data_ptr(), ws.numel(), stream(lib)))
+    for l in range(L):
+        got = keep[5 * l + 4].float().cpu().permute(0, 3, 1, 2)
+        ref = refs[l]
+        err = float((got - ref).abs().max())
+        assert err <= 4e-2 * max(1.0, float(ref.abs().max())), (l, err)
+        assert float((got - ref).abs().mean()) <= 2e-3 * max(1.0, float(ref.abs().mean()))
