@@ -355,6 +355,179 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// v2: bf16 implicit GEMM staged by LDS-DMA (global_load_lds_dwordx4) through a STAGES-deep
+// ring with counted vmcnt waits and raw barriers (cdna_hip_programming.md §5 "Pipelining
+// across barriers").  No register staging: the K loop issues one DMA per 16 tile rows and
+// the MFMAs; zero padding comes from DMA reads of a zero line.  LDS rows are 64 B (BK = 32)
+// with chunk c of row r stored at c ^ ((r >> 1) & 3): conflict-free ds_read_b128 for the
+// 16x16x32 fragments, applied on the DMA *source* side (the LDS image is lane-linear).
+// ---------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) unsigned int g_zero_line[64] = {0};
+
+GHOST_DEV int swz(int r, int c) { return c ^ ((r >> 1) & 3); }
+
+template <int N>
+GHOST_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// issue the LDS-DMA of K tile `kt` into ring slot `sb` (one 16-row piece per instruction)
+template <int BM, int NA, int NB>
+GHOST_DEV void glds_issue(const ConvArgs& a, const bf16* __restrict__ x, const bf16* const (&b_src)[NB],
+                          const long (&a_off)[NA], const unsigned (&a_mask)[NA], const int (&a_gc)[NA], int wid,
+                          int kt, unsigned char* sb) {
+#if defined(__HIP_DEVICE_COMPILE__)   // the amdgcn builtin does not exist in the host pass of this TU
+  const int k0 = kt * 32;
+  const int tap = k0 / a.Cin;
+  const int ty = tap / a.ntx, tx = tap - ty * a.ntx;
+  const long toff = ((long)a.tsign * ty * a.Wi + a.tsign * tx) * a.ldx + (k0 - tap * a.Cin);
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const void* src = ((a_mask[j] >> tap) & 1u) ? (const void*)(x + a_off[j] + toff + a_gc[j])
+                                                 : (const void*)g_zero_line;
+    __builtin_amdgcn_global_load_lds(src, sb + (wid * NA + j) * 1024, 16, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+    __builtin_amdgcn_global_load_lds(b_src[j] + k0, sb + BM * 64 + (wid * NB + j) * 1024, 16, 0, 0);
+#endif
+}
+
+template <int BM, int BN, int STAGES, int EPI>
+__global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
+  typedef bf16 TI;
+  typedef bf16 TO;
+  constexpr int WM = WaveGrid<BM, BN>::WM, WN = WaveGrid<BM, BN>::WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int NA = BM / 64, NB = BN / 64;        // DMA instructions per wave per stage (16 rows each)
+  constexpr int LPS = NA + NB;
+  constexpr int STAGE_B = (BM + BN) * 64;          // bytes per stage
+  static_assert(BM % 64 == 0 && BN % 64 == 0 && EPI != KEPI_AAD, "v2 tile");
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[STAGES * STAGE_B];
+
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = tile % a.nNt, mt = tile / a.nNt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int split = blockIdx.y, par = blockIdx.z, py = par >> 1, px = par & 1;
+  const TI* __restrict__ x = reinterpret_cast<const TI*>(a.x);
+  const TI* __restrict__ w = reinterpret_cast<const TI*>(a.w) + par * a.wpar_stride;
+  const int nk = a.Kpad / 32;
+  const int kt0 = split * a.kt_per_split;
+  const int kt1 = min(nk, kt0 + a.kt_per_split);
+
+  // this lane's DMA rows: A rows 16*(wid*NA + j) + lane/4, B rows 16*(wid*NB + j) + lane/4
+  const int lrow = lane >> 2, pc = lane & 3;
+  const int HoWo = a.Ho * a.Wo;
+  const int tby = a.deconv ? py : a.tbase, tbx = a.deconv ? px : a.tbase;
+  const int nty = a.K / (a.Cin * a.ntx);
+  long a_off[NA];
+  unsigned a_mask[NA];
+  int a_gc[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int r = 16 * (wid * NA + j) + lrow;
+    const int m = m0 + r;
+    a_gc[j] = swz(r, pc) * 8;
+    a_off[j] = 0;
+    a_mask[j] = 0u;
+    if (m < a.M) {
+      const int b = m / HoWo;
+      const int rr = m - b * HoWo;
+      const int oy = rr / a.Wo, ox = rr - oy * a.Wo;
+      const int iyb = oy * a.stride + tby, ixb = ox * a.stride + tbx;
+      a_off[j] = ((long)(b * a.Hi + iyb) * a.Wi + ixb) * a.ldx;
+      unsigned mk = 0u;
+      for (int ty = 0; ty < nty; ++ty) {
+        const int iy = iyb + a.tsign * ty;
+        if (iy < 0 || iy >= a.Hi) continue;
+        for (int tx = 0; tx < a.ntx; ++tx) {
+          const int ix = ixb + a.tsign * tx;
+          if (ix >= 0 && ix < a.Wi) mk |= 1u << (ty * a.ntx + tx);
+        }
+      }
+      a_mask[j] = mk;
+    }
+  }
+  const TI* b_src[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int r = 16 * (wid * NB + j) + lrow;
+    b_src[j] = w + (long)(n0 + r) * a.Kpad + swz(r, pc) * 8;
+  }
+
+  const int wm = wid / WN, wn = wid % WN;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int n = kt1 - kt0;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < n) glds_issue<BM, NA, NB>(a, x, b_src, a_off, a_mask, a_gc, wid, kt0 + s, lds + s * STAGE_B);
+  for (int it = 0; it < n; ++it) {
+    // stages issued after `it` that may stay in flight
+    const int after = min(STAGES - 2, n - 1 - it);
+    if constexpr (STAGES >= 4) {
+      if (after >= 2) wait_vmcnt<2 * LPS>();
+      else if (after == 1) wait_vmcnt<LPS>();
+      else wait_vmcnt<0>();
+    } else {
+      if (after >= 1) wait_vmcnt<LPS>();
+      else wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + STAGES - 1 < n)
+      glds_issue<BM, NA, NB>(a, x, b_src, a_off, a_mask, a_gc, wid, kt0 + it + STAGES - 1,
+                             lds + ((it + STAGES - 1) % STAGES) * STAGE_B);
+    const unsigned char* sb = lds + (it % STAGES) * STAGE_B;
+    const unsigned char* As = sb;
+    const unsigned char* Bs = sb + BM * 64;
+    bf16x8 af[TM], bfv[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * WTM + i * 16 + lr;
+      af[i] = *reinterpret_cast<const bf16x8*>(As + r * 64 + swz(r, lq) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int r = wn * WTN + j * 16 + lr;
+      bfv[j] = *reinterpret_cast<const bf16x8*>(Bs + r * 64 + swz(r, lq) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+  }
+
+  // ---- epilogue (as v1) ----
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
+      if (m >= a.M) continue;
+      if constexpr (EPI == KEPI_SPLIT) {
+        float* dst = a.partial + (((long)par * a.nsplit + split) * a.M + m) * a.NT;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) dst[n0 + wn * WTN + j * 16 + lr] = acc[i][j][r];
+      } else {
+        const long op = out_pixel(a, m, py, px);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int nn = n0 + wn * WTN + j * 16 + lr;
+          if (nn < a.N) store_std<TO>(a, epi_std<TO>(a, acc[i][j][r], nn, op), nn, op);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host side: tile choice, split-K heuristic, dispatch
 // ---------------------------------------------------------------------------
 namespace {
@@ -492,9 +665,39 @@ int dispatch_tile(const ConvArgs& a, const Plan& p, hipStream_t s) {
 #undef GHOST_TILE
 }
 
+template <int EPI>
+bool launch_glds(const ConvArgs& a, const Plan& p, hipStream_t s) {
+  static const int stages = env_int("GHOST_CONV_STAGES", 3);
+  dim3 grid(p.nMt * p.nNt, p.nsplit, p.npar);
+#define GHOST_G(bm, bn, st)                                                                      \
+  if (p.BM == bm && p.BN == bn && stages == st) {                                                \
+    hipLaunchKernelGGL((conv_glds_kernel<bm, bn, st, EPI>), grid, dim3(256), 0, s, a);           \
+    return true;                                                                                  \
+  }
+  GHOST_G(128, 128, 4) GHOST_G(256, 64, 4) GHOST_G(128, 64, 4) GHOST_G(64, 128, 4)
+  GHOST_G(128, 128, 3) GHOST_G(256, 64, 3) GHOST_G(128, 64, 3) GHOST_G(64, 128, 3)
+#undef GHOST_G
+  return false;
+}
+
 template <typename TI, typename TO>
 int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStream_t s) {
   int rc;
+  static const int use_v2 = env_int("GHOST_CONV_V2", 1);
+  if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
+    // measured (tools/bench_ops.py): the DMA ring wins on the 128-row tiles, loses on 256x64
+    if (use_v2 && p.fast && p.BK == 32 && d.epi != EPI_AAD && p.BM <= 128) {
+      const bool ok = p.nsplit > 1 ? launch_glds<KEPI_SPLIT>(a, p, s) : launch_glds<KEPI_STD>(a, p, s);
+      if (ok) {
+        if (p.nsplit > 1) {
+          const long total = (long)p.M * d.N;
+          dim3 grid((unsigned)((total + 255) / 256), 1, p.npar);
+          hipLaunchKernelGGL((splitk_reduce_kernel<TO, KEPI_STD>), grid, dim3(256), 0, s, a);
+        }
+        return 0;
+      }
+    }
+  }
   if (p.nsplit > 1) {
     rc = p.fast ? dispatch_tile<TI, TO, KEPI_SPLIT, true>(a, p, s) : dispatch_tile<TI, TO, KEPI_SPLIT, false>(a, p, s);
     if (rc) return rc;
