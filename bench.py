@@ -9,9 +9,13 @@ then (N > 1) an RCCL all-gather of every rank's swapped crops (frame order = ran
 Weak scaling: B frames per GPU; value = N*B*K / max-over-ranks wall time of the K timed steps.
 
 Besides the JSON line's throughput, it reports
-* roofline: the AAD-layer GEMM (fused IN-normalise / gamma-beta / sigmoid-mask blend) at the
-  256x256 stage, HBM-bound: algorithmic bytes |h_in|+|z_attr|+|out| per launch / its average
-  launch time (HIP events around each launch on the launch stream, inside the timed region);
+* roofline: the dominant AAD kernel, aad_v3_kernel<64,64,2> (the two AADLayers of AADBlk8 that
+  read the same h_in / z_attr at 256x256), HBM-bound: its algorithmic bytes |h_in| + |z_attr| +
+  2|out| per launch / its average launch time, timed with HIP events recorded around each of its
+  launches on the launch stream inside the timed region; `traffic` = PMC-measured HBM bytes per
+  launch of the same kernel from profiles/traffic_latest.json;
+* roofline_conv3x3 (MFMA-bound, all generator 3x3 convs) and aad_decoder_gbs (SURVEY.md §8d
+  definition: 135.58 MB/frame of AADLayer bytes / total AAD kernel time);
 * cpu_baseline: the CPU restatement (oracle/aei_ref.py, fp32, same ATen op sequence as the
   reference) on this host's cores over a bounded sample (rank 0, N=1 only).
 """
@@ -47,6 +51,21 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     return ap.parse_args()
+
+
+def pmc_traffic(kernel_substr):
+    """HBM bytes per launch of a kernel from the committed PMC summary (tools/pmc_traffic.py over
+    separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 FETCH x2 correction)."""
+    path = os.path.join(REPO, "profiles", "traffic_latest.json")
+    try:
+        data = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    for k in data.get("kernels", []):
+        if kernel_substr in k["kernel"] and k.get("hbm_bytes"):
+            return {"bytes_per_launch": k["hbm_bytes"], "read": k["read_bytes"], "write": k["write_bytes"],
+                    "source": "profiles/traffic_latest.json (" + data.get("source", "rocprofv3 --pmc") + ")"}
+    return None
 
 
 def cpu_baseline(backbone, nb, seconds):
@@ -105,7 +124,7 @@ def main():
     torch.cuda.synchronize()
     prof = not a.no_profile
     if prof:
-        G.profile(0b1111111)
+        G.profile(0xFF)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -123,7 +142,8 @@ def main():
 
     classes = {}
     if prof:
-        names = ["aad_gemm_all", "aad_gemm_256", "conv3x3_all", "conv3x3_256", "in_stats_mask", "encoder", "upsample"]
+        names = ["aad_all", "aad_dual_256", "conv3x3_all", "conv3x3_256", "in_stats_mask", "encoder", "upsample",
+                 "id_proj"]
         for i, n in enumerate(names):
             classes[n] = G.profile_read(i)
         G.profile(0)
@@ -142,22 +162,29 @@ def main():
                        "global_batch": world * B, "per_gpu_batch": B, "backbone": a.backbone,
                        "num_blocks": a.num_blocks, "parallelism": f"dp{world}"},
         }
-        if prof and classes["aad_gemm_256"]["launches"]:
-            c = classes["aad_gemm_256"]
+        if prof and classes["aad_dual_256"]["launches"]:
+            c = classes["aad_dual_256"]
             per_launch_bytes = c["bytes"] / c["launches"]
             per_launch_s = c["ms"] / c["launches"] / 1e3
             ach = per_launch_bytes / per_launch_s / 1e9
-            res["roofline"] = {"kernel": "AAD fused GEMM (IN-normalise + gamma/beta + sigmoid-mask blend), 256x256 stage",
+            kname = "aad_v3_kernel<64, 64, 2>"
+            res["roofline"] = {"kernel": f"{kname}: two AADLayers sharing h_in/z_attr at 256x256 (IN-normalise, "
+                                         "sigmoid mask, MFMA gamma/beta, blend, ReLU)",
                                "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                               "bytes_per_launch": per_launch_bytes, "avg_launch_us": round(per_launch_s * 1e6, 2)}
+                               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kname),
+                               "bytes_per_launch": per_launch_bytes, "avg_launch_us": round(per_launch_s * 1e6, 2),
+                               "launches_timed": c["launches"]}
             cc = classes["conv3x3_all"]
             if cc["launches"]:
                 tf = cc["flops"] / (cc["ms"] / 1e3) / 1e12
                 res["roofline_conv3x3"] = {"bound": "mfma", "achieved": round(tf, 1), "peak": BF16_PEAK_TFLOPS,
                                            "unit": "TFLOP/s", "frac": round(tf / BF16_PEAK_TFLOPS, 4)}
-            aad = classes["aad_gemm_all"]
-            res["aad_decoder_gbs"] = round(aad["bytes"] / (aad["ms"] / 1e3) / 1e9, 1) if aad["ms"] else None
+            aad = classes["aad_all"]
+            if aad["ms"]:
+                # SURVEY.md §8d definition: sum over AADLayers of |h_in|+|z_attr|+|out| / AAD kernel time
+                res["aad_decoder_gbs"] = round(AAD_BYTES_PER_FRAME[a.backbone] * B * a.steps
+                                               / (aad["ms"] / 1e3) / 1e9, 1)
+                res["aad_decoder_hbm_frac"] = round(res["aad_decoder_gbs"] / HBM_PEAK_GBS, 4)
             res["kernel_ms_per_step"] = {k: round(v["ms"] / a.steps, 3) for k, v in classes.items()}
         if world == 1 and a.cpu_seconds > 0:
             res["cpu_baseline"] = cpu_baseline(a.backbone, a.num_blocks, a.cpu_seconds)

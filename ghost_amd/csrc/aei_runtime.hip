@@ -292,9 +292,8 @@ void aad(Ctx& c, const std::string& name, const void* hin, int ldh, const float*
   const float* bh = (const float*)c.W(name + ".bh");
   if (aad_fused_supported(h->dt, B, n * n, C, Ca, lda, ldh, ldo)) {
     if (!c.ok() || c.dry) return;
-    const bool big = n == 256;
     int e_all = c.prof_begin(0);
-    int e_big = big ? c.prof_begin(1) : -1;
+    int e_big = -1;
     c.check(aad_fused(h->dt, za, lda, Ca, gbw, rup(Ca, 32), gbb, hin, ldh, stat, wh, bh, idgb + id_off, h->id_total,
                       out, ldo, B, n * n, C, 0.0f, c.s),
             "aad_fused");
@@ -316,7 +315,7 @@ void aad(Ctx& c, const std::string& name, const void* hin, int ldh, const float*
   d.epi = EPI_AAD;
   d.hin = hin; d.ldh = ldh; d.stat = stat;
   d.idgb = idgb ? idgb + id_off : nullptr; d.id_ld = h->id_total; d.mask = mask; d.C_aad = C;
-  run_conv(c, d, 0, 1, flops);
+  run_conv(c, d, 0, -1, flops);
 }
 
 struct AadOut {
@@ -358,7 +357,7 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     const double bytes = Pn * (C + Ca + (double)d.L * C) * h->esz;   // |h_in| + |z_attr| + L |out|
     const double flops = 2.0 * Pn * 2.0 * C * Ca * d.L;
     int e_all = c.prof_begin(0);
-    int e_big = n == 256 ? c.prof_begin(1) : -1;
+    int e_big = (n == 256 && d.L == 2) ? c.prof_begin(1) : -1;   // class 1: the dual-layer kernel at 256x256
     c.check(aad_v3(d, c.s), "aad_v3");
     if (e_big >= 0) c.prof_end(1, e_big, bytes, flops);
     if (e_all >= 0) c.prof_end(0, e_all, bytes, flops);

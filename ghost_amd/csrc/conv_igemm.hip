@@ -35,7 +35,7 @@ struct ConvArgs {
   int N, Kpad, K, NT;   // NT = padded channel extent covered by tiles
   int nNt;              // number of channel tiles
   int ldy, ldres, ldh, id_ld, C_aad;
-  int stride, ntx, tbase, tsign;   // input coord = out*stride + tbase + tsign*tap  (per dim)
+  int stride, ntx, ntaps, tbase, tsign;   // input coord = out*stride + tbase + tsign*tap  (per dim)
   int deconv;           // 1: four parity phases in blockIdx.z, output pixel (2qy+py, 2qx+px)
   int nsplit, kt_per_split;
   float slope;
@@ -189,9 +189,13 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK;
     if constexpr (FAST) {
-      const int tap = k0 / a.Cin;                       // the BK slice lies inside one tap
+      // K is ordered (channel block of 32, tap, channel): a block's nine (or 16 / 4) taps are
+      // consecutive K steps, so a tile re-reads the same few input rows from L1/L2 instead of
+      // sweeping all channels once per tap (pack.py pack_conv)
+      const int chunk = (k0 + cch * VEC) >> 5;
+      const int cb = chunk / a.ntaps, tap = chunk - cb * a.ntaps;
       const int ty = tap / a.ntx, tx = tap - ty * a.ntx;
-      const long toff = ((long)a.tsign * ty * a.Wi + a.tsign * tx) * a.ldx + (k0 - tap * a.Cin) + cch * VEC;
+      const long toff = ((long)a.tsign * ty * a.Wi + a.tsign * tx) * a.ldx + cb * 32 + ((cch * VEC) & 31);
 #pragma unroll
       for (int p = 0; p < AP; ++p) {
         if ((a_mask[p] >> tap) & 1u)
@@ -378,9 +382,9 @@ GHOST_DEV void glds_issue(const ConvArgs& a, const bf16* __restrict__ x, const b
                           int kt, unsigned char* sb) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the amdgcn builtin does not exist in the host pass of this TU
   const int k0 = kt * 32;
-  const int tap = k0 / a.Cin;
+  const int cb = kt / a.ntaps, tap = kt - cb * a.ntaps;    // K order (channel block, tap, channel)
   const int ty = tap / a.ntx, tx = tap - ty * a.ntx;
-  const long toff = ((long)a.tsign * ty * a.Wi + a.tsign * tx) * a.ldx + (k0 - tap * a.Cin);
+  const long toff = ((long)a.tsign * ty * a.Wi + a.tsign * tx) * a.ldx + cb * 32;
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
     const void* src = ((a_mask[j] >> tap) & 1u) ? (const void*)(x + a_off[j] + toff + a_gc[j])
@@ -614,9 +618,10 @@ ConvArgs make_args(const ConvDesc& d, const Plan& p, float* partial) {
   a.N = d.N; a.Kpad = d.Kpad; a.NT = p.NT; a.nNt = p.nNt;
   a.ldy = d.ldy; a.ldres = d.ldres; a.ldh = d.ldh; a.id_ld = d.id_ld; a.C_aad = d.C_aad;
   if (d.kind == CONV_T4S2) {
-    a.K = 4 * d.Cin; a.stride = 1; a.ntx = 2; a.tbase = 0; a.tsign = -1; a.deconv = 1;
+    a.K = 4 * d.Cin; a.stride = 1; a.ntx = 2; a.ntaps = 4; a.tbase = 0; a.tsign = -1; a.deconv = 1;
   } else {
-    a.K = d.kh * d.kw * d.Cin; a.stride = d.stride; a.ntx = d.kw; a.tbase = -d.pad; a.tsign = 1; a.deconv = 0;
+    a.K = d.kh * d.kw * d.Cin; a.stride = d.stride; a.ntx = d.kw; a.ntaps = d.kh * d.kw; a.tbase = -d.pad;
+    a.tsign = 1; a.deconv = 0;
   }
   a.nsplit = p.nsplit; a.kt_per_split = p.kt_per_split;
   a.slope = d.slope; a.tanh_out = d.tanh_out;

@@ -1,0 +1,79 @@
+"""Data-parallel frame sharding for the swap path, one process per GPU.
+
+The reference runs every frame of an identity through G on one GPU in batches of BS
+(utils/inference/core.py:57-88).  Frames are independent inside G (eval BatchNorm,
+per-sample InstanceNorm), so the build shards them:
+
+* rank r of W swaps the contiguous block of present crops ``[r*S, min(N, (r+1)*S))`` with
+  ``S = ceil(N / W)`` (the last block padded to S so every rank contributes equal bytes);
+* one all-gather over the process group (RCCL over xGMI on MI355X, gloo in the CPU tests)
+  returns every rank's uint8 swaps; because blocks are contiguous and gathered in rank
+  order, trimming the padding restores frame order exactly;
+* the ``present`` bookkeeping of core.py:79-88 then re-inserts ``[]`` for frames without
+  a face, bit-exactly as the single-GPU path.
+
+No collective other than that all-gather is on the data path.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .core import reinsert_present
+
+
+def shard_bounds(n: int, world: int, rank: int):
+    """[start, end) of rank's contiguous block and the padded per-rank size S = ceil(n / world)."""
+    per = (n + world - 1) // world if n else 0
+    start = min(n, rank * per)
+    return start, min(n, start + per), per
+
+
+def gather_frames(local: torch.Tensor, per: int, n: int, group=None) -> torch.Tensor:
+    """All-gather each rank's [<=per, ...] uint8 block (padded to per) and return the first n rows in order."""
+    world = dist.get_world_size(group)
+    pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]] = local
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, pad, group=group)
+    else:
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        out = torch.cat(parts, 0)
+    return out[:n]
+
+
+def swap_frames_dp(crops: torch.Tensor, swap: Callable[[torch.Tensor], torch.Tensor], BS: int = 64,
+                   group=None) -> torch.Tensor:
+    """Shard N crops [N,256,256,3] (uint8, identical on every rank) over the group, swap this
+    rank's block in batches of BS with ``swap`` (crops -> uint8 swaps), all-gather; every rank
+    returns the N swapped crops in frame order."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    n = crops.shape[0]
+    start, end, per = shard_bounds(n, world, rank)
+    outs = [swap(crops[i:min(end, i + BS)]) for i in range(start, end, BS)]
+    local = torch.cat(outs, 0) if outs else crops[:0].clone()
+    return gather_frames(local, per, n, group)
+
+
+def model_inference_dp(resized_frs: np.ndarray, present: Sequence[int], source_embed: torch.Tensor, G,
+                       BS: int = 64, device=None, group=None) -> List:
+    """core.py:57-88 for one identity, data-parallel over the group: returns the per-frame list
+    (swapped crop or ``[]``) on every rank."""
+    device = torch.device(device or "cuda")
+    crops = torch.from_numpy(np.ascontiguousarray(resized_frs)).to(device)
+    gathered = swap_frames_dp(crops, lambda c: G.swap_u8(c, source_embed), BS, group)
+    return reinsert_present(gathered.cpu().numpy(), present)
+
+
+def swap_mixed_identities(crops: torch.Tensor, identity_index: torch.Tensor, source_embeds: torch.Tensor, G,
+                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Config 5 (several identities in one batch): each crop carries the index of its source
+    identity; the per-sample z_id rows are gathered on the device and the AAD identity path
+    (fc1/fc2 per sample, AADLayer.py:28-29) handles the mix in one launch sequence."""
+    z = source_embeds.reshape(source_embeds.shape[0], -1).index_select(0, identity_index.to(source_embeds.device))
+    return G.swap_u8(crops, z, out=out)

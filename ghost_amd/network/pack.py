@@ -5,9 +5,10 @@ Slot names are the ones ``ghost_aei_bind`` accepts (see aei_runtime.hip
 ``declare_slots``); INTEGRATION.md documents every layout.
 
 Layouts (Npad = Cout rounded up to 128, Kpad = K rounded up to 32, zero padded):
-  conv  [Cout,Cin,kh,kw]      -> [Npad][Kpad], K = (ky*kw + kx)*Cin + c
+  conv  [Cout,Cin,kh,kw]      -> [Npad][Kpad], K = (cb*kh*kw + ky*kw + kx)*32 + c%32 (cb = c/32) when
+                                 Cin % 32 == 0, else (ky*kw + kx)*Cin + c
   conv3x3 to <= 3 channels    -> also [32][Kpad], row = (ky*3 + kx)*Cout + o, K = c  (narrow kernel)
-  convT [Cin,Cout,4,4] (s2p1) -> [4][Npad][Kpad], phase = 2*py+px, K = (ty*2+tx)*Cin + c,
+  convT [Cin,Cout,4,4] (s2p1) -> [4][Npad][Kpad], phase = 2*py+px, K = (cb*4 + ty*2+tx)*32 + c%32,
                                  kernel tap ky = ((1,3),(0,2))[py][ty]  (sub-pixel decomposition)
   AAD conv1/conv2 (1x1)       -> [Npad][Kpad] rows interleaved per 16 channels: gamma c0..15,
                                  beta c0..15, gamma c16..31, ...  (+ the same for the biases)
@@ -42,10 +43,16 @@ def rup(v: int, m: int) -> int:
 
 
 def pack_conv(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """K order (channel block of 32, tap, channel) when Cin % 32 == 0 — consecutive K steps are
+    the taps of one channel block (input-row reuse in L1/L2); (tap, channel) otherwise."""
     co, ci, kh, kw = w.shape
     k = kh * kw * ci
     out = torch.zeros(rup(co, 128), rup(k, 32), dtype=dtype, device=w.device)
-    out[:co, :k] = w.permute(0, 2, 3, 1).reshape(co, k).to(dtype)
+    if ci % 32 == 0:
+        wk = w.reshape(co, ci // 32, 32, kh * kw).permute(0, 1, 3, 2)      # [co][cb][tap][c]
+    else:
+        wk = w.permute(0, 2, 3, 1)                                          # [co][ky][kx][c]
+    out[:co, :k] = wk.reshape(co, k).to(dtype)
     return out
 
 
@@ -64,7 +71,10 @@ def pack_convT4x4(w: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     for py in range(2):
         for px in range(2):
             taps = [w[:, :, _KTAP[py][ty], _KTAP[px][tx]].t() for ty in range(2) for tx in range(2)]
-            out[2 * py + px, :co, :4 * ci] = torch.stack(taps, 1).reshape(co, 4 * ci).to(dtype)
+            blk = torch.stack(taps, 1)                                      # [co][tap][ci]
+            if ci % 32 == 0:
+                blk = blk.reshape(co, 4, ci // 32, 32).permute(0, 2, 1, 3)  # [co][cb][tap][c]
+            out[2 * py + px, :co, :4 * ci] = blk.reshape(co, 4 * ci).to(dtype)
     return out
 
 

@@ -78,8 +78,9 @@ int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_str
                       void* stream);
 
 /* per-kernel-class device timing with HIP events (bench instrumentation).
- * class_mask bit i enables class i; classes: 0 AAD GEMM (all stages), 1 AAD GEMM at
- * 256x256, 2 conv3x3 (all), 3 conv3x3 at 256x256, 4 IN stats + mask, 5 encoder, 6 upsample. */
+ * class_mask bit i enables class i; classes: 0 AAD kernels (all stages), 1 the dual-layer AAD
+ * kernel at 256x256 (aad_v3<64,64,2>), 2 conv3x3 (all), 3 conv3x3 at 256x256, 4 IN stats + mask,
+ * 5 encoder, 6 upsample, 7 identity projections. */
 int ghost_aei_profile(ghost_aei* h, int class_mask);
 /* after the stream is synchronised: total ms, launches, algorithmic bytes and flops of class i */
 int ghost_aei_profile_read(ghost_aei* h, int cls, double* ms, int64_t* launches, double* bytes, double* flops);

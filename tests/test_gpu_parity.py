@@ -413,3 +413,17 @@ def test_aad_layers_v3_vs_oracle(lib, c_x, c_a, n, B, L):
         err = float((got - ref).abs().max())
         assert err <= 4e-2 * max(1.0, float(ref.abs().max())), (l, err)
         assert float((got - ref).abs().mean()) <= 2e-3 * max(1.0, float(ref.abs().mean()))
+
+
+def test_mixed_identity_batch_and_dp_single_rank(lib):
+    """Config 5 path: per-sample identity rows in one launch sequence == per-identity batches."""
+    from ghost_amd.inference.dp import swap_mixed_identities
+    G = model("unet", 2)
+    crops = torch.from_numpy(aei_ref.make_u8_crops(4, 9)).to(DEV)
+    _, z = aei_ref.make_inputs(2, 9)
+    z = z.to(DEV)
+    idx = torch.tensor([0, 1, 0, 1], device=DEV)
+    mixed = swap_mixed_identities(crops, idx, z, G).cpu().int()
+    a = G.swap_u8(crops[0::2].contiguous(), z[0:1]).cpu().int()
+    b = G.swap_u8(crops[1::2].contiguous(), z[1:2]).cpu().int()
+    assert int((mixed[0::2] - a).abs().max()) <= 1 and int((mixed[1::2] - b).abs().max()) <= 1

@@ -64,11 +64,11 @@ def test_create_rejects_bad_arguments(lib):
 
 
 def _gemm_conv(x, wp, cout, k, stride, pad):
-    """Replay the implicit GEMM on CPU: rows = output pixels, K = (ky, kx, c)."""
+    """Replay the implicit GEMM on CPU: rows = output pixels, K = (channel block, tap, c)."""
     B, Cin, H, W = x.shape
     cols = F.unfold(x, k, padding=pad, stride=stride)          # [B, Cin*k*k, L] with (c, ky, kx) order
     L = cols.shape[-1]
-    cols = cols.reshape(B, Cin, k * k, L).permute(0, 3, 2, 1).reshape(B, L, k * k * Cin)  # (ky,kx,c)
+    cols = cols.reshape(B, Cin // 32, 32, k * k, L).permute(0, 4, 1, 3, 2).reshape(B, L, k * k * Cin)
     y = cols @ wp[:cout, :k * k * Cin].t()
     Ho = (H + 2 * pad - k) // stride + 1
     return y.reshape(B, Ho, -1, cout).permute(0, 3, 1, 2)
@@ -86,7 +86,7 @@ def test_pack_conv_layout():
 
 def test_pack_convT_subpixel_layout():
     g = torch.Generator().manual_seed(1)
-    ci, co, H = 16, 24, 5
+    ci, co, H = 64, 24, 5
     x = torch.randn(2, ci, H, H, generator=g, dtype=torch.float64)
     w = torch.randn(ci, co, 4, 4, generator=g, dtype=torch.float64)
     wp = pack.pack_convT4x4(w, torch.float64)
@@ -100,7 +100,8 @@ def test_pack_convT_subpixel_layout():
                 for tx in range(2):
                     dy, dx = py - ty, px - tx           # input offset = parity - tap (kernel tbase/tsign)
                     patch = xp[:, :, 1 + dy:1 + dy + H, 1 + dx:1 + dx + H]
-                    wt = wp[2 * py + px, :co, (ty * 2 + tx) * ci:(ty * 2 + tx + 1) * ci]
+                    t = ty * 2 + tx     # K order (cb, tap, c): gather this tap's channels block by block
+                    wt = wp[2 * py + px, :co, :4 * ci].reshape(co, ci // 32, 4, 32)[:, :, t, :].reshape(co, ci)
                     acc += torch.einsum("bchw,oc->bohw", patch, wt)
             out[:, :, py::2, px::2] = acc
     torch.testing.assert_close(out, ref)

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("fetch")
     ap.add_argument("write")
     ap.add_argument("--out")
+    ap.add_argument("--source", default="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes")
     a = ap.parse_args()
     f = load(a.fetch, "FETCH_SIZE")
     w = load(a.write, "WRITE_SIZE")
@@ -48,7 +49,7 @@ def main():
               f"write {r['write_bytes'] or 0:14.0f}  {r['kernel'][:90]}")
     if a.out:
         json.dump({"correction": "read = 2*FETCH_SIZE*1024 (gfx950 half-count), write = WRITE_SIZE*1024",
-                   "kernels": rows}, open(a.out, "w"), indent=1)
+                   "source": a.source, "kernels": rows}, open(a.out, "w"), indent=1)
 
 
 if __name__ == "__main__":
