@@ -112,6 +112,35 @@ def stats_cases(lib, iters, dt=torch.bfloat16):
         print(f"stats C={C} n={n} {us:9.1f} us  {x.numel() * x.element_size() / us / 1e3:7.1f} GB/s", flush=True)
 
 
+def ceiling_cases(iters, dt=torch.bfloat16):
+    """Library ceilings on the same work: hipBLASLt GEMM of the im2col shape and MIOpen conv."""
+    import torch.nn.functional as F
+    B = 64
+    for name, H, ci, co in [("gen256 64->64", 256, 64, 64), ("gen128 128->128", 128, 128, 128),
+                            ("gen64 256->256", 64, 256, 256), ("gen64 cat512->128", 64, 512, 128),
+                            ("gen32 512->512", 32, 512, 512)]:
+        M, N, K = B * H * H, co, ci * 9
+        a = torch.randn(M, K, device=DEV).to(dt)
+        b = torch.randn(K, N, device=DEV).to(dt)
+        us = timeit(lambda: torch.matmul(a, b), iters)
+        fl = 2.0 * M * N * K
+        print(f"blas  {name:22s} M={M} N={N} K={K} {us:9.1f} us  {fl / us / 1e6:7.1f} TF/s", flush=True)
+        del a, b
+        x = torch.randn(B, ci, H, H, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+        w = (torch.randn(co, ci, 3, 3, device=DEV) * 0.05).to(dt).contiguous(memory_format=torch.channels_last)
+        try:
+            us = timeit(lambda: F.conv2d(x, w, padding=1), iters)
+            print(f"miopen {name:21s} {us:9.1f} us  {fl / us / 1e6:7.1f} TF/s", flush=True)
+        except RuntimeError as e:   # noqa: BLE001
+            print(f"miopen {name}: {e}")
+        del x, w
+    for n in (8192,):
+        a = torch.randn(n, n, device=DEV).to(dt)
+        b = torch.randn(n, n, device=DEV).to(dt)
+        us = timeit(lambda: torch.matmul(a, b), iters)
+        print(f"blas  square {n} {us:9.1f} us  {2.0 * n ** 3 / us / 1e6:7.1f} TF/s", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
@@ -119,6 +148,8 @@ def main():
     a = ap.parse_args()
     lib = _lib.load()
     print("env:", {k: v for k, v in os.environ.items() if k.startswith("GHOST_")})
+    if a.only == "ceil":
+        ceiling_cases(a.iters)
     if a.only in ("", "conv"):
         conv_cases(lib, a.iters)
     if a.only in ("", "aad"):
