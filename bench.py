@@ -9,9 +9,11 @@ then (N > 1) an RCCL all-gather of every rank's swapped crops (frame order = ran
 Weak scaling: B frames per GPU; value = N*B*K / max-over-ranks wall time of the K timed steps.
 
 Besides the JSON line's throughput, it reports
-* roofline: the dominant AAD kernel, aad_v3_kernel<64,64,2> (the two AADLayers of AADBlk8 that
-  read the same h_in / z_attr at 256x256), HBM-bound: its algorithmic bytes |h_in| + |z_attr| +
-  2|out| per launch / its average launch time, timed with HIP events recorded around each of its
+* roofline: the dominant AAD kernel, aad_v3_kernel<64,64,2,true> (the two AADLayers of AADBlk8 that
+  read the same h_in / z_attr at 256x256, h_in sampled through the bilinear x2 upsample of AADBlk7's
+  128x128 output), HBM-bound: its algorithmic bytes per launch by SURVEY.md §8d's formula (fixed
+  regardless of fusion: sum over its two AADLayers of |h_in| + |z_attr| + |out|, 64 frames at
+  256x256x64 bf16 = 3.22 GB) / its average launch time, timed with HIP events recorded around each of its
   launches on the launch stream inside the timed region; `traffic` = PMC-measured HBM bytes per
   launch of the same kernel from profiles/traffic_latest.json;
 * roofline_conv3x3 (MFMA-bound, all generator 3x3 convs) and aad_decoder_gbs (SURVEY.md §8d
@@ -167,9 +169,10 @@ def main():
             per_launch_bytes = c["bytes"] / c["launches"]
             per_launch_s = c["ms"] / c["launches"] / 1e3
             ach = per_launch_bytes / per_launch_s / 1e9
-            kname = "aad_v3_kernel<64, 64, 2>"
-            res["roofline"] = {"kernel": f"{kname}: two AADLayers sharing h_in/z_attr at 256x256 (IN-normalise, "
-                                         "sigmoid mask, MFMA gamma/beta, blend, ReLU)",
+            kname = "aad_v3_kernel<64, 64, 2, true>"
+            res["roofline"] = {"kernel": f"{kname}: two AADLayers sharing h_in/z_attr at 256x256, h_in = bilinear "
+                                         "x2 of the 128x128 block output sampled in-kernel (IN-normalise, sigmoid "
+                                         "mask, MFMA gamma/beta, blend, ReLU)",
                                "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kname),
                                "bytes_per_launch": per_launch_bytes, "avg_launch_us": round(per_launch_s * 1e6, 2),

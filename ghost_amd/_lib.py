@@ -55,7 +55,8 @@ _SIGS = {
     "ghost_nhwc_to_nchw": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp]),
     "ghost_crops_to_input_nhwc": (i32, [vp, i64, i32, i32, i32, i32, vp, vp]),
     "ghost_set_split_k": (i32, [i32]),
-    "ghost_aad_layers_v3_nhwc": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp), C.POINTER(vp),
+    "ghost_set_fuse_upsample": (i32, [i32]),
+    "ghost_aad_layers_v3_nhwc": (i32, [vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp), C.POINTER(vp),
                                        C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), i32, f32, C.POINTER(vp),
                                        C.POINTER(i32), vp, i64, vp]),
     "ghost_conv3x3_narrow_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, vp, i32, i32, vp, i32, vp,

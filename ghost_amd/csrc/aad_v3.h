@@ -7,6 +7,9 @@ namespace ghost {
 struct AadV3Desc {
   const void* za = nullptr;  int lda = 0, Ca = 0;   // z_attr NHWC
   const void* hin = nullptr; int ldh = 0;           // h_in NHWC (shared by the L layers)
+  // up_H > 0: h_in = upsample2x(hin) (bilinear x2, align_corners) with hin the [B, up_H, up_W]
+  // source, sampled on the fly (values rounded to bf16 as upsample2x stores them)
+  int up_H = 0, up_W = 0;
   const float* stat = nullptr;                       // [B][C][2] mean, rstd of h_in
   int B = 0, HW = 0, C = 0, L = 1, id_ld = 0;
   float slope = 0.f;

@@ -18,6 +18,7 @@
 // HBM bytes per launch = |h_in| + |z_attr| + L * |out|  (the algorithmic minimum).
 #include "aad_v3.h"
 #include "ghost_common.h"
+#include "up2x.h"
 
 namespace ghost {
 
@@ -34,12 +35,13 @@ struct AadV3Args {
   int ldo[2];
   int lda, ldh, id_ld, HW, PPW;
   float slope;
+  Up2xSrc up;   // UP: h_in is the bilinear x2 upsample of hin (a [B, up.H, up.W] source)
 };
 
 static constexpr int kWaves = 8;
 
-template <int C, int CA, int L>
-__global__ void __launch_bounds__(512) aad_v3_kernel(const AadV3Args a) {
+template <int C, int CA, int L, bool UP>
+GHOST_DEV void aad_v3_body(const AadV3Args& a) {
   constexpr int CT = C / 64;          // 64-channel tiles
   constexpr int KS = CA / 32;         // MFMA k-steps
   constexpr int WLD = CA + 8;         // padded LDS weight row (bf16 elements)
@@ -48,7 +50,8 @@ __global__ void __launch_bounds__(512) aad_v3_kernel(const AadV3Args a) {
   __shared__ __attribute__((aligned(16))) float s_b[L * CT * 128];
   __shared__ __attribute__((aligned(16))) float s_rs[C];
   __shared__ __attribute__((aligned(16))) float s_nm[C];
-  __shared__ __attribute__((aligned(16))) float s_wh[L * C];
+  __shared__ __attribute__((aligned(16))) float s_cf[L * C];     // wh * rstd
+  __shared__ float s_k[L];                                        // sum_c wh * (-mu * rstd)
   __shared__ __attribute__((aligned(16))) float s_gi[L * C];
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
 
@@ -65,7 +68,8 @@ __global__ void __launch_bounds__(512) aad_v3_kernel(const AadV3Args a) {
     }
     for (int idx = tid; idx < CT * 128; idx += kWaves * 64) s_b[l * CT * 128 + idx] = a.b3[l][idx];
     for (int c = tid; c < C; c += kWaves * 64) {
-      s_wh[l * C + c] = a.wh[l][c];
+      const float rs = a.stat[((long)b * C + c) * 2 + 1];
+      s_cf[l * C + c] = a.wh[l][c] * rs;
       s_gi[l * C + c] = a.idgb[l][(long)b * a.id_ld + c];
       s_bi[l * C + c] = a.idgb[l][(long)b * a.id_ld + C + c];
     }
@@ -76,10 +80,19 @@ __global__ void __launch_bounds__(512) aad_v3_kernel(const AadV3Args a) {
     s_nm[c] = -mu * rs;
   }
   __syncthreads();
+  // mask logit = sum_c wh_c * ((h_c - mu_c) * rs_c) + bh = sum_c cf_c * h_c + k + bh: one FMA per channel
+  if (wid < L) {
+    float k = 0.f;
+    for (int c = lane; c < C; c += 64) k = fmaf(a.wh[wid][c], s_nm[c], k);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) k += __shfl_xor(k, o, 64);
+    if (lane == 0) s_k[wid] = k;
+  }
+  __syncthreads();
 
   float bh[L];
 #pragma unroll
-  for (int l = 0; l < L; ++l) bh[l] = a.bh[l][0];
+  for (int l = 0; l < L; ++l) bh[l] = a.bh[l][0] + s_k[l];
 
   // one 16-pixel tile per wave iteration; latency is hidden by the 8 waves of the workgroup
   // and the co-resident workgroups (no software prefetch: it would cost the occupancy)
@@ -92,9 +105,26 @@ __global__ void __launch_bounds__(512) aad_v3_kernel(const AadV3Args a) {
     u32x4 zc[KS], hc[NH];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + ks * 32 + lq * 8);
+    if constexpr (UP) {
+      // the tile's 16 pixels lie on one output row; each chunk is interpolated from the four
+      // source pixels (L1/L2 hits: a source pixel feeds ~4 outputs) and rounded to bf16
+      const int r = (int)(p - (long)b * a.HW);
+      const int oy = r / (2 * a.up.W), ox = r - oy * (2 * a.up.W);
+      const Up2xTap tp = up2x_tap(a.up, oy, ox);
+      const bf16* src = a.hin + (long)b * a.up.H * a.up.W * a.ldh;
 #pragma unroll
-    for (int j = 0; j < NH; ++j)   // chunk j = (ct, s): channels ct*64 + 32s + 8lq .. +7
-      hc[j] = *reinterpret_cast<const u32x4*>(a.hin + p * a.ldh + (j >> 1) * 64 + (j & 1) * 32 + lq * 8);
+      for (int j = 0; j < NH; ++j) {
+        float v[8];
+        up2x_load16_f(src + (j >> 1) * 64 + (j & 1) * 32 + lq * 8, a.ldh, tp, v);
+        bf16* hv = reinterpret_cast<bf16*>(&hc[j]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hv[e] = (bf16)v[e];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NH; ++j)   // chunk j = (ct, s): channels ct*64 + 32s + 8lq .. +7
+        hc[j] = *reinterpret_cast<const u32x4*>(a.hin + p * a.ldh + (j >> 1) * 64 + (j & 1) * 32 + lq * 8);
+    }
 
     // mask partials of every layer over this lane's 8*NH channels, then across the 4 lanes of the pixel
     float ms[L];
@@ -105,11 +135,9 @@ __global__ void __launch_bounds__(512) aad_v3_kernel(const AadV3Args a) {
       const int c0 = (j >> 1) * 64 + (j & 1) * 32 + lq * 8;
       const bf16* hv = reinterpret_cast<const bf16*>(&hc[j]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float hh = fmaf((float)hv[e], s_rs[c0 + e], s_nm[c0 + e]);
+      for (int e = 0; e < 8; ++e)
 #pragma unroll
-        for (int l = 0; l < L; ++l) ms[l] = fmaf(s_wh[l * C + c0 + e], hh, ms[l]);
-      }
+        for (int l = 0; l < L; ++l) ms[l] = fmaf(s_cf[l * C + c0 + e], (float)hv[e], ms[l]);
     }
     float Mk[L];
 #pragma unroll
@@ -122,26 +150,32 @@ __global__ void __launch_bounds__(512) aad_v3_kernel(const AadV3Args a) {
 
 #pragma unroll
     for (int l = 0; l < L; ++l) {
+      asm volatile("" ::: "memory");   // one layer's accumulators live at a time
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         const bf16* W = s_w + (l * CT + ct) * 128 * WLD;
-        f32x4 acc[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          acc[i] = *reinterpret_cast<const f32x4*>(&s_b[(l * CT + ct) * 128 + i * 16 + lq * 4]);
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          bf16x8 bfrag;
-          __builtin_memcpy(&bfrag, &zc[ks], 16);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&W[(i * 16 + lr) * WLD + ks * 32 + lq * 8]);
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i], 0, 0, 0);
-          }
-        }
-        // lane holds gamma (row tiles 2s + e/4) and beta (4 + 2s + e/4) of channels ct*64 + 32s + 8lq + e
+        // half sh: row tiles {2sh, 2sh+1} (gamma) and {4+2sh, 5+2sh} (beta) = channels
+        // ct*64 + 32sh + 8lq + e of this lane's pixel; one half's accumulators live at a time
 #pragma unroll
         for (int sh = 0; sh < 2; ++sh) {
+          asm volatile("" ::: "memory");
+          f32x4 acc[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
+            acc[i] = *reinterpret_cast<const f32x4*>(&s_b[(l * CT + ct) * 128 + rt * 16 + lq * 4]);
+          }
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            bf16x8 bfrag;
+            __builtin_memcpy(&bfrag, &zc[ks], 16);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
+              const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&W[(rt * 16 + lr) * WLD + ks * 32 + lq * 8]);
+              acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i], 0, 0, 0);
+            }
+          }
           const int j = ct * 2 + sh;
           const int c0 = ct * 64 + sh * 32 + lq * 8;
           const bf16* hv = reinterpret_cast<const bf16*>(&hc[j]);
@@ -149,11 +183,11 @@ __global__ void __launch_bounds__(512) aad_v3_kernel(const AadV3Args a) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float hh = fmaf((float)hv[e], s_rs[c0 + e], s_nm[c0 + e]);
-            const float g = acc[2 * sh + (e >> 2)][e & 3];
-            const float be = acc[4 + 2 * sh + (e >> 2)][e & 3];
+            const float g = acc[e >> 2][e & 3];
+            const float be = acc[2 + (e >> 2)][e & 3];
             const float A = fmaf(g, hh, be);
             const float I = fmaf(s_gi[l * C + c0 + e], hh, s_bi[l * C + c0 + e]);
-            const float v = (1.0f - Mk[l]) * A + Mk[l] * I;
+            const float v = fmaf(Mk[l], I - A, A);
             o[e] = v > 0.f ? v : v * a.slope;
           }
           store16_f(a.out[l] + p * a.ldo[l] + c0, o);
@@ -163,9 +197,20 @@ __global__ void __launch_bounds__(512) aad_v3_kernel(const AadV3Args a) {
   }
 }
 
+// C = 64: held to 4 waves per SIMD (<= 128 VGPRs) so two 512-thread workgroups share a CU;
+// C = 128 keeps the compiler's allocation (forcing it spills)
+template <int C, int CA, int L, bool UP>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v3_kernel(const AadV3Args a) {
+  aad_v3_body<C, CA, L, UP>(a);
+}
+template <int C, int CA, int L>
+__global__ void __launch_bounds__(512) aad_v3_wide_kernel(const AadV3Args a) {
+  aad_v3_body<C, CA, L, false>(a);
+}
+
 bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo) {
   if (dt != GHOST_BF16) return false;
-  const bool shape = (C == 64 && (Ca == 64 || Ca == 32)) || (C == 128 && (Ca == 128 || Ca == 64));
+  const bool shape = (C == 64 && (Ca == 64 || Ca == 32)) || (C == 128 && (Ca == 128 || Ca == 64 || Ca == 32));
   if (!shape || lda % 8 || ldh % 8 || ldo % 8) return false;
   const int ppw = HW >= 65536 ? 1024 : 512;
   return HW % ppw == 0 && (long)B * HW / ppw >= 32;
@@ -174,7 +219,7 @@ bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, in
 int aad_v3(const AadV3Desc& d, hipStream_t s) {
   if (!aad_v3_supported(GHOST_BF16, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo[0])) return -1;
   if (d.L == 2 && d.ldo[1] % 8) return -1;
-  if (d.L < 1 || d.L > 2 || (d.L == 2 && d.C != 64)) return -1;   // two layers' weights must fit LDS
+  if (d.L < 1 || d.L > 2 || (d.L == 2 && d.C != 64)) return -1;   // C = 128 pairs spill registers
   AadV3Args a{};
   a.za = (const bf16*)d.za; a.hin = (const bf16*)d.hin; a.stat = d.stat;
   for (int l = 0; l < d.L; ++l) {
@@ -183,14 +228,27 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   }
   a.lda = d.lda; a.ldh = d.ldh; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
   a.PPW = d.HW >= 65536 ? 1024 : 512;
-  dim3 grid((unsigned)((long)d.B * d.HW / a.PPW));
-#define GHOST_V3(c, ca, l)                                                              \
-  if (d.C == c && d.Ca == ca && d.L == l) {                                             \
-    hipLaunchKernelGGL((aad_v3_kernel<c, ca, l>), grid, dim3(kWaves * 64), 0, s, a);            \
-    return (int)hipGetLastError();                                                      \
+  const bool up = d.up_H > 0;
+  if (up) {
+    if (4 * d.up_H * d.up_W != d.HW || d.up_W * 2 < 16 || d.C != 64) return -1;
+    a.up = up2x_src(d.up_H, d.up_W);
   }
-  GHOST_V3(64, 64, 1) GHOST_V3(64, 64, 2) GHOST_V3(64, 32, 1) GHOST_V3(64, 32, 2)
-  GHOST_V3(128, 128, 1) GHOST_V3(128, 64, 1)
+  dim3 grid((unsigned)((long)d.B * d.HW / a.PPW));
+#define GHOST_V3(c, ca, l, u)                                                                   \
+  if (d.C == c && d.Ca == ca && d.L == l && up == u) {                                          \
+    hipLaunchKernelGGL((aad_v3_kernel<c, ca, l, u>), grid, dim3(kWaves * 64), 0, s, a);         \
+    return (int)hipGetLastError();                                                              \
+  }
+#define GHOST_V3W(c, ca, l)                                                                     \
+  if (d.C == c && d.Ca == ca && d.L == l && !up) {                                              \
+    hipLaunchKernelGGL((aad_v3_wide_kernel<c, ca, l>), grid, dim3(kWaves * 64), 0, s, a);       \
+    return (int)hipGetLastError();                                                              \
+  }
+  GHOST_V3(64, 64, 1, false) GHOST_V3(64, 64, 2, false) GHOST_V3(64, 32, 1, false) GHOST_V3(64, 32, 2, false)
+  // through-upsample forms: the block-input AADLayers of AADBlk8 (first add_block + last_add_block)
+  GHOST_V3(64, 64, 2, true) GHOST_V3(64, 32, 2, true) GHOST_V3(64, 64, 1, true) GHOST_V3(64, 32, 1, true)
+  GHOST_V3W(128, 128, 1) GHOST_V3W(128, 64, 1) GHOST_V3W(128, 32, 1)
+#undef GHOST_V3W
 #undef GHOST_V3
   return -1;
 }

@@ -173,6 +173,8 @@ void run_conv(Ctx& c, ConvDesc& d, int cls_all, int cls_big, double flops) {
   if (e_all >= 0) c.prof_end(cls_all, e_all, bytes, flops);
 }
 
+static int g_fuse_upsample = 1;   // ghost_set_fuse_upsample (testing knob)
+
 void run_stats(Ctx& c, const void* x, int ldx, int B, int HW, int C, float* stat) {
   if (!c.ok()) return;
   if (c.dry) {
@@ -183,6 +185,19 @@ void run_stats(Ctx& c, const void* x, int ldx, int B, int HW, int C, float* stat
   int e = c.prof_begin(4);
   c.check(in_stats(c.h->dt, x, ldx, B, HW, C, stat, c.scratch, c.scratch_cap, c.s), "in_stats");
   c.prof_end(4, e, (double)B * HW * C * c.h->esz, 0);
+}
+
+// statistics of upsample2x(x) for an [B, H, W, C] source, without materialising it
+void run_stats_up(Ctx& c, const void* x, int ldx, int B, int H, int W, int C, float* stat) {
+  if (!c.ok()) return;
+  if (c.dry) {
+    size_t need = in_stats_workspace_bytes(B, 4 * H * W, C);
+    if (need > c.scratch_need) c.scratch_need = need;
+    return;
+  }
+  int e = c.prof_begin(4);
+  c.check(in_stats_up2x(c.h->dt, x, ldx, B, H, W, C, stat, c.scratch, c.scratch_cap, c.s), "in_stats_up2x");
+  c.prof_end(4, e, (double)B * H * W * C * c.h->esz, 0);
 }
 
 void run_mask(Ctx& c, const void* x, int ldx, int B, int HW, int C, const float* stat, const float* wh,
@@ -327,11 +342,16 @@ struct AadOut {
 
 // AADLayers that read the same h_in / z_attr: the register-epilogue kernel takes up to two at
 // once (one pass over the inputs); other shapes run one fused / split AAD kernel per layer
+// up_src: h_in is upsample2x of the [B, n/2, n/2] tensor hin (the through-upsample AAD kernel)
 void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, const float* stat, const void* za,
-               int lda, int Ca, int B, int n, int C, const float* idgb) {
+               int lda, int Ca, int B, int n, int C, const float* idgb, bool up_src = false) {
   ghost_aei* h = c.h;
   bool v3 = aad_v3_supported(h->dt, B, n * n, C, Ca, lda, ldh, 8);
   for (auto& l : ls) v3 = v3 && l.ldo % 8 == 0;
+  if (up_src && !v3) {
+    c.check(GHOST_EINVAL, "aad_group: through-upsample input needs the v3 kernel");
+    return;
+  }
   if (!v3) {
     for (auto& l : ls) aad(c, l.name, hin, ldh, stat, za, lda, Ca, B, n, C, l.id_off, idgb, l.out, l.ldo);
     return;
@@ -342,6 +362,7 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     d.za = za; d.lda = lda; d.Ca = Ca; d.hin = hin; d.ldh = ldh; d.stat = stat;
     d.B = B; d.HW = n * n; d.C = C; d.id_ld = h->id_total; d.slope = 0.0f;   // + the ReLU that follows
     d.L = (int)std::min(lmax, ls.size() - i0);
+    if (up_src) d.up_H = d.up_W = n / 2;
     for (int l = 0; l < d.L; ++l) {
       const AadOut& o = ls[i0 + l];
       d.w3[l] = c.W(o.name + ".w3");
@@ -354,7 +375,9 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     }
     if (!c.ok() || c.dry) continue;
     const double Pn = (double)B * n * n;
-    const double bytes = Pn * (C + Ca + (double)d.L * C) * h->esz;   // |h_in| + |z_attr| + L |out|
+    // algorithmic bytes by SURVEY.md §8d's formula, fixed regardless of fusion:
+    // sum over the L AADLayers of |h_in| + |z_attr| + |out| (PMC traffic shows what fusion saves)
+    const double bytes = Pn * (double)d.L * (2.0 * C + Ca) * h->esz;
     const double flops = 2.0 * Pn * 2.0 * C * Ca * d.L;
     int e_all = c.prof_begin(0);
     int e_big = (n == 256 && d.L == 2) ? c.prof_begin(1) : -1;   // class 1: the dual-layer kernel at 256x256
@@ -419,6 +442,7 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     run_conv(c, d, 7, -1, 2.0 * B * 4096 * h->c_id);
   }
   int id_off = 0;
+  bool m_virtual = false;   // m is not materialised: h_in = upsample2x(m) at n x n (m is n/2 x n/2)
   for (int k = 1; k <= 8; ++k) {
     const int cin = h->gen()[k - 1][0], cout = h->gen()[k - 1][1];
     int Ca, n;
@@ -430,7 +454,10 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     const bool split = cin != cout;          // AAD_ResBlk has a last_add_block (AADLayer.py:68-72)
     const int base = id_off;                  // idgb offset of this block's first AADLayer
     float* stat_m = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
-    run_stats(c, m, cin, B, n * n, cin, stat_m);
+    if (m_virtual)
+      run_stats_up(c, m, cin, B, n / 2, n / 2, cin, stat_m);
+    else
+      run_stats(c, m, cin, B, n * n, cin, stat_m);
     void* y = last_k ? y_out : c.alloc(P * cout * es);
     // x-branch and h'-branch share the output conv: conv(cat(a_x, a_h), [W_x | W_h]) = x + h'
     void* cat = split ? c.alloc(P * 2 * cin * es) : nullptr;
@@ -445,7 +472,7 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
       group.push_back({blk + ".aad" + std::to_string(i), base + 2 * cin * i, a, lda_out});
       if (i == 0 && split)   // last_add_block's AADLayer reads the block input m as well
         group.push_back({blk + ".aadlast", base + 2 * cin * nb, (char*)cat + (size_t)cin * es, 2 * cin});
-      aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb);
+      aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb, i == 0 && m_virtual);
       if (!last) {
         void* xn = c.alloc(P * cin * es);
         conv3x3(c, cn, a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr);
@@ -461,9 +488,22 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     }
     id_off = base + 2 * cin * nb + (split ? 2 * cin : 0);
     if (!last_k) {
-      void* mn = c.alloc((size_t)B * 4 * n * n * cout * es);
-      run_up(c, y, cout, mn, cout, B, n, n, cout);
-      m = mn;
+      // AADBlk(k+1) reads its input m only through the first AADLayer pair and the statistics
+      // when cin != cout: those sample the upsample on the fly and m is never written
+      int Ca_n, n_n;
+      h->attr_geom(k + 1, Ca_n, n_n);
+      const int cout_n = h->gen()[k][1];
+      const bool fuse = g_fuse_upsample && cout != cout_n && cout == 64 && Ca_n % 32 == 0 &&
+                        aad_v3_supported(h->dt, B, n_n * n_n, cout, Ca_n, Ca_n, cout, 8);
+      if (fuse) {
+        m = y;
+        m_virtual = true;
+      } else {
+        void* mn = c.alloc((size_t)B * 4 * n * n * cout * es);
+        run_up(c, y, cout, mn, cout, B, n, n, cout);
+        m = mn;
+        m_virtual = false;
+      }
     }
   }
 }
@@ -726,6 +766,11 @@ extern "C" int ghost_aei_profile_read(ghost_aei* h, int cls, double* ms, int64_t
 // ---------------------------------------------------------------------------
 // C ABI: single operators
 // ---------------------------------------------------------------------------
+extern "C" int ghost_set_fuse_upsample(int on) {
+  g_fuse_upsample = on ? 1 : 0;
+  return 0;
+}
+
 static int g_force_split = 0;
 extern "C" int ghost_set_split_k(int n) {
   if (n < 0) return fail(GHOST_EINVAL, "split must be >= 0");
@@ -853,14 +898,15 @@ extern "C" int ghost_conv3x3_narrow_nhwc(int dtype, const void* x, int B, int H,
   return rc ? fail(rc, "conv3x3_narrow failed (H % 8, W % 32, Cin % 32 and Cout <= 3 required)") : 0;
 }
 
-extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, const void* z_attr, int lda, int B, int H, int W,
-                                        int C, int Ca, int L, const void* const w3[], const float* const b3[],
+extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, const void* z_attr, int lda, int B, int H,
+                                        int W, int C, int Ca, int L, const void* const w3[], const float* const b3[],
                                         const float* const wh[], const float* const bh[], const float* const idgb[],
                                         int id_ld, float slope, void* const out[], const int ldo[], void* ws,
                                         int64_t ws_bytes, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int HW = H * W;
   if (L < 1 || L > 2) return fail(GHOST_EINVAL, "aad_v3: L must be 1 or 2");
+  if (up2x && (H % 2 || W % 2 || C != 64)) return fail(GHOST_EINVAL, "aad_v3: up2x needs even H, W and C = 64");
   for (int l = 0; l < L; ++l)
     if (!aad_v3_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[l]))
       return fail(GHOST_EINVAL, "aad_v3: unsupported shape (bf16, C in {64,128}, enough pixels)");
@@ -869,11 +915,16 @@ extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, const void* z
   char* base = (char*)(((uintptr_t)ws + 255) & ~uintptr_t(255));
   if (!ws || (size_t)ws_bytes < stat_b + sc + 256) return fail(GHOST_ENOWS, "aad_v3: workspace too small");
   float* stat = (float*)base;
-  int rc = in_stats(GHOST_BF16, h_in, ldh, B, HW, C, stat, base + stat_b, sc, s);
+  int rc = up2x ? in_stats_up2x(GHOST_BF16, h_in, ldh, B, H / 2, W / 2, C, stat, base + stat_b, sc, s)
+                : in_stats(GHOST_BF16, h_in, ldh, B, HW, C, stat, base + stat_b, sc, s);
   if (rc) return fail(rc, "aad_v3: in_stats failed");
   AadV3Desc d;
   d.za = z_attr; d.lda = lda; d.Ca = Ca; d.hin = h_in; d.ldh = ldh; d.stat = stat;
   d.B = B; d.HW = HW; d.C = C; d.L = L; d.id_ld = id_ld; d.slope = slope;
+  if (up2x) {
+    d.up_H = H / 2;
+    d.up_W = W / 2;
+  }
   for (int l = 0; l < L; ++l) {
     d.w3[l] = w3[l]; d.b3[l] = b3[l]; d.wh[l] = wh[l]; d.bh[l] = bh[l]; d.idgb[l] = idgb[l];
     d.out[l] = out[l]; d.ldo[l] = ldo[l];

@@ -29,7 +29,7 @@ struct NarrowArgs {
   int H, W, Cin, ldx, Kpad, ldy, ldres, NO, tanh_out;
 };
 
-template <typename T>
+template <typename T, int CIN>
 __global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const NarrowArgs a) {
   __shared__ float Z[NRT * 16 * ZLD];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
@@ -41,44 +41,89 @@ __global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const NarrowArgs a)
   const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
   const long img = (long)b * a.H * a.W;
 
-  for (int rt = wid; rt < NRT; rt += 4) {
-    // this lane's halo pixel (A row) for the tile
-    const int p = rt * 16 + lr;
-    const int hy = p / HW_, hx = p - hy * HW_;
-    const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
-    const bool ok = p < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-    const T* xp = x + (img + (long)(ok ? iy : 0) * a.W + (ok ? ix : 0)) * a.ldx;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (sizeof(T) == 2) {
-      for (int k0 = 0; k0 < a.Cin; k0 += 32) {
-        u32x4 av = ok ? *reinterpret_cast<const u32x4*>(xp + k0 + lq * 8) : u32x4{0u, 0u, 0u, 0u};
-        const u32x4 b0 = *reinterpret_cast<const u32x4*>(w + (long)lr * a.Kpad + k0 + lq * 8);
-        const u32x4 b1 = *reinterpret_cast<const u32x4*>(w + (long)(16 + lr) * a.Kpad + k0 + lq * 8);
-        bf16x8 af, bf0, bf1;
-        __builtin_memcpy(&af, &av, 16);
-        __builtin_memcpy(&bf0, &b0, 16);
-        __builtin_memcpy(&bf1, &b1, 16);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf0, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf1, acc1, 0, 0, 0);
-      }
-    } else {
-      for (int k0 = 0; k0 < a.Cin; k0 += 16) {
-        const f32x4 av = ok ? *reinterpret_cast<const f32x4*>(xp + k0 + lq * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-        const f32x4 b0 = *reinterpret_cast<const f32x4*>(w + (long)lr * a.Kpad + k0 + lq * 4);
-        const f32x4 b1 = *reinterpret_cast<const f32x4*>(w + (long)(16 + lr) * a.Kpad + k0 + lq * 4);
+  if constexpr (CIN > 0) {
+    // bf16, Cin known: the weight fragments stay in registers and each lane issues the loads of
+    // two row tiles (2 * CIN/32 x 16 B) before their MFMAs, so the HBM latency overlaps
+    bf16x8 wf0[CIN / 32], wf1[CIN / 32];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], b0[e], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], b1[e], acc1, 0, 0, 0);
+    for (int k = 0; k < CIN / 32; ++k) {
+      const u32x4 b0 = *reinterpret_cast<const u32x4*>(w + (long)lr * a.Kpad + k * 32 + lq * 8);
+      const u32x4 b1 = *reinterpret_cast<const u32x4*>(w + (long)(16 + lr) * a.Kpad + k * 32 + lq * 8);
+      __builtin_memcpy(&wf0[k], &b0, 16);
+      __builtin_memcpy(&wf1[k], &b1, 16);
+    }
+    for (int rt = wid; rt < NRT; rt += 8) {
+      u32x4 av[2][CIN / 32];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int p = (rt + 4 * u) * 16 + lr;
+        const int hy = p / HW_, hx = p - hy * HW_;
+        const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+        const bool ok = rt + 4 * u < NRT && p < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+        const T* xp = x + (img + (long)(ok ? iy : 0) * a.W + (ok ? ix : 0)) * a.ldx + lq * 8;
+#pragma unroll
+        for (int k = 0; k < CIN / 32; ++k)
+          av[u][k] = ok ? *reinterpret_cast<const u32x4*>(xp + k * 32) : u32x4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (rt + 4 * u >= NRT) break;
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < CIN / 32; ++k) {
+          bf16x8 af;
+          __builtin_memcpy(&af, &av[u][k], 16);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf0[k], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf1[k], acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = (rt + 4 * u) * 16 + lq * 4 + i;
+          Z[row * ZLD + lr] = acc0[i];
+          Z[row * ZLD + 16 + lr] = acc1[i];
         }
       }
     }
-    // C layout: column = lane&15, rows (lane>>4)*4 + i
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = rt * 16 + lq * 4 + i;
-      Z[row * ZLD + lr] = acc0[i];
-      Z[row * ZLD + 16 + lr] = acc1[i];
+  } else {
+    for (int rt = wid; rt < NRT; rt += 4) {
+      // this lane's halo pixel (A row) for the tile
+      const int p = rt * 16 + lr;
+      const int hy = p / HW_, hx = p - hy * HW_;
+      const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+      const bool ok = p < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      const T* xp = x + (img + (long)(ok ? iy : 0) * a.W + (ok ? ix : 0)) * a.ldx;
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (sizeof(T) == 2) {
+        for (int k0 = 0; k0 < a.Cin; k0 += 32) {
+          u32x4 av = ok ? *reinterpret_cast<const u32x4*>(xp + k0 + lq * 8) : u32x4{0u, 0u, 0u, 0u};
+          const u32x4 b0 = *reinterpret_cast<const u32x4*>(w + (long)lr * a.Kpad + k0 + lq * 8);
+          const u32x4 b1 = *reinterpret_cast<const u32x4*>(w + (long)(16 + lr) * a.Kpad + k0 + lq * 8);
+          bf16x8 af, bf0, bf1;
+          __builtin_memcpy(&af, &av, 16);
+          __builtin_memcpy(&bf0, &b0, 16);
+          __builtin_memcpy(&bf1, &b1, 16);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf0, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf1, acc1, 0, 0, 0);
+        }
+      } else {
+        for (int k0 = 0; k0 < a.Cin; k0 += 16) {
+          const f32x4 av = ok ? *reinterpret_cast<const f32x4*>(xp + k0 + lq * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+          const f32x4 b0 = *reinterpret_cast<const f32x4*>(w + (long)lr * a.Kpad + k0 + lq * 4);
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(w + (long)(16 + lr) * a.Kpad + k0 + lq * 4);
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], b0[e], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], b1[e], acc1, 0, 0, 0);
+          }
+        }
+      }
+      // C layout: column = lane&15, rows (lane>>4)*4 + i
+  #pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = rt * 16 + lq * 4 + i;
+        Z[row * ZLD + lr] = acc0[i];
+        Z[row * ZLD + 16 + lr] = acc1[i];
+      }
     }
   }
   __syncthreads();
@@ -112,10 +157,14 @@ int conv3x3_narrow(int dt, const void* x, int B, int H, int W, int Cin, int ldx,
   if (!conv3x3_narrow_supported(dt, H, W, Cin, ldx, NO) || (uintptr_t)x % 16 || (uintptr_t)w_narrow % 16) return -1;
   NarrowArgs a{x, w_narrow, res, y, u8, H, W, Cin, ldx, Kpad, ldy, ldres, NO, tanh_out};
   dim3 grid((unsigned)(B * (H / TH) * (W / TW)));
-  if (dt == GHOST_BF16)
-    hipLaunchKernelGGL(conv3x3_narrow_kernel<bf16>, grid, dim3(256), 0, s, a);
+  if (dt == GHOST_BF16 && Cin == 128)
+    hipLaunchKernelGGL((conv3x3_narrow_kernel<bf16, 128>), grid, dim3(256), 0, s, a);
+  else if (dt == GHOST_BF16 && Cin == 64)
+    hipLaunchKernelGGL((conv3x3_narrow_kernel<bf16, 64>), grid, dim3(256), 0, s, a);
+  else if (dt == GHOST_BF16)
+    hipLaunchKernelGGL((conv3x3_narrow_kernel<bf16, 0>), grid, dim3(256), 0, s, a);
   else if (dt == GHOST_F32)
-    hipLaunchKernelGGL(conv3x3_narrow_kernel<float>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv3x3_narrow_kernel<float, 0>), grid, dim3(256), 0, s, a);
   else
     return -1;
   return (int)hipGetLastError();

@@ -12,6 +12,10 @@ namespace ghost {
 size_t in_stats_workspace_bytes(int B, int HW, int C);
 int in_stats(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, void* ws, size_t ws_bytes,
              hipStream_t s);
+// the same statistics of upsample2x(x) ([B, 2H, 2W, C], values rounded to dt) without materialising
+// it: x is the [B, H, W, C] source; workspace = in_stats_workspace_bytes(B, 4HW, C)
+int in_stats_up2x(int dt, const void* x, int ldx, int B, int H, int W, int C, float* stat, void* ws, size_t ws_bytes,
+                  hipStream_t s);
 
 // AAD mask: M[p] = sigmoid(sum_c wh[c] * (h[p,c]-mu[b,c])*rstd[b,c] + bh)   (AADLayer.py:35)
 int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh,

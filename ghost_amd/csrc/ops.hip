@@ -3,6 +3,7 @@
 // vector accesses along channels, fp32 arithmetic.
 #include "ghost_common.h"
 #include "ops.h"
+#include "up2x.h"
 
 namespace ghost {
 
@@ -13,9 +14,12 @@ static constexpr float kInEps = 1e-5f;   // nn.InstanceNorm2d default (AADLayer.
 // grid (nchunk, ceil(C/64), B); a block reduces `chunk` pixels x 64 channels.
 // Shift K_c = x[b, pixel 0, c] makes the partial sums robust to |mean| >> std.
 // ---------------------------------------------------------------------------
-template <typename T>
+// UP: x is the source of a virtual bilinear x2 upsample (u); the statistics are those of the
+// upsampled tensor as upsample2x would store it (values rounded to T), HW = 4 * u.H * u.W.
+template <typename T, bool UP>
 __global__ void __launch_bounds__(256)
-in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chunk, int nchunk, float* __restrict__ part) {
+in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chunk, int nchunk, float* __restrict__ part,
+                        const Up2xSrc u) {
   constexpr int VEC = Vec16<T>::N;
   constexpr int TPP = 64 / VEC;   // threads per pixel (64 channels)
   constexpr int PPP = 256 / TPP;  // pixels per pass
@@ -24,7 +28,7 @@ in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chu
   const int t = threadIdx.x, cc = t % TPP, po = t / TPP;
   const int c0 = cg * 64 + cc * VEC;
   const bool cok = c0 < C;
-  const T* xb = x + (long)b * HW * ldx;
+  const T* xb = x + (long)b * (UP ? u.H * u.W : HW) * ldx;
   float K[VEC], s1[VEC], s2[VEC];
 #pragma unroll
   for (int e = 0; e < VEC; ++e) { K[e] = 0.f; s1[e] = 0.f; s2[e] = 0.f; }
@@ -34,7 +38,14 @@ in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chu
   if (cok) {
     for (int p = p0 + po; p < p1; p += PPP) {
       float v[VEC];
-      load16_f(xb + (long)p * ldx + c0, v);
+      if constexpr (UP) {
+        const int oy = p / (2 * u.W), ox = p - oy * (2 * u.W);
+        up2x_load16_f(xb + c0, ldx, up2x_tap(u, oy, ox), v);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) v[e] = to_f(from_f<T>(v[e]));
+      } else {
+        load16_f(xb + (long)p * ldx + c0, v);
+      }
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
         const float d = v[e] - K[e];
@@ -63,12 +74,12 @@ in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chu
 
 template <typename T>
 __global__ void __launch_bounds__(256)
-in_stats_final_kernel(const T* __restrict__ x, int ldx, int B, int HW, int C, int nchunk, const float* __restrict__ part,
-                      float* __restrict__ stat) {
+in_stats_final_kernel(const T* __restrict__ x, int ldx, long bstride, int B, int HW, int C, int nchunk,
+                      const float* __restrict__ part, float* __restrict__ stat) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= B * C) return;
   const int b = i / C, c = i - b * C;
-  const double K = (double)to_f(x[(long)b * HW * ldx + c]);
+  const double K = (double)to_f(x[(long)b * bstride * ldx + c]);   // pixel 0 (also of an upsample)
   double S1 = 0.0, S2 = 0.0;
   for (int k = 0; k < nchunk; ++k) {
     const float* o = part + (((long)b * nchunk + k) * C + c) * 2;
@@ -94,25 +105,45 @@ size_t in_stats_workspace_bytes(int B, int HW, int C) {
   return (size_t)B * nchunk * C * 2 * sizeof(float);
 }
 
-int in_stats(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, void* ws, size_t ws_bytes,
-             hipStream_t s) {
-  if (C % 16 || ldx % 8 || (uintptr_t)x % 16) return -1;
+template <typename T>
+static void in_stats_launch(const T* x, int ldx, int B, int HW, int C, float* stat, float* part, const Up2xSrc* up,
+                            hipStream_t s) {
   int chunk, nchunk;
   stats_geometry(HW, chunk, nchunk);
-  if (!ws || ws_bytes < in_stats_workspace_bytes(B, HW, C)) return -1;
-  float* part = reinterpret_cast<float*>(ws);
   dim3 g1(nchunk, (C + 63) / 64, B);
   dim3 g2((B * C + 255) / 256);
-  if (dt == GHOST_F32) {
-    hipLaunchKernelGGL(in_stats_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)x, ldx, HW, C, chunk, nchunk, part);
-    hipLaunchKernelGGL(in_stats_final_kernel<float>, g2, dim3(256), 0, s, (const float*)x, ldx, B, HW, C, nchunk, part, stat);
-  } else if (dt == GHOST_BF16) {
-    hipLaunchKernelGGL(in_stats_partial_kernel<bf16>, g1, dim3(256), 0, s, (const bf16*)x, ldx, HW, C, chunk, nchunk, part);
-    hipLaunchKernelGGL(in_stats_final_kernel<bf16>, g2, dim3(256), 0, s, (const bf16*)x, ldx, B, HW, C, nchunk, part, stat);
-  } else {
+  const Up2xSrc u = up ? *up : Up2xSrc{0, 0, 0.f, 0.f};
+  if (up)
+    hipLaunchKernelGGL((in_stats_partial_kernel<T, true>), g1, dim3(256), 0, s, x, ldx, HW, C, chunk, nchunk, part, u);
+  else
+    hipLaunchKernelGGL((in_stats_partial_kernel<T, false>), g1, dim3(256), 0, s, x, ldx, HW, C, chunk, nchunk, part, u);
+  const long bstride = up ? (long)u.H * u.W : HW;
+  hipLaunchKernelGGL(in_stats_final_kernel<T>, g2, dim3(256), 0, s, x, ldx, bstride, B, HW, C, nchunk, part, stat);
+}
+
+static int in_stats_any(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, void* ws, size_t ws_bytes,
+                        const Up2xSrc* up, hipStream_t s) {
+  if (C % 16 || ldx % 8 || (uintptr_t)x % 16) return -1;
+  if (!ws || ws_bytes < in_stats_workspace_bytes(B, HW, C)) return -1;
+  float* part = reinterpret_cast<float*>(ws);
+  if (dt == GHOST_F32)
+    in_stats_launch((const float*)x, ldx, B, HW, C, stat, part, up, s);
+  else if (dt == GHOST_BF16)
+    in_stats_launch((const bf16*)x, ldx, B, HW, C, stat, part, up, s);
+  else
     return -1;
-  }
   return (int)hipGetLastError();
+}
+
+int in_stats(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, void* ws, size_t ws_bytes,
+             hipStream_t s) {
+  return in_stats_any(dt, x, ldx, B, HW, C, stat, ws, ws_bytes, nullptr, s);
+}
+
+int in_stats_up2x(int dt, const void* x, int ldx, int B, int H, int W, int C, float* stat, void* ws, size_t ws_bytes,
+                  hipStream_t s) {
+  const Up2xSrc u = up2x_src(H, W);
+  return in_stats_any(dt, x, ldx, B, 4 * H * W, C, stat, ws, ws_bytes, &u, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -169,33 +200,19 @@ int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* 
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ void __launch_bounds__(256)
-upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, int H, int W, int C, float sh,
-                  float sw) {
+upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, const Up2xSrc u, int C) {
   // grid: x = chunks of one output row (2W * C/VEC work items), y = b * 2H + oy; 32-bit index math only
   constexpr int VEC = Vec16<T>::N;
   const int nch = C / VEC;
-  const int Wo = 2 * W, Ho = 2 * H;
+  const int Wo = 2 * u.W, Ho = 2 * u.H;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= Wo * nch) return;
   const int row = blockIdx.y;
   const int b = row / Ho, oy = row - b * Ho;
   const int ox = i / nch, ci = i - ox * nch;
-  // keep the rounded source coordinate, as PyTorch does: the empty asm stops hipcc from
-  // re-forming sh*oy - y0 as one fma (which would skip the product's rounding)
-  float ry = sh * (float)oy, rx = sw * (float)ox;
-  asm volatile("" : "+v"(ry), "+v"(rx));
-  const int y0 = (int)ry, x0 = (int)rx;
-  const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
-  const float ly1 = ry - (float)y0, ly0 = 1.f - ly1;
-  const float lx1 = rx - (float)x0, lx0 = 1.f - lx1;
-  const T* xb = x + (long)b * H * W * ldx + ci * VEC;
-  float v00[VEC], v01[VEC], v10[VEC], v11[VEC], o[VEC];
-  load16_f(xb + (long)(y0 * W + x0) * ldx, v00);
-  load16_f(xb + (long)(y0 * W + x1) * ldx, v01);
-  load16_f(xb + (long)(y1 * W + x0) * ldx, v10);
-  load16_f(xb + (long)(y1 * W + x1) * ldx, v11);
-#pragma unroll
-  for (int e = 0; e < VEC; ++e) o[e] = ly0 * (lx0 * v00[e] + lx1 * v01[e]) + ly1 * (lx0 * v10[e] + lx1 * v11[e]);
+  const Up2xTap t = up2x_tap(u, oy, ox);
+  float o[VEC];
+  up2x_load16_f(x + (long)b * u.H * u.W * ldx + ci * VEC, ldx, t, o);
   store16_f(y + ((long)row * Wo + ox) * ldy + ci * VEC, o);
 }
 
@@ -204,14 +221,11 @@ int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, i
   if (C % vec || ldx % vec || ldy % vec || (uintptr_t)x % 16 || (uintptr_t)y % 16) return -1;
   dim3 grid((unsigned)((2 * W * (C / vec) + 255) / 256), (unsigned)(B * 2 * H));
   // source scale (in-1)/(out-1) rounded once on the host, as PyTorch's area_pixel_compute_scale
-  const float sh = H > 0 ? (float)(H - 1) / (float)(2 * H - 1) : 0.f;
-  const float sw = W > 0 ? (float)(W - 1) / (float)(2 * W - 1) : 0.f;
+  const Up2xSrc u = up2x_src(H, W);
   if (dt == GHOST_F32)
-    hipLaunchKernelGGL(upsample2x_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, H, W, C,
-                       sh, sw);
+    hipLaunchKernelGGL(upsample2x_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, u, C);
   else if (dt == GHOST_BF16)
-    hipLaunchKernelGGL(upsample2x_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, H, W, C,
-                       sh, sw);
+    hipLaunchKernelGGL(upsample2x_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, u, C);
   else
     return -1;
   return (int)hipGetLastError();

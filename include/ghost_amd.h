@@ -119,11 +119,13 @@ int ghost_aad_layer_nhwc(int dtype, const void* h_in, int ldh, const void* z_att
                          int64_t ws_bytes, void* stream);
 /* One or two AADLayers (bf16, C in {64,128}) that read the same h_in and z_attr, in one pass:
  * w3/b3 per layer in the permuted layout of pack.py pack_aad_v3; InstanceNorm statistics of h_in
- * are computed into the workspace first. */
-int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, const void* z_attr, int lda, int B, int H, int W, int C,
-                             int Ca, int L, const void* const w3[], const float* const b3[], const float* const wh[],
-                             const float* const bh[], const float* const idgb[], int id_ld, float slope,
-                             void* const out[], const int ldo[], void* ws, int64_t ws_bytes, void* stream);
+ * are computed into the workspace first.  up2x = 1: h_in is upsample2x of the [B, H/2, W/2, C]
+ * tensor passed as h_in (F.interpolate of AEI_Net.py:137 fused into the AADLayer read; C = 64). */
+int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, const void* z_attr, int lda, int B, int H, int W,
+                             int C, int Ca, int L, const void* const w3[], const float* const b3[],
+                             const float* const wh[], const float* const bh[], const float* const idgb[], int id_ld,
+                             float slope, void* const out[], const int ldo[], void* ws, int64_t ws_bytes,
+                             void* stream);
 int ghost_upsample2x_nhwc(int dtype, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C,
                           void* stream);
 int ghost_nhwc_to_nchw(int dtype, const void* x, int ldx, int B, int H, int W, int C, void* y, void* stream);
@@ -132,6 +134,9 @@ int ghost_crops_to_input_nhwc(const uint8_t* crops, int64_t crop_batch_stride, i
                               void* stream);
 /* testing knob: force the split-K factor of subsequent single-operator convs (0 = heuristic) */
 int ghost_set_split_k(int n);
+/* testing knob: 1 (default) lets the generator sample the upsample of AADBlk7's output inside
+ * AADBlk8's first AADLayer pair instead of materialising it; 0 materialises it */
+int ghost_set_fuse_upsample(int on);
 
 #ifdef __cplusplus
 }

@@ -272,6 +272,27 @@ def test_forward_bf16_close_to_oracle(lib):
     bf16_gate(Y.float().cpu(), torch.from_numpy(g["Y"]))
 
 
+@pytest.mark.parametrize("backbone,nb", [("unet", 2), ("linknet", 3)])
+def test_bf16_through_upsample_aad_matches_materialised(lib, backbone, nb):
+    """AADBlk8's first AADLayer pair sampling upsample2x(y7) on the fly == the materialised path."""
+    G = model(backbone, nb, compute_dtype=torch.bfloat16)
+    xt, z = aei_ref.make_inputs(4, 5)
+    try:
+        _lib_mod().check(lib.ghost_set_fuse_upsample(0))
+        Y0, _ = G(xt.to(DEV), z.to(DEV))
+        Y0 = Y0.float().cpu()
+    finally:
+        lib.ghost_set_fuse_upsample(1)
+    Y1, _ = G(xt.to(DEV), z.to(DEV))
+    d = (Y1.float().cpu() - Y0).abs()
+    assert float(d.mean()) <= 1e-3 and float(d.max()) <= 0.1, (float(d.mean()), float(d.max()))
+
+
+def _lib_mod():
+    from ghost_amd import _lib
+    return _lib
+
+
 def test_full_batch64_bf16_properties_and_fp32_rows(lib):
     """B=64 (the bench configuration): batch independence and oracle parity on sampled rows."""
     G32 = model("unet", 2)
@@ -370,19 +391,24 @@ def test_conv3x3_narrow_op(lib, dt, cin, cout, H, W, use_res):
     assert int((got_u8.int() - ref_u8[..., :cout].int()).abs().max()) <= (1 if dt == torch.float32 else 3)
 
 
-@pytest.mark.parametrize("c_x,c_a,n,B,L", [(64, 64, 256, 2, 2), (64, 64, 256, 2, 1), (128, 128, 128, 2, 1),
-                                           (64, 32, 128, 4, 2), (128, 64, 64, 8, 1)])
-def test_aad_layers_v3_vs_oracle(lib, c_x, c_a, n, B, L):
-    """Register-epilogue AAD kernel (1 or 2 layers sharing h_in / z_attr) against the oracle AADLayer."""
+@pytest.mark.parametrize("c_x,c_a,n,B,L,up", [(64, 64, 256, 2, 2, 0), (64, 64, 256, 2, 1, 0), (128, 128, 128, 2, 1, 0),
+                                              (64, 32, 128, 4, 2, 0), (128, 64, 64, 8, 1, 0), (128, 32, 64, 8, 1, 0),
+                                              (64, 64, 256, 2, 2, 1), (64, 32, 128, 4, 2, 1), (64, 64, 64, 8, 1, 1)])
+def test_aad_layers_v3_vs_oracle(lib, c_x, c_a, n, B, L, up):
+    """Register-epilogue AAD kernel (1 or 2 layers sharing h_in / z_attr) against the oracle AADLayer;
+    up = 1: h_in is read through the bilinear x2 upsample of an n/2 source (AEI_Net.py:137)."""
     import ctypes as C
     from ghost_amd import _lib
     from ghost_amd.network.pack import pack_aad_v3
     dt = torch.bfloat16
     g = torch.Generator().manual_seed(c_x * 3 + n + L)
-    h = (torch.randn(B, c_x, n, n, generator=g) * 1.5 + 0.7).to(dt).float()
+    hn = n // 2 if up else n
+    hs = (torch.randn(B, c_x, hn, hn, generator=g) * 1.5 + 0.7).to(dt).float()
+    # the materialised path stores the upsample in bf16: the reference sees those values
+    h = F.interpolate(hs, scale_factor=2, mode="bilinear", align_corners=True).to(dt).float() if up else hs
     za = torch.randn(B, c_a, n, n, generator=g).to(dt).float()
     zi = torch.randn(B, 512, generator=g)
-    hd, zad = nhwc(h).to(dt).to(DEV), nhwc(za).to(dt).to(DEV)
+    hd, zad = nhwc(hs).to(dt).to(DEV), nhwc(za).to(dt).to(DEV)
     keep, w3s, b3s, whs, bhs, ids, outs, refs = [], [], [], [], [], [], [], []
     for l in range(L):
         specs = [(f"v3_{l}.{k}", shp, kind) for k, shp, kind in [
@@ -404,7 +430,7 @@ def test_aad_layers_v3_vs_oracle(lib, c_x, c_a, n, B, L):
         bhs.append(bh.data_ptr()); ids.append(idgb.data_ptr()); outs.append(out.data_ptr())
     arr = lambda xs: (C.c_void_p * L)(*xs)  # noqa: E731
     ws = torch.empty(64 << 20, dtype=torch.uint8, device=DEV)
-    _lib.check(lib.ghost_aad_layers_v3_nhwc(hd.data_ptr(), c_x, zad.data_ptr(), c_a, B, n, n, c_x, c_a, L, arr(w3s),
+    _lib.check(lib.ghost_aad_layers_v3_nhwc(hd.data_ptr(), c_x, up, zad.data_ptr(), c_a, B, n, n, c_x, c_a, L, arr(w3s),
                                             arr(b3s), arr(whs), arr(bhs), arr(ids), 2 * c_x, 0.0, arr(outs),
                                             (C.c_int * L)(*([c_x] * L)), ws.data_ptr(), ws.numel(), stream(lib)))
     for l in range(L):
