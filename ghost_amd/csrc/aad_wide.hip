@@ -1,0 +1,220 @@
+// ghost_amd — AADLayer kernel for the wide stages (C >= 256: 16x16 .. 64x64, bf16).
+//
+// AADLayer.py:20-38 (+ the ReLU that follows it) as in aad_v3.hip (transposed MFMA whose
+// accumulators are gamma/beta of 16 channels of one pixel, register epilogue), but a
+// workgroup owns ONE 64-channel tile of a block of pixels: the tile's 128 permuted weight
+// rows (pack.py pack_aad_v3) fit LDS for any Ca <= 256, where all C/64 tiles would not.
+// The mask needs every channel of the pixel, so each workgroup forms it from the whole h_in
+// row; the C/64 workgroups of one pixel block are adjacent in launch order (and on one XCD),
+// so those re-reads are L2 hits and HBM sees h_in, z_attr and out about once each.
+#include <cstdlib>
+
+#include "aad_wide.h"
+#include "ghost_common.h"
+
+namespace ghost {
+
+struct AadWideArgs {
+  const bf16* za;
+  const bf16* hin;
+  const float* stat;
+  const bf16* w3;
+  const float* b3;
+  const float* wh;
+  const float* bh;
+  const float* idgb;
+  bf16* out;
+  int lda, ldh, ldo, id_ld, HW, PPW, nblk;
+  float slope;
+};
+
+static constexpr int kWideWaves = 8;
+
+GHOST_DEV int wide_xcd_tile(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+template <int C, int CA>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_wide_kernel(const AadWideArgs a) {
+  constexpr int CT = C / 64;
+  constexpr int KS = CA / 32;
+  constexpr int WLD = CA + 8;
+  constexpr int NCH = C / 32;        // 16-byte chunks of a pixel per lane group position
+  __shared__ __attribute__((aligned(16))) bf16 s_w[128 * WLD];
+  __shared__ __attribute__((aligned(16))) float s_b[128];
+  __shared__ __attribute__((aligned(16))) float s_cf[C];    // wh * rstd, every channel (mask)
+  __shared__ __attribute__((aligned(16))) float s_rs[64];
+  __shared__ __attribute__((aligned(16))) float s_nm[64];
+  __shared__ __attribute__((aligned(16))) float s_gi[64];
+  __shared__ __attribute__((aligned(16))) float s_bi[64];
+  __shared__ float s_k;
+
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int tile = wide_xcd_tile(blockIdx.x, gridDim.x);
+  const int ct = tile % CT, blk = tile / CT;
+  const long p_begin = (long)blk * a.PPW;
+  const int b = (int)(p_begin / a.HW);
+
+  for (int idx = tid; idx < 128 * (CA / 8); idx += kWideWaves * 64) {
+    const int row = idx / (CA / 8), kc = idx - row * (CA / 8);
+    *reinterpret_cast<u32x4*>(&s_w[row * WLD + kc * 8]) =
+        *reinterpret_cast<const u32x4*>(a.w3 + (long)(ct * 128 + row) * CA + kc * 8);
+  }
+  for (int i = tid; i < 128; i += kWideWaves * 64) s_b[i] = a.b3[ct * 128 + i];
+  for (int c = tid; c < C; c += kWideWaves * 64) s_cf[c] = a.wh[c] * a.stat[((long)b * C + c) * 2 + 1];
+  if (tid < 64) {
+    const int c = ct * 64 + tid;
+    const float mu = a.stat[((long)b * C + c) * 2], rs = a.stat[((long)b * C + c) * 2 + 1];
+    s_rs[tid] = rs;
+    s_nm[tid] = -mu * rs;
+    s_gi[tid] = a.idgb[(long)b * a.id_ld + c];
+    s_bi[tid] = a.idgb[(long)b * a.id_ld + C + c];
+  }
+  if (wid == 1) {   // k = sum_c wh_c * (-mu_c * rstd_c): the mask logit is sum_c cf_c h_c + k + bh
+    float k = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      const float mu = a.stat[((long)b * C + c) * 2], rs = a.stat[((long)b * C + c) * 2 + 1];
+      k = fmaf(a.wh[c], -mu * rs, k);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) k += __shfl_xor(k, o, 64);
+    if (lane == 0) s_k = k;
+  }
+  __syncthreads();
+  const float bh = a.bh[0] + s_k;
+
+  const int ntiles = a.PPW / 16;
+  for (int t = wid; t < ntiles; t += kWideWaves) {
+    asm volatile("" ::: "memory");
+    const long p = p_begin + t * 16 + lr;
+    const bf16* hrow = a.hin + p * a.ldh;
+    // z_attr: shallow rows are issued before the mask pass (overlapping it); deep rows (Ca = 256)
+    // are streamed four k-steps at a time inside the GEMM (second half: L1 hits)
+    constexpr bool ZEARLY = KS <= 4;
+    u32x4 zc[ZEARLY ? KS : 1];
+    if constexpr (ZEARLY) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + ks * 32 + lq * 8);
+    }
+
+    // mask over all C channels, 8 chunks at a time (bounded registers)
+    float ms = 0.f;
+#pragma unroll 1
+    for (int g = 0; g < NCH; g += 8) {
+      asm volatile("" ::: "memory");
+      u32x4 hv8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (g + u < NCH) hv8[u] = *reinterpret_cast<const u32x4*>(hrow + (g + u) * 32 + lq * 8);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (g + u >= NCH) break;
+        if (NCH > 8) asm volatile("" ::: "memory");   // one chunk's cf values live at a time
+        const bf16* hv = reinterpret_cast<const bf16*>(&hv8[u]);
+        const int c0 = (g + u) * 32 + lq * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ms = fmaf(s_cf[c0 + e], (float)hv[e], ms);
+      }
+    }
+    ms += __shfl_xor(ms, 16, 64);
+    ms += __shfl_xor(ms, 32, 64);
+    const float Mk = sigmoidf_ref(ms + bh);
+#pragma unroll
+    for (int sh = 0; sh < 2; ++sh) {
+      asm volatile("" ::: "memory");
+      const int cl = sh * 32 + lq * 8;     // channel within the tile
+      const u32x4 hraw = *reinterpret_cast<const u32x4*>(hrow + ct * 64 + cl);   // L1 hit (mask pass)
+      f32x4 acc[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
+        acc[i] = *reinterpret_cast<const f32x4*>(&s_b[rt * 16 + lq * 4]);
+      }
+#pragma unroll
+      for (int k0 = 0; k0 < KS; k0 += 4) {
+        u32x4 zg[4];
+        if constexpr (ZEARLY) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) if (k0 + u < KS) zg[u] = zc[k0 + u];
+        } else {
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            zg[u] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + (k0 + u) * 32 + lq * 8);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (k0 + u >= KS) break;
+          const int ks = k0 + u;
+          bf16x8 bfrag;
+          __builtin_memcpy(&bfrag, &zg[u], 16);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
+            const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&s_w[(rt * 16 + lr) * WLD + ks * 32 + lq * 8]);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i], 0, 0, 0);
+          }
+        }
+      }
+      const bf16* hv = reinterpret_cast<const bf16*>(&hraw);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float hh = fmaf((float)hv[e], s_rs[cl + e], s_nm[cl + e]);
+        const float A = fmaf(acc[e >> 2][e & 3], hh, acc[2 + (e >> 2)][e & 3]);
+        const float I = fmaf(s_gi[cl + e], hh, s_bi[cl + e]);
+        const float v = fmaf(Mk, I - A, A);
+        o[e] = v > 0.f ? v : v * a.slope;
+      }
+      store16_f(a.out + p * a.ldo + ct * 64 + cl, o);
+    }
+  }
+}
+
+namespace {
+int wide_ppw(int B, int HW, int C) {
+  // as many pixels per workgroup as keep >= 512 workgroups (two per CU): the 128 weight rows
+  // staged per workgroup are then amortised over as many 16-pixel tiles as possible
+  static const int force = [] {
+    const char* e = getenv("GHOST_AAD_WIDE_PPW");
+    return e ? atoi(e) : 0;
+  }();
+  if (force > 0 && HW % force == 0 && force % 16 == 0) return force;
+  int best = 0;
+  for (int ppw = 16; ppw <= HW && ppw <= 4096; ppw *= 2)
+    if (HW % ppw == 0 && (best == 0 || (long)B * HW / ppw * (C / 64) >= 512)) best = ppw;
+  return best;
+}
+}  // namespace
+
+bool aad_wide_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo) {
+  if (dt != GHOST_BF16) return false;
+  const bool shape = (C == 256 || C == 512 || C == 1024) && (Ca == 64 || Ca == 128 || Ca == 256);
+  if (!shape || lda % 8 || ldh % 8 || ldo % 8) return false;
+  const int ppw = wide_ppw(B, HW, C);
+  return ppw > 0 && (long)B * HW / ppw * (C / 64) >= 256;
+}
+
+int aad_wide(const AadWideDesc& d, hipStream_t s) {
+  if (!aad_wide_supported(GHOST_BF16, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo)) return -1;
+  AadWideArgs a{};
+  a.za = (const bf16*)d.za; a.hin = (const bf16*)d.hin; a.stat = d.stat;
+  a.w3 = (const bf16*)d.w3; a.b3 = d.b3; a.wh = d.wh; a.bh = d.bh; a.idgb = d.idgb; a.out = (bf16*)d.out;
+  a.lda = d.lda; a.ldh = d.ldh; a.ldo = d.ldo; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
+  a.PPW = wide_ppw(d.B, d.HW, d.C);
+  a.nblk = (int)((long)d.B * d.HW / a.PPW);
+  dim3 grid((unsigned)(a.nblk * (d.C / 64)));
+#define GHOST_W(c, ca)                                                                 \
+  if (d.C == c && d.Ca == ca) {                                                        \
+    hipLaunchKernelGGL((aad_wide_kernel<c, ca>), grid, dim3(kWideWaves * 64), 0, s, a); \
+    return (int)hipGetLastError();                                                     \
+  }
+  GHOST_W(256, 64) GHOST_W(256, 128) GHOST_W(256, 256) GHOST_W(512, 64) GHOST_W(512, 128) GHOST_W(512, 256)
+  GHOST_W(1024, 64) GHOST_W(1024, 128) GHOST_W(1024, 256)
+#undef GHOST_W
+  return -1;
+}
+
+}  // namespace ghost

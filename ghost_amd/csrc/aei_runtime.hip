@@ -17,6 +17,7 @@
 #include "../../include/ghost_amd.h"
 #include "aad_fused.h"
 #include "aad_v3.h"
+#include "aad_wide.h"
 #include "conv_igemm.h"
 #include "conv_narrow.h"
 #include "ghost_common.h"
@@ -353,7 +354,28 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     return;
   }
   if (!v3) {
-    for (auto& l : ls) aad(c, l.name, hin, ldh, stat, za, lda, Ca, B, n, C, l.id_off, idgb, l.out, l.ldo);
+    bool wide = aad_wide_supported(h->dt, B, n * n, C, Ca, lda, ldh, 8);
+    for (auto& l : ls) wide = wide && l.ldo % 8 == 0;
+    for (auto& l : ls) {
+      if (!wide) {
+        aad(c, l.name, hin, ldh, stat, za, lda, Ca, B, n, C, l.id_off, idgb, l.out, l.ldo);
+        continue;
+      }
+      AadWideDesc d;
+      d.za = za; d.lda = lda; d.Ca = Ca; d.hin = hin; d.ldh = ldh; d.stat = stat;
+      d.B = B; d.HW = n * n; d.C = C; d.id_ld = h->id_total; d.slope = 0.0f;   // + the ReLU that follows
+      d.w3 = c.W(l.name + ".w3");
+      d.b3 = (const float*)c.W(l.name + ".b3");
+      d.wh = (const float*)c.W(l.name + ".wh");
+      d.bh = (const float*)c.W(l.name + ".bh");
+      d.idgb = idgb ? idgb + l.id_off : nullptr;
+      d.out = l.out; d.ldo = l.ldo;
+      if (!c.ok() || c.dry) continue;
+      const double Pn = (double)B * n * n;
+      int e_all = c.prof_begin(0);
+      c.check(aad_wide(d, c.s), "aad_wide");
+      if (e_all >= 0) c.prof_end(0, e_all, Pn * (2.0 * C + Ca) * h->esz, 2.0 * Pn * 2.0 * C * Ca);
+    }
     return;
   }
   const size_t lmax = C == 64 ? 2 : 1;
@@ -532,7 +554,12 @@ void declare_slots(ghost_aei* h) {
   for (int k = 1; k <= 8; ++k) {
     const int cin = h->gen()[k - 1][0], cout = h->gen()[k - 1][1];
     const std::string blk = "gen.blk" + std::to_string(k);
-    const bool v3 = h->dt == GHOST_BF16 && (cin == 64 || cin == 128);   // register-epilogue AAD layouts
+    int Ca_k, n_k;
+    h->attr_geom(k, Ca_k, n_k);
+    // permuted register-epilogue AAD layouts (pack.py pack_aad_v3): aad_v3 for C in {64, 128},
+    // aad_wide for C in {256, 512, 1024} with Ca <= 256
+    const bool v3 = h->dt == GHOST_BF16 && (cin == 64 || cin == 128 ||
+                                            ((cin == 256 || cin == 512 || cin == 1024) && Ca_k <= 256));
     for (int i = 0; i < h->nb; ++i) {
       const std::string an = blk + ".aad" + std::to_string(i);
       add(an + ".gbw"); add(an + ".gbb"); add(an + ".wh"); add(an + ".bh");
@@ -907,7 +934,10 @@ extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, con
   const int HW = H * W;
   if (L < 1 || L > 2) return fail(GHOST_EINVAL, "aad_v3: L must be 1 or 2");
   if (up2x && (H % 2 || W % 2 || C != 64)) return fail(GHOST_EINVAL, "aad_v3: up2x needs even H, W and C = 64");
-  for (int l = 0; l < L; ++l)
+  const bool wide = C >= 256;   // aad_wide: one layer, C in {256, 512, 1024}, Ca <= 256
+  if (wide && (L != 1 || up2x || !aad_wide_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[0])))
+    return fail(GHOST_EINVAL, "aad_wide: unsupported shape (one layer, C in {256,512,1024}, Ca <= 256)");
+  for (int l = 0; l < L && !wide; ++l)
     if (!aad_v3_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[l]))
       return fail(GHOST_EINVAL, "aad_v3: unsupported shape (bf16, C in {64,128}, enough pixels)");
   const size_t stat_b = ((size_t)B * C * 2 * sizeof(float) + 255) & ~size_t(255);
@@ -918,6 +948,14 @@ extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, con
   int rc = up2x ? in_stats_up2x(GHOST_BF16, h_in, ldh, B, H / 2, W / 2, C, stat, base + stat_b, sc, s)
                 : in_stats(GHOST_BF16, h_in, ldh, B, HW, C, stat, base + stat_b, sc, s);
   if (rc) return fail(rc, "aad_v3: in_stats failed");
+  if (wide) {
+    AadWideDesc w;
+    w.za = z_attr; w.lda = lda; w.Ca = Ca; w.hin = h_in; w.ldh = ldh; w.stat = stat;
+    w.B = B; w.HW = HW; w.C = C; w.id_ld = id_ld; w.slope = slope;
+    w.w3 = w3[0]; w.b3 = b3[0]; w.wh = wh[0]; w.bh = bh[0]; w.idgb = idgb[0]; w.out = out[0]; w.ldo = ldo[0];
+    rc = aad_wide(w, s);
+    return rc ? fail(rc, "aad_wide launch failed") : 0;
+  }
   AadV3Desc d;
   d.za = z_attr; d.lda = lda; d.Ca = Ca; d.hin = h_in; d.ldh = ldh; d.stat = stat;
   d.B = B; d.HW = HW; d.C = C; d.L = L; d.id_ld = id_ld; d.slope = slope;

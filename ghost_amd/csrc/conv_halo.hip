@@ -1,0 +1,216 @@
+// ghost_amd — 3x3/s1/p1 convolution with the input staged once per channel block as a halo
+// tile (AAD_ResBlk's conv3x3, AADLayer.py:64,71; bf16).
+//
+// The implicit GEMM (conv_igemm.hip) gathers an A tile per K step: for a 3x3 conv every input
+// pixel is fetched nine times (once per tap), which makes the narrow-N convs of the 128x128 and
+// 256x256 stages (N = 64 / 128) bound by the vector-memory path, not the matrix cores.  Here a
+// workgroup owns a 16 x 32 output tile of one sample and 64 output channels; per block of 32
+// input channels it DMAs the 18 x 34 halo (1.2x the tile) and the block's 9 x 64 weight rows
+// into LDS (global_load_lds, source-side XOR swizzle), then runs all nine taps from LDS:
+//   tap (ty, tx): D[n][p] += W_t[n][c] . X[p + (ty, tx)][c]      (v_mfma_f32_16x16x32_bf16)
+// The weights are the MFMA A operand, so a lane's accumulators are 4 consecutive output
+// channels of one pixel and the epilogue stores 8 bytes per lane.
+// 8 waves, each 2 output rows (64 pixels) x 64 channels; 75 KB LDS -> two workgroups per CU,
+// which overlap one workgroup's DMA with the other's MFMAs.
+#include <cstdlib>
+
+#include "conv_halo.h"
+#include "ghost_common.h"
+
+namespace ghost {
+
+namespace {
+constexpr int TH = 16, TW = 32, BN = 64;
+constexpr int HWW = TW + 2, HHH = TH + 2;
+constexpr int HP = HHH * HWW;                    // 612 halo pixels
+constexpr int HPIECES = (HP + 15) / 16;          // 39 DMA pieces of 16 pixels x 64 B
+constexpr int WPIECES = 9 * BN / 16;             // 36 pieces of 16 weight rows x 64 B
+constexpr int HALO_B = HPIECES * 1024;
+constexpr int LDS_B = HALO_B + 9 * BN * 64;      // 39 KB + 36 KB
+constexpr int NWAVES = 8;
+constexpr int HPW = (HPIECES + NWAVES - 1) / NWAVES;   // halo pieces per wave (5)
+constexpr int WPW = (WPIECES + NWAVES - 1) / NWAVES;   // weight pieces per wave (5)
+}  // namespace
+
+struct HaloArgs {
+  const bf16* x;
+  const bf16* w;
+  bf16* y;
+  const float* scale;
+  const float* shift;
+  const bf16* res;
+  int H, W, Cin, ldx, N, Kpad, ldy, ldres, tanh_out;
+  float slope;
+  int tiles_x, tiles_y, nNt, ntiles;
+};
+
+__device__ __attribute__((aligned(16))) unsigned int g_halo_zero[64] = {0};
+
+GHOST_DEV int hswz(int r) { return (r >> 1) & 3; }   // conflict-free for 16 consecutive rows at any offset
+
+GHOST_DEV int xcd_tile(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+__global__ void __launch_bounds__(NWAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 8))) conv3x3_halo_kernel(const HaloArgs a) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_B];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  // tile order: channel tile fastest, then x, y, sample; XCD-contiguous so neighbouring tiles
+  // (shared halo rows, same input pixels for every channel tile) meet in one L2
+  int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int nt = t % a.nNt;
+  t /= a.nNt;
+  const int tx = t % a.tiles_x;
+  t /= a.tiles_x;
+  const int ty = t % a.tiles_y;
+  const int b = t / a.tiles_y;
+  const int y0 = ty * TH, x0 = tx * TW, n0 = nt * BN;
+  const long img = (long)b * a.H * a.W;
+  const bf16* __restrict__ xs = a.x + img * a.ldx;            // this sample
+  const bf16* __restrict__ ws = a.w + (long)n0 * a.Kpad;      // this channel tile
+
+  // this lane's DMA sources (32-bit element offsets within the sample / tile; + channel block)
+  const int prow = lane >> 2, slot = lane & 3;
+  int h_off[HPW];
+  unsigned h_ok = 0u;
+#pragma unroll
+  for (int j = 0; j < HPW; ++j) {
+    const int piece = wid + j * NWAVES;
+    const int P = piece * 16 + prow;
+    const int hy = P / HWW, hx = P - hy * HWW;
+    const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+    const bool ok = piece < HPIECES && P < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    h_off[j] = ok ? (iy * a.W + ix) * a.ldx + ((slot ^ hswz(P)) * 8) : 0;
+    h_ok |= (ok ? 1u : 0u) << j;
+  }
+  int w_off[WPW];
+#pragma unroll
+  for (int j = 0; j < WPW; ++j) {
+    const int piece = wid + j * NWAVES;           // = tap * 4 + 16-row group
+    const int tap = piece >> 2, n = (piece & 3) * 16 + prow;
+    w_off[j] = n * a.Kpad + tap * 32 + ((slot ^ hswz(n)) * 8);
+  }
+
+  f32x4 acc[4][4];   // [channel frag j][pixel frag i]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ncb = a.Cin / 32;
+  for (int cb = 0; cb < ncb; ++cb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int j = 0; j < HPW; ++j) {
+      const int piece = wid + j * NWAVES;
+      if (piece < HPIECES) {
+        const void* src = ((h_ok >> j) & 1u) ? (const void*)(xs + h_off[j] + cb * 32) : (const void*)g_halo_zero;
+        __builtin_amdgcn_global_load_lds(src, lds + piece * 1024, 16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) {
+      const int piece = wid + j * NWAVES;
+      if (piece < WPIECES)
+        __builtin_amdgcn_global_load_lds(ws + w_off[j] + cb * 288, lds + HALO_B + piece * 1024, 16, 0, 0);
+    }
+#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      // keep each tap's fragment reads after the previous tap's MFMAs are issued: hoisting all
+      // nine taps' reads needs ~300 VGPRs; the other waves of the SIMD hide the LDS latency
+      asm volatile("" ::: "memory");
+      const int dy = tap / 3, dx = tap - dy * 3;
+      bf16x8 wf[4], pf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = j * 16 + lr;
+        wf[j] = *reinterpret_cast<const bf16x8*>(lds + HALO_B + (tap * BN + n) * 64 + ((lq ^ hswz(n)) * 16));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int P = (wid * 2 + (i >> 1) + dy) * HWW + (i & 1) * 16 + lr + dx;
+        pf[i] = *reinterpret_cast<const bf16x8*>(lds + P * 64 + ((lq ^ hswz(P)) * 16));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], pf[i], acc[j][i], 0, 0, 0);
+    }
+    __syncthreads();   // every wave is done with this block's LDS before the next DMA
+  }
+
+  // epilogue: lane holds channels n0 + 16j + 4lq + r of pixel (row 2*wid + (i>>1), col 16(i&1) + lr)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int oy = y0 + wid * 2 + (i >> 1), ox = x0 + (i & 1) * 16 + lr;
+    const long pix = img + (long)oy * a.W + ox;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + j * 16 + lq * 4;
+      if (n >= a.N) continue;
+      float v[4];
+      float rv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.res) {
+        const uint2 raw = *reinterpret_cast<const uint2*>(a.res + pix * a.ldres + n);
+        const bf16* e = reinterpret_cast<const bf16*>(&raw);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rv[r] = (float)e[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = acc[j][i][r];
+        if (a.scale) s *= a.scale[n + r];
+        if (a.shift) s += a.shift[n + r];
+        s = s > 0.f ? s : s * a.slope;
+        s += rv[r];
+        if (a.tanh_out) s = tanhf(s);
+        v[r] = s;
+      }
+      uint2 o;
+      bf16* oe = reinterpret_cast<bf16*>(&o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) oe[r] = (bf16)v[r];
+      *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+    }
+  }
+}
+
+bool conv3x3_halo_supported(const ConvDesc& d) {
+  static const int enabled = [] {
+    const char* e = getenv("GHOST_CONV_HALO");
+    return e ? atoi(e) : 1;
+  }();
+  if (!enabled || d.kind != CONV_FWD || d.kh != 3 || d.kw != 3 || d.stride != 1 || d.pad != 1) return false;
+  if (d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD || d.u8 || d.force_split) return false;
+  if (d.Cin % 32 || d.ldx % 8 || d.N % BN || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
+  if (d.Hi % TH || d.Wi % TW || d.Kpad < 9 * d.Cin || d.Npad < d.N) return false;
+  if ((uintptr_t)d.x % 16 || (uintptr_t)d.w % 16 || (uintptr_t)d.y % 8 || (d.res && (uintptr_t)d.res % 8)) return false;
+  if ((long)d.Hi * d.Wi * d.ldx >= (1L << 31) || (long)d.Npad * d.Kpad >= (1L << 31)) return false;   // 32-bit offsets
+  // where it pays (tools/bench_ops.py): narrow N at the 64x64 .. 256x256 stages
+  static const int max_n = [] {
+    const char* e = getenv("GHOST_CONV_HALO_MAXN");
+    return e ? atoi(e) : 128;
+  }();
+  return d.N <= max_n && d.Hi >= 32;
+}
+
+int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
+  if (!conv3x3_halo_supported(d)) return -1;
+  HaloArgs a{};
+  a.x = (const bf16*)d.x; a.w = (const bf16*)d.w; a.y = (bf16*)d.y;
+  a.scale = d.scale; a.shift = d.shift; a.res = (const bf16*)d.res;
+  a.H = d.Hi; a.W = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx; a.N = d.N; a.Kpad = d.Kpad;
+  a.ldy = d.ldy; a.ldres = d.ldres; a.tanh_out = d.tanh_out; a.slope = d.slope;
+  a.tiles_x = d.Wi / TW; a.tiles_y = d.Hi / TH; a.nNt = d.N / BN;
+  a.ntiles = d.B * a.tiles_x * a.tiles_y * a.nNt;
+  hipLaunchKernelGGL(conv3x3_halo_kernel, dim3((unsigned)a.ntiles), dim3(NWAVES * 64), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+}  // namespace ghost

@@ -137,6 +137,12 @@ def pack_aad_v3(sd, prefix: str, dtype) -> Dict[str, torch.Tensor]:
     return {"w3": torch.cat(w3, 0).to(dtype).contiguous(), "b3": torch.cat(b3, 0).contiguous()}
 
 
+def v3_layout(c: int, ca: int) -> bool:
+    """AADLayers packed for the register-epilogue kernels too: aad_v3 (C in {64, 128}) and
+    aad_wide (C in {256, 512, 1024}, Ca <= 256); mirrors aei_runtime.hip declare_slots."""
+    return c in (64, 128) or (c in (256, 512, 1024) and ca <= 256)
+
+
 def aad_plan(backbone: str, num_blocks: int) -> List[Tuple[str, str]]:
     """(slot prefix, state_dict prefix) of every AADLayer in the runtime's plan order."""
     out = []
@@ -174,7 +180,7 @@ def pack_all(sd: Dict[str, torch.Tensor], backbone: str, num_blocks: int, c_id: 
     for slot, pre in aad_plan(backbone, num_blocks):
         for k, v in pack_aad(sd, pre, dtype).items():
             slots[f"{slot}.{k}"] = v
-        if dtype == torch.bfloat16 and sd[f"{pre}.conv1.weight"].shape[0] in (64, 128):
+        if dtype == torch.bfloat16 and v3_layout(*sd[f"{pre}.conv1.weight"].shape[:2]):
             for k, v in pack_aad_v3(sd, pre, dtype).items():
                 slots[f"{slot}.{k}"] = v
         ids_w += [sd[f"{pre}.fc1.weight"].float(), sd[f"{pre}.fc2.weight"].float()]

@@ -69,7 +69,9 @@ def nhwc(x):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cin,cout,k,s,p,H", [(32, 64, 4, 2, 1, 32), (3, 32, 4, 2, 1, 64), (64, 64, 3, 1, 1, 40),
-                                              (128, 3, 3, 1, 1, 32), (96, 200, 1, 1, 0, 9)])
+                                              (128, 3, 3, 1, 1, 32), (96, 200, 1, 1, 0, 9),
+                                              # halo-tiled 3x3 kernel shapes (bf16, H % 16, W % 32, N % 64)
+                                              (64, 64, 3, 1, 1, 64), (96, 128, 3, 1, 1, 32), (256, 64, 3, 1, 1, 32)])
 def test_conv2d_op(lib, dt, cin, cout, k, s, p, H):
     from ghost_amd import _lib
     from ghost_amd.network.pack import pack_conv, rup
@@ -393,7 +395,10 @@ def test_conv3x3_narrow_op(lib, dt, cin, cout, H, W, use_res):
 
 @pytest.mark.parametrize("c_x,c_a,n,B,L,up", [(64, 64, 256, 2, 2, 0), (64, 64, 256, 2, 1, 0), (128, 128, 128, 2, 1, 0),
                                               (64, 32, 128, 4, 2, 0), (128, 64, 64, 8, 1, 0), (128, 32, 64, 8, 1, 0),
-                                              (64, 64, 256, 2, 2, 1), (64, 32, 128, 4, 2, 1), (64, 64, 64, 8, 1, 1)])
+                                              (64, 64, 256, 2, 2, 1), (64, 32, 128, 4, 2, 1), (64, 64, 64, 8, 1, 1),
+                                              # aad_wide: one 64-channel tile per workgroup
+                                              (256, 128, 64, 8, 1, 0), (512, 256, 32, 8, 1, 0),
+                                              (1024, 256, 16, 16, 1, 0), (512, 64, 32, 4, 1, 0)])
 def test_aad_layers_v3_vs_oracle(lib, c_x, c_a, n, B, L, up):
     """Register-epilogue AAD kernel (1 or 2 layers sharing h_in / z_attr) against the oracle AADLayer;
     up = 1: h_in is read through the bilinear x2 upsample of an n/2 source (AEI_Net.py:137)."""

@@ -87,6 +87,38 @@ def aad_cases(lib, iters, dt=torch.bfloat16):
               flush=True)
 
 
+def aad_v3_cases(lib, iters):
+    """Register-epilogue AAD kernels through ghost_aad_layers_v3_nhwc (stats + kernel)."""
+    import ctypes as C
+    B, dt = 64, torch.bfloat16
+    st = torch.cuda.current_stream().cuda_stream
+    ws = torch.empty(512 << 20, dtype=torch.uint8, device=DEV)
+    for c, ca, n, L, up in [(64, 64, 256, 2, 1), (64, 64, 256, 2, 0), (64, 64, 256, 1, 0), (128, 64, 128, 1, 0),
+                            (256, 128, 64, 1, 0), (512, 256, 32, 1, 0), (1024, 512 // 2, 16, 1, 0)]:
+        hn = n // 2 if up else n
+        h = torch.randn(B, hn, hn, c, device=DEV).to(dt)
+        za = torch.randn(B, n, n, ca, device=DEV).to(dt)
+        keep, w3, b3, wh, bh, ids, outs = [], [], [], [], [], [], []
+        for _ in range(L):
+            t = [torch.randn(c // 64 * 128, ca, device=DEV).to(dt) * 0.05, torch.zeros(c // 64 * 128, device=DEV),
+                 torch.randn(c, device=DEV) * 0.05, torch.zeros(1, device=DEV), torch.randn(B, 2 * c, device=DEV),
+                 torch.empty(B, n, n, c, dtype=dt, device=DEV)]
+            keep += t
+            for lst, v in zip((w3, b3, wh, bh, ids, outs), t):
+                lst.append(v.data_ptr())
+        arr = lambda xs: (C.c_void_p * L)(*xs)  # noqa: E731
+        ldo = (C.c_int * L)(*([c] * L))
+
+        def run():
+            _lib.check(lib.ghost_aad_layers_v3_nhwc(h.data_ptr(), c, up, za.data_ptr(), ca, B, n, n, c, ca, L,
+                                                    arr(w3), arr(b3), arr(wh), arr(bh), arr(ids), 2 * c, 0.0,
+                                                    arr(outs), ldo, ws.data_ptr(), ws.numel(), st))
+        us = timeit(run, iters)
+        alg = B * n * n * L * (2 * c + ca) * 2    # SURVEY formula: per layer |h_in| + |z_attr| + |out|
+        print(f"aadv3 C={c:4d} Ca={ca:4d} n={n:3d} L={L} up={up} (stats+kernel) {us:9.1f} us  "
+              f"{alg / us / 1e3:7.1f} GB/s(alg)", flush=True)
+
+
 def up_cases(lib, iters, dt=torch.bfloat16):
     B = 64
     st = torch.cuda.current_stream().cuda_stream
@@ -154,6 +186,8 @@ def main():
         conv_cases(lib, a.iters)
     if a.only in ("", "aad"):
         aad_cases(lib, a.iters)
+    if a.only in ("", "aad", "aadv3"):
+        aad_v3_cases(lib, a.iters)
     if a.only in ("", "up"):
         up_cases(lib, a.iters)
     if a.only in ("", "stats"):
