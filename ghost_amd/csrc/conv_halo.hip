@@ -192,12 +192,13 @@ bool conv3x3_halo_supported(const ConvDesc& d) {
   if (d.Hi % TH || d.Wi % TW || d.Kpad < 9 * d.Cin || d.Npad < d.N) return false;
   if ((uintptr_t)d.x % 16 || (uintptr_t)d.w % 16 || (uintptr_t)d.y % 8 || (d.res && (uintptr_t)d.res % 8)) return false;
   if ((long)d.Hi * d.Wi * d.ldx >= (1L << 31) || (long)d.Npad * d.Kpad >= (1L << 31)) return false;   // 32-bit offsets
-  // where it pays (tools/bench_ops.py): narrow N at the 64x64 .. 256x256 stages
+  // measured (tools/bench_ops.py, B = 64): faster than the implicit GEMM at every generator stage
+  // from 32x32 up (N = 64 .. 512); GHOST_CONV_HALO_MAXN caps N for A/B runs
   static const int max_n = [] {
     const char* e = getenv("GHOST_CONV_HALO_MAXN");
-    return e ? atoi(e) : 128;
+    return e ? atoi(e) : 1 << 30;
   }();
-  return d.N <= max_n && d.Hi >= 32;
+  return d.N <= max_n;
 }
 
 int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
