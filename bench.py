@@ -125,8 +125,13 @@ def main():
         step()
     torch.cuda.synchronize()
     prof = not a.no_profile
+    names = ["aad_all", "aad_dual_256", "conv3x3_all", "conv3x3_256", "in_stats_mask", "encoder", "upsample",
+             "id_proj"]
+    classes = {}
     if prof:
-        G.profile(0xFF)
+        # inside the timed region only the roofline kernel is bracketed (one HIP event pair per step,
+        # recorded on the launch stream around each of its launches)
+        G.profile(1 << names.index("aad_dual_256"))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -141,13 +146,16 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-
-    classes = {}
     if prof:
-        names = ["aad_all", "aad_dual_256", "conv3x3_all", "conv3x3_256", "in_stats_mask", "encoder", "upsample",
-                 "id_proj"]
+        classes["aad_dual_256"] = G.profile_read(names.index("aad_dual_256"))
+        # per-class breakdown from a separate, untimed pass (every kernel class bracketed)
+        G.profile(0xFF)
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
         for i, n in enumerate(names):
-            classes[n] = G.profile_read(i)
+            if n != "aad_dual_256":
+                classes[n] = G.profile_read(i)
         G.profile(0)
 
     if rank == 0:
@@ -189,6 +197,8 @@ def main():
                                                / (aad["ms"] / 1e3) / 1e9, 1)
                 res["aad_decoder_hbm_frac"] = round(res["aad_decoder_gbs"] / HBM_PEAK_GBS, 4)
             res["kernel_ms_per_step"] = {k: round(v["ms"] / a.steps, 3) for k, v in classes.items()}
+            res["kernel_ms_per_step_note"] = ("aad_dual_256 from the timed region; the other classes from an "
+                                              "untimed pass with every class bracketed by HIP events")
         if world == 1 and a.cpu_seconds > 0:
             res["cpu_baseline"] = cpu_baseline(a.backbone, a.num_blocks, a.cpu_seconds)
         print(json.dumps(res), flush=True)

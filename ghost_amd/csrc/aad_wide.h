@@ -16,6 +16,7 @@ struct AadWideDesc {
   const float* wh = nullptr;                   // conv_h weight [C]
   const float* bh = nullptr;                   // conv_h bias [1]
   const float* idgb = nullptr;                 // [B][id_ld]: gamma_id at c, beta_id at C + c
+  const float* mask = nullptr;                 // [B*HW] sigmoid mask of this layer (aad_mask)
   void* out = nullptr;       int ldo = 0;
 };
 

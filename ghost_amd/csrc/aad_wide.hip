@@ -4,9 +4,10 @@
 // accumulators are gamma/beta of 16 channels of one pixel, register epilogue), but a
 // workgroup owns ONE 64-channel tile of a block of pixels: the tile's 128 permuted weight
 // rows (pack.py pack_aad_v3) fit LDS for any Ca <= 256, where all C/64 tiles would not.
-// The mask needs every channel of the pixel, so each workgroup forms it from the whole h_in
-// row; the C/64 workgroups of one pixel block are adjacent in launch order (and on one XCD),
-// so those re-reads are L2 hits and HBM sees h_in, z_attr and out about once each.
+// The mask needs every channel of the pixel: it comes from one aad_mask pass over h_in
+// (ops.hip), so a 16-pixel tile here is one round trip: z_attr row, the tile's 64 channels of
+// h_in and the mask.  The C/64 workgroups of one pixel block are adjacent in launch order (and
+// on one XCD), so their shared z_attr reads are L2 hits.
 #include <cstdlib>
 
 #include "aad_wide.h"
@@ -23,6 +24,7 @@ struct AadWideArgs {
   const float* wh;
   const float* bh;
   const float* idgb;
+  const float* mask;
   bf16* out;
   int lda, ldh, ldo, id_ld, HW, PPW, nblk;
   float slope;
@@ -41,15 +43,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   constexpr int CT = C / 64;
   constexpr int KS = CA / 32;
   constexpr int WLD = CA + 8;
-  constexpr int NCH = C / 32;        // 16-byte chunks of a pixel per lane group position
   __shared__ __attribute__((aligned(16))) bf16 s_w[128 * WLD];
   __shared__ __attribute__((aligned(16))) float s_b[128];
-  __shared__ __attribute__((aligned(16))) float s_cf[C];    // wh * rstd, every channel (mask)
   __shared__ __attribute__((aligned(16))) float s_rs[64];
   __shared__ __attribute__((aligned(16))) float s_nm[64];
   __shared__ __attribute__((aligned(16))) float s_gi[64];
   __shared__ __attribute__((aligned(16))) float s_bi[64];
-  __shared__ float s_k;
 
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
   const int tile = wide_xcd_tile(blockIdx.x, gridDim.x);
@@ -63,7 +62,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
         *reinterpret_cast<const u32x4*>(a.w3 + (long)(ct * 128 + row) * CA + kc * 8);
   }
   for (int i = tid; i < 128; i += kWideWaves * 64) s_b[i] = a.b3[ct * 128 + i];
-  for (int c = tid; c < C; c += kWideWaves * 64) s_cf[c] = a.wh[c] * a.stat[((long)b * C + c) * 2 + 1];
   if (tid < 64) {
     const int c = ct * 64 + tid;
     const float mu = a.stat[((long)b * C + c) * 2], rs = a.stat[((long)b * C + c) * 2 + 1];
@@ -72,60 +70,30 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     s_gi[tid] = a.idgb[(long)b * a.id_ld + c];
     s_bi[tid] = a.idgb[(long)b * a.id_ld + C + c];
   }
-  if (wid == 1) {   // k = sum_c wh_c * (-mu_c * rstd_c): the mask logit is sum_c cf_c h_c + k + bh
-    float k = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      const float mu = a.stat[((long)b * C + c) * 2], rs = a.stat[((long)b * C + c) * 2 + 1];
-      k = fmaf(a.wh[c], -mu * rs, k);
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) k += __shfl_xor(k, o, 64);
-    if (lane == 0) s_k = k;
-  }
   __syncthreads();
-  const float bh = a.bh[0] + s_k;
 
   const int ntiles = a.PPW / 16;
   for (int t = wid; t < ntiles; t += kWideWaves) {
     asm volatile("" ::: "memory");
     const long p = p_begin + t * 16 + lr;
-    const bf16* hrow = a.hin + p * a.ldh;
-    // z_attr: shallow rows are issued before the mask pass (overlapping it); deep rows (Ca = 256)
-    // are streamed four k-steps at a time inside the GEMM (second half: L1 hits)
-    constexpr bool ZEARLY = KS <= 4;
+    const bf16* hrow = a.hin + p * a.ldh + ct * 64;
+    // one round trip: the z_attr row (Ca <= 256; deeper rows would stream inside the GEMM), this
+    // tile's two h_in chunks and the mask
+    constexpr bool ZEARLY = KS <= 8;
     u32x4 zc[ZEARLY ? KS : 1];
     if constexpr (ZEARLY) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + ks * 32 + lq * 8);
     }
+    u32x4 hc[2];
+#pragma unroll
+    for (int sh = 0; sh < 2; ++sh) hc[sh] = *reinterpret_cast<const u32x4*>(hrow + sh * 32 + lq * 8);
+    const float Mk = a.mask[p];
 
-    // mask over all C channels, 8 chunks at a time (bounded registers)
-    float ms = 0.f;
-#pragma unroll 1
-    for (int g = 0; g < NCH; g += 8) {
-      asm volatile("" ::: "memory");
-      u32x4 hv8[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (g + u < NCH) hv8[u] = *reinterpret_cast<const u32x4*>(hrow + (g + u) * 32 + lq * 8);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (g + u >= NCH) break;
-        if (NCH > 8) asm volatile("" ::: "memory");   // one chunk's cf values live at a time
-        const bf16* hv = reinterpret_cast<const bf16*>(&hv8[u]);
-        const int c0 = (g + u) * 32 + lq * 8;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ms = fmaf(s_cf[c0 + e], (float)hv[e], ms);
-      }
-    }
-    ms += __shfl_xor(ms, 16, 64);
-    ms += __shfl_xor(ms, 32, 64);
-    const float Mk = sigmoidf_ref(ms + bh);
 #pragma unroll
     for (int sh = 0; sh < 2; ++sh) {
       asm volatile("" ::: "memory");
       const int cl = sh * 32 + lq * 8;     // channel within the tile
-      const u32x4 hraw = *reinterpret_cast<const u32x4*>(hrow + ct * 64 + cl);   // L1 hit (mask pass)
       f32x4 acc[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -158,7 +126,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
           }
         }
       }
-      const bf16* hv = reinterpret_cast<const bf16*>(&hraw);
+      const bf16* hv = reinterpret_cast<const bf16*>(&hc[sh]);
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -198,10 +166,10 @@ bool aad_wide_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, 
 }
 
 int aad_wide(const AadWideDesc& d, hipStream_t s) {
-  if (!aad_wide_supported(GHOST_BF16, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo)) return -1;
+  if (!aad_wide_supported(GHOST_BF16, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo) || !d.mask) return -1;
   AadWideArgs a{};
   a.za = (const bf16*)d.za; a.hin = (const bf16*)d.hin; a.stat = d.stat;
-  a.w3 = (const bf16*)d.w3; a.b3 = d.b3; a.wh = d.wh; a.bh = d.bh; a.idgb = d.idgb; a.out = (bf16*)d.out;
+  a.w3 = (const bf16*)d.w3; a.b3 = d.b3; a.wh = d.wh; a.bh = d.bh; a.idgb = d.idgb; a.mask = d.mask; a.out = (bf16*)d.out;
   a.lda = d.lda; a.ldh = d.ldh; a.ldo = d.ldo; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
   a.PPW = wide_ppw(d.B, d.HW, d.C);
   a.nblk = (int)((long)d.B * d.HW / a.PPW);

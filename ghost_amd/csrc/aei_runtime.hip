@@ -354,9 +354,25 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     return;
   }
   if (!v3) {
-    bool wide = aad_wide_supported(h->dt, B, n * n, C, Ca, lda, ldh, 8);
+    bool wide = aad_wide_supported(h->dt, B, n * n, C, Ca, lda, ldh, 8) && ls.size() <= 2;
     for (auto& l : ls) wide = wide && l.ldo % 8 == 0;
-    for (auto& l : ls) {
+    // the masks of every layer of the group from one pass over h_in
+    float* masks[2] = {nullptr, nullptr};
+    if (wide) {
+      for (size_t i = 0; i < ls.size(); ++i) masks[i] = (float*)c.alloc((size_t)B * n * n * sizeof(float));
+      const float* wh0 = (const float*)c.W(ls[0].name + ".wh");
+      const float* bh0 = (const float*)c.W(ls[0].name + ".bh");
+      const float* wh1 = ls.size() > 1 ? (const float*)c.W(ls[1].name + ".wh") : nullptr;
+      const float* bh1 = ls.size() > 1 ? (const float*)c.W(ls[1].name + ".bh") : nullptr;
+      if (c.ok() && !c.dry) {
+        int e = c.prof_begin(4);
+        c.check(aad_mask2(h->dt, hin, ldh, B, n * n, C, stat, wh0, bh0, masks[0], wh1, bh1, masks[1], c.s),
+                "aad_mask2");
+        c.prof_end(4, e, (double)B * n * n * C * h->esz, 0);
+      }
+    }
+    for (size_t li = 0; li < ls.size(); ++li) {
+      const AadOut& l = ls[li];
       if (!wide) {
         aad(c, l.name, hin, ldh, stat, za, lda, Ca, B, n, C, l.id_off, idgb, l.out, l.ldo);
         continue;
@@ -370,6 +386,7 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
       d.bh = (const float*)c.W(l.name + ".bh");
       d.idgb = idgb ? idgb + l.id_off : nullptr;
       d.out = l.out; d.ldo = l.ldo;
+      d.mask = masks[li];
       if (!c.ok() || c.dry) continue;
       const double Pn = (double)B * n * n;
       int e_all = c.prof_begin(0);
@@ -949,7 +966,13 @@ extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, con
                 : in_stats(GHOST_BF16, h_in, ldh, B, HW, C, stat, base + stat_b, sc, s);
   if (rc) return fail(rc, "aad_v3: in_stats failed");
   if (wide) {
+    const size_t mask_b = ((size_t)B * HW * sizeof(float) + 255) & ~size_t(255);
+    if ((size_t)ws_bytes < stat_b + sc + mask_b + 256) return fail(GHOST_ENOWS, "aad_wide: workspace too small");
+    float* mask = (float*)(base + stat_b + sc);
+    rc = aad_mask(GHOST_BF16, h_in, ldh, B, HW, C, stat, wh[0], bh[0], mask, s);
+    if (rc) return fail(rc, "aad_wide: aad_mask failed");
     AadWideDesc w;
+    w.mask = mask;
     w.za = z_attr; w.lda = lda; w.Ca = Ca; w.hin = h_in; w.ldh = ldh; w.stat = stat;
     w.B = B; w.HW = HW; w.C = C; w.id_ld = id_ld; w.slope = slope;
     w.w3 = w3[0]; w.b3 = b3[0]; w.wh = wh[0]; w.bh = bh[0]; w.idgb = idgb[0]; w.out = out[0]; w.ldo = ldo[0];

@@ -19,18 +19,23 @@
 
 namespace ghost {
 
-namespace {
-constexpr int TH = 16, TW = 32, BN = 64;
-constexpr int HWW = TW + 2, HHH = TH + 2;
-constexpr int HP = HHH * HWW;                    // 612 halo pixels
-constexpr int HPIECES = (HP + 15) / 16;          // 39 DMA pieces of 16 pixels x 64 B
-constexpr int WPIECES = 9 * BN / 16;             // 36 pieces of 16 weight rows x 64 B
-constexpr int HALO_B = HPIECES * 1024;
-constexpr int LDS_B = HALO_B + 9 * BN * 64;      // 39 KB + 36 KB
-constexpr int NWAVES = 8;
-constexpr int HPW = (HPIECES + NWAVES - 1) / NWAVES;   // halo pieces per wave (5)
-constexpr int WPW = (WPIECES + NWAVES - 1) / NWAVES;   // weight pieces per wave (5)
-}  // namespace
+// tile configurations: TH x TW output pixels, WM x WN waves of 64 pixels x 64 channels each
+template <int TH_, int TW_, int WM_, int WN_>
+struct HaloCfg {
+  static constexpr int TH = TH_, TW = TW_, WM = WM_, WN = WN_;
+  static constexpr int BN = 64 * WN, NW = WM * WN;
+  static constexpr int HWW = TW + 2, HHH = TH + 2;
+  static constexpr int HP = HHH * HWW;                      // halo pixels
+  static constexpr int HPIECES = (HP + 15) / 16;            // DMA pieces of 16 pixels x 64 B
+  static constexpr int WPIECES = 9 * BN / 16;               // pieces of 16 weight rows x 64 B
+  static constexpr int HALO_B = HPIECES * 1024;
+  static constexpr int LDS_B = HALO_B + 9 * BN * 64;
+  static constexpr int HPW = (HPIECES + NW - 1) / NW;       // halo pieces per wave
+  static constexpr int WPW = (WPIECES + NW - 1) / NW;       // weight pieces per wave
+  static_assert(TH * TW == 64 * WM, "each wave owns 64 output pixels");
+};
+using HaloWide = HaloCfg<16, 32, 8, 1>;    // W % 32 == 0: 16 x 32 tile, 8 waves, 75 KB LDS
+using HaloSmall = HaloCfg<16, 16, 4, 1>;   // W == 16: 16 x 16 tile, 4 waves, 57 KB LDS
 
 struct HaloArgs {
   const bf16* x;
@@ -54,9 +59,14 @@ GHOST_DEV int xcd_tile(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-__global__ void __launch_bounds__(NWAVES * 64) __attribute__((amdgpu_waves_per_eu(4, 8))) conv3x3_halo_kernel(const HaloArgs a) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_B];
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+template <class G>
+__global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8))) conv3x3_halo_kernel(const HaloArgs a) {
+  constexpr int TH = G::TH, TW = G::TW, BN = G::BN, HWW = G::HWW, HP = G::HP, HPIECES = G::HPIECES;
+  constexpr int WPIECES = G::WPIECES, HALO_B = G::HALO_B, NWAVES = G::NW, HPW = G::HPW, WPW = G::WPW;
+  constexpr int RPW = 64 / TW;                       // output rows per wave
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[G::LDS_B];
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int wid = tid >> 6, wm = wid % G::WM, wn = wid / G::WM;
   // tile order: channel tile fastest, then x, y, sample; XCD-contiguous so neighbouring tiles
   // (shared halo rows, same input pixels for every channel tile) meet in one L2
   int t = xcd_tile(blockIdx.x, gridDim.x);
@@ -88,8 +98,8 @@ __global__ void __launch_bounds__(NWAVES * 64) __attribute__((amdgpu_waves_per_e
   int w_off[WPW];
 #pragma unroll
   for (int j = 0; j < WPW; ++j) {
-    const int piece = wid + j * NWAVES;           // = tap * 4 + 16-row group
-    const int tap = piece >> 2, n = (piece & 3) * 16 + prow;
+    const int piece = wid + j * NWAVES;           // = tap * BN/16 + 16-row group
+    const int tap = piece / (BN / 16), n = (piece % (BN / 16)) * 16 + prow;
     w_off[j] = n * a.Kpad + tap * 32 + ((slot ^ hswz(n)) * 8);
   }
 
@@ -129,12 +139,12 @@ __global__ void __launch_bounds__(NWAVES * 64) __attribute__((amdgpu_waves_per_e
       bf16x8 wf[4], pf[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int n = j * 16 + lr;
+        const int n = wn * 64 + j * 16 + lr;
         wf[j] = *reinterpret_cast<const bf16x8*>(lds + HALO_B + (tap * BN + n) * 64 + ((lq ^ hswz(n)) * 16));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int P = (wid * 2 + (i >> 1) + dy) * HWW + (i & 1) * 16 + lr + dx;
+        const int P = (wm * RPW + (i * 16) / TW + dy) * HWW + (i * 16) % TW + lr + dx;
         pf[i] = *reinterpret_cast<const bf16x8*>(lds + P * 64 + ((lq ^ hswz(P)) * 16));
       }
 #pragma unroll
@@ -145,14 +155,15 @@ __global__ void __launch_bounds__(NWAVES * 64) __attribute__((amdgpu_waves_per_e
     __syncthreads();   // every wave is done with this block's LDS before the next DMA
   }
 
-  // epilogue: lane holds channels n0 + 16j + 4lq + r of pixel (row 2*wid + (i>>1), col 16(i&1) + lr)
+  // epilogue: lane holds channels n0 + 64wn + 16j + 4lq + r of pixel (row RPW*wm + 16i/TW,
+  // column 16i % TW + lr)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int oy = y0 + wid * 2 + (i >> 1), ox = x0 + (i & 1) * 16 + lr;
+    const int oy = y0 + wm * RPW + (i * 16) / TW, ox = x0 + (i * 16) % TW + lr;
     const long pix = img + (long)oy * a.W + ox;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int n = n0 + j * 16 + lq * 4;
+      const int n = n0 + wn * 64 + j * 16 + lq * 4;
       if (n >= a.N) continue;
       float v[4];
       float rv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -188,8 +199,10 @@ bool conv3x3_halo_supported(const ConvDesc& d) {
   }();
   if (!enabled || d.kind != CONV_FWD || d.kh != 3 || d.kw != 3 || d.stride != 1 || d.pad != 1) return false;
   if (d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD || d.u8 || d.force_split) return false;
-  if (d.Cin % 32 || d.ldx % 8 || d.N % BN || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
-  if (d.Hi % TH || d.Wi % TW || d.Kpad < 9 * d.Cin || d.Npad < d.N) return false;
+  if (d.Cin % 32 || d.ldx % 8 || d.N % 64 || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
+  const bool wide = d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0;
+  const bool small = d.Wi == HaloSmall::TW && d.Hi % HaloSmall::TH == 0;
+  if ((!wide && !small) || d.Kpad < 9 * d.Cin || d.Npad < d.N) return false;
   if ((uintptr_t)d.x % 16 || (uintptr_t)d.w % 16 || (uintptr_t)d.y % 8 || (d.res && (uintptr_t)d.res % 8)) return false;
   if ((long)d.Hi * d.Wi * d.ldx >= (1L << 31) || (long)d.Npad * d.Kpad >= (1L << 31)) return false;   // 32-bit offsets
   // measured (tools/bench_ops.py, B = 64): faster than the implicit GEMM at every generator stage
@@ -201,17 +214,23 @@ bool conv3x3_halo_supported(const ConvDesc& d) {
   return d.N <= max_n;
 }
 
-int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
-  if (!conv3x3_halo_supported(d)) return -1;
+template <class G>
+static int halo_launch(const ConvDesc& d, hipStream_t s) {
   HaloArgs a{};
   a.x = (const bf16*)d.x; a.w = (const bf16*)d.w; a.y = (bf16*)d.y;
   a.scale = d.scale; a.shift = d.shift; a.res = (const bf16*)d.res;
   a.H = d.Hi; a.W = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx; a.N = d.N; a.Kpad = d.Kpad;
   a.ldy = d.ldy; a.ldres = d.ldres; a.tanh_out = d.tanh_out; a.slope = d.slope;
-  a.tiles_x = d.Wi / TW; a.tiles_y = d.Hi / TH; a.nNt = d.N / BN;
+  a.tiles_x = d.Wi / G::TW; a.tiles_y = d.Hi / G::TH; a.nNt = (d.N + G::BN - 1) / G::BN;
   a.ntiles = d.B * a.tiles_x * a.tiles_y * a.nNt;
-  hipLaunchKernelGGL(conv3x3_halo_kernel, dim3((unsigned)a.ntiles), dim3(NWAVES * 64), 0, s, a);
+  hipLaunchKernelGGL(conv3x3_halo_kernel<G>, dim3((unsigned)a.ntiles), dim3(G::NW * 64), 0, s, a);
   return (int)hipGetLastError();
+}
+
+int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
+  if (!conv3x3_halo_supported(d)) return -1;
+  if (d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0) return halo_launch<HaloWide>(d, s);
+  return halo_launch<HaloSmall>(d, s);
 }
 
 }  // namespace ghost

@@ -20,6 +20,9 @@ int in_stats_up2x(int dt, const void* x, int ldx, int B, int H, int W, int C, fl
 // AAD mask: M[p] = sigmoid(sum_c wh[c] * (h[p,c]-mu[b,c])*rstd[b,c] + bh)   (AADLayer.py:35)
 int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh,
              const float* bh, float* mask, hipStream_t s);
+// the masks of two AADLayers reading the same h_in in one pass (wh1 == nullptr: one layer)
+int aad_mask2(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh0,
+              const float* bh0, float* mask0, const float* wh1, const float* bh1, float* mask1, hipStream_t s);
 
 // bilinear x2, align_corners=True, NHWC (AEI_Net.py:94,125-137)
 int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C, hipStream_t s);

@@ -1,6 +1,8 @@
 // ghost_amd — bandwidth-bound kernels: InstanceNorm statistics, AAD mask, bilinear x2,
 // and the layout/precision conversions at the AEI_Net boundary.  All NHWC, 16-byte
 // vector accesses along channels, fp32 arithmetic.
+#include <algorithm>
+
 #include "ghost_common.h"
 #include "ops.h"
 #include "up2x.h"
@@ -147,52 +149,86 @@ int in_stats_up2x(int dt, const void* x, int ldx, int B, int H, int W, int C, fl
 }
 
 // ---------------------------------------------------------------------------
-// AAD mask: one lane group of G = min(64, C/VEC) lanes per pixel
+// AAD mask: M_l[p] = sigmoid(sum_c wh_l[c] * (h[p,c] - mu[b,c]) * rstd[b,c] + bh_l)  (AADLayer.py:35)
+// grid (pixel blocks of one sample, B); per-channel tables (wh*rstd, mu) staged in LDS once per
+// block; one lane group of G = min(64, C/VEC) lanes per pixel; L <= 2 layers sharing h_in.
 // ---------------------------------------------------------------------------
-template <typename T>
+template <typename T, int L>
 __global__ void __launch_bounds__(256)
-aad_mask_kernel(const T* __restrict__ h, int ldh, long P, int HW, int C, int G, const float* __restrict__ stat,
-                const float* __restrict__ wh, const float* __restrict__ bh, float* __restrict__ mask) {
+aad_mask_kernel(const T* __restrict__ h, int ldh, int HW, int C, int G, int ppb, const float* __restrict__ stat,
+                const float* __restrict__ wh0, const float* __restrict__ bh0, float* __restrict__ mask0,
+                const float* __restrict__ wh1, const float* __restrict__ bh1, float* __restrict__ mask1) {
   constexpr int VEC = Vec16<T>::N;
-  const int t = threadIdx.x;
-  const int ppb = 256 / G;
-  const long p = (long)blockIdx.x * ppb + t / G;
-  const int gl = t % G;
-  float s = 0.f;
-  if (p < P) {
-    const int b = (int)(p / HW);
-    const float* st = stat + (long)b * C * 2;
-    for (int ci = gl; ci < C / VEC; ci += G) {
-      float v[VEC];
-      load16_f(h + p * ldh + ci * VEC, v);
+  extern __shared__ float s_tab[];   // [L][C] wh * rstd, [C] mean
+  float* s_mu = s_tab + L * C;
+  const int t = threadIdx.x, b = blockIdx.y;
+  const float* st = stat + (long)b * C * 2;
+  for (int c = t; c < C; c += 256) {
+    const float mu = st[2 * c], rs = st[2 * c + 1];
+    s_mu[c] = mu;
+    s_tab[c] = wh0[c] * rs;
+    if (L == 2) s_tab[C + c] = wh1[c] * rs;
+  }
+  __syncthreads();
+  const int per = 256 / G, gl = t % G;
+  const long base = (long)b * HW;
+  const int pend = min(HW, (blockIdx.x + 1) * ppb);
+  // the G lanes of a pixel share q (and the trip count), so the in-group shuffles stay converged
+  for (int q = blockIdx.x * ppb + t / G; q < pend; q += per) {
+    float s0 = 0.f, s1 = 0.f;
+    {
+      const T* hp = h + (base + q) * ldh;
+      for (int ci = gl; ci < C / VEC; ci += G) {
+        float v[VEC];
+        load16_f(hp + ci * VEC, v);
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        const int c = ci * VEC + e;
-        s = fmaf(wh[c], (v[e] - st[2 * c]) * st[2 * c + 1], s);
+        for (int e = 0; e < VEC; ++e) {
+          const int c = ci * VEC + e;
+          const float d = v[e] - s_mu[c];
+          s0 = fmaf(s_tab[c], d, s0);
+          if (L == 2) s1 = fmaf(s_tab[C + c], d, s1);
+        }
       }
     }
+    s0 = group_sum(s0, G);
+    if (L == 2) s1 = group_sum(s1, G);
+    if (gl == 0) {
+      mask0[base + q] = sigmoidf_ref(s0 + bh0[0]);
+      if (L == 2) mask1[base + q] = sigmoidf_ref(s1 + bh1[0]);
+    }
   }
-  s = group_sum(s, G);
-  if (p < P && gl == 0) mask[p] = sigmoidf_ref(s + bh[0]);
 }
 
-int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh, const float* bh,
-             float* mask, hipStream_t s) {
+int aad_mask2(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh0,
+              const float* bh0, float* mask0, const float* wh1, const float* bh1, float* mask1, hipStream_t s) {
   const int vec = dt == GHOST_F32 ? 4 : 8;
   if (C % vec || ldh % vec || (uintptr_t)h % 16) return -1;
   int G = C / vec;
   if (G > 64) G = 64;
   if (G & (G - 1)) return -1;   // power-of-two lane groups
-  const long P = (long)B * HW;
-  const int ppb = 256 / G;
-  dim3 grid((unsigned)((P + ppb - 1) / ppb));
-  if (dt == GHOST_F32)
-    hipLaunchKernelGGL(aad_mask_kernel<float>, grid, dim3(256), 0, s, (const float*)h, ldh, P, HW, C, G, stat, wh, bh, mask);
-  else if (dt == GHOST_BF16)
-    hipLaunchKernelGGL(aad_mask_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)h, ldh, P, HW, C, G, stat, wh, bh, mask);
-  else
+  // >= ~2048 blocks to fill the chip; each block stages the tables once for its ppb pixels
+  int ppb = (int)std::min<long>(256, std::max<long>(256 / G, (long)HW * B / 2048));
+  if (ppb > HW) ppb = HW;
+  dim3 grid((unsigned)((HW + ppb - 1) / ppb), (unsigned)B);
+  const int L = wh1 ? 2 : 1;
+  const size_t lds = (size_t)(L + 1) * C * sizeof(float);
+#define GHOST_M(T, l)                                                                                            \
+  hipLaunchKernelGGL((aad_mask_kernel<T, l>), grid, dim3(256), lds, s, (const T*)h, ldh, HW, C, G, ppb, stat, wh0, \
+                     bh0, mask0, wh1, bh1, mask1)
+  if (dt == GHOST_F32) {
+    if (L == 2) GHOST_M(float, 2); else GHOST_M(float, 1);
+  } else if (dt == GHOST_BF16) {
+    if (L == 2) GHOST_M(bf16, 2); else GHOST_M(bf16, 1);
+  } else {
     return -1;
+  }
+#undef GHOST_M
   return (int)hipGetLastError();
+}
+
+int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh, const float* bh,
+             float* mask, hipStream_t s) {
+  return aad_mask2(dt, h, ldh, B, HW, C, stat, wh, bh, mask, nullptr, nullptr, nullptr, s);
 }
 
 // ---------------------------------------------------------------------------

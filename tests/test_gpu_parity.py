@@ -71,7 +71,8 @@ def nhwc(x):
 @pytest.mark.parametrize("cin,cout,k,s,p,H", [(32, 64, 4, 2, 1, 32), (3, 32, 4, 2, 1, 64), (64, 64, 3, 1, 1, 40),
                                               (128, 3, 3, 1, 1, 32), (96, 200, 1, 1, 0, 9),
                                               # halo-tiled 3x3 kernel shapes (bf16, H % 16, W % 32, N % 64)
-                                              (64, 64, 3, 1, 1, 64), (96, 128, 3, 1, 1, 32), (256, 64, 3, 1, 1, 32)])
+                                              (64, 64, 3, 1, 1, 64), (96, 128, 3, 1, 1, 32), (256, 64, 3, 1, 1, 32),
+                                              (128, 192, 3, 1, 1, 16)])
 def test_conv2d_op(lib, dt, cin, cout, k, s, p, H):
     from ghost_amd import _lib
     from ghost_amd.network.pack import pack_conv, rup
