@@ -243,7 +243,7 @@ void encoder(Ctx& c, const void* xin, int B, void* const attr[8]) {
     }
   }
   // down path: conv_i = Conv4x4/s2/p1 -> BN -> LReLU(0.1)
-  Buf in{const_cast<void*>(xin), 3};
+  Buf in{const_cast<void*>(xin), 4};
   for (int i = 1; i <= 7; ++i) {
     const int ci = kEncDown[i - 1][0], co = kEncDown[i - 1][1];
     Buf out = i <= 6 ? feat[i] : Buf{attr[0], 1024};
@@ -614,12 +614,13 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
     h->attr_geom(k, C, H);
     attr[k - 1] = (mode == M_SWAP) ? c.alloc((size_t)B * H * H * C * es) : io.attr[k - 1];
   }
-  void* xin = c.alloc((size_t)B * 256 * 256 * 3 * es);
+  // network input NHWC with a zero fourth channel: 8-byte (bf16) pixels for the first conv
+  void* xin = c.alloc((size_t)B * 256 * 256 * 4 * es);
   if (!c.dry && c.ok()) {
     if (mode == M_SWAP)
-      c.check(crops_u8_to_input(io.crops, io.crop_bs, B, 256, 256, h->dt, xin, c.s), "crops_u8_to_input");
+      c.check(crops_u8_to_input(io.crops, io.crop_bs, B, 256, 256, h->dt, xin, c.s, 4), "crops_u8_to_input");
     else
-      c.check(input_to_nhwc(io.xt_dtype, io.xt, io.st, B, 3, 256, 256, h->dt, xin, c.s), "input_to_nhwc");
+      c.check(input_to_nhwc(io.xt_dtype, io.xt, io.st, B, 3, 256, 256, h->dt, xin, c.s, 4), "input_to_nhwc");
   }
   encoder(c, xin, B, attr);
   if (mode == M_ATTR) return;
@@ -930,7 +931,7 @@ extern "C" int ghost_nhwc_to_nchw(int dtype, const void* x, int ldx, int B, int 
 
 extern "C" int ghost_crops_to_input_nhwc(const uint8_t* crops, int64_t crop_batch_stride, int B, int H, int W, int dtype,
                                          void* y, void* stream) {
-  int rc = crops_u8_to_input(crops, crop_batch_stride, B, H, W, dtype, y, (hipStream_t)stream);
+  int rc = crops_u8_to_input(crops, crop_batch_stride, B, H, W, dtype, y, (hipStream_t)stream, 3);
   return rc ? fail(rc, "crops_to_input failed") : 0;
 }
 

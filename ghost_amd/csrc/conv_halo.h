@@ -11,4 +11,9 @@ namespace ghost {
 bool conv3x3_halo_supported(const ConvDesc& d);
 int conv3x3_halo(const ConvDesc& d, hipStream_t s);
 
+// ConvTranspose2d 4x4/s2/p1 on 8 x 16 input tiles (bf16, Cin % 32 == 0, N % 64 == 0 or N == 32,
+// H % 8 == 0, W % 16 == 0; weights as pack.py pack_convT4x4 lays them out)
+bool convT_halo_supported(const ConvDesc& d);
+int convT_halo(const ConvDesc& d, hipStream_t s);
+
 }  // namespace ghost

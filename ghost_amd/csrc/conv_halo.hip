@@ -192,6 +192,191 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
   }
 }
 
+// ---------------------------------------------------------------------------
+// ConvTranspose2d 4x4/s2/p1 (AEI_Net.py:27-41, the encoder's deconv layers) on the same plan:
+// a workgroup owns an 8 x 16 tile of INPUT pixels (= a 16 x 32 output tile: four sub-pixel
+// phases) and BN output channels.  Per block of 32 input channels it DMAs the 10 x 18 input
+// halo and the block's 16 (phase, tap) x BN weight rows; wave w computes phase w/2 for input
+// rows 4(w%2) .. +3 with its four 2x2 taps:
+//   out(2qy+py, 2qx+px)[n] += W[ky(py,ty)][kx(px,tx)][n][c] . x(qy+py-ty, qx+px-tx)[c]
+// ---------------------------------------------------------------------------
+template <int BN>
+struct HaloTCfg {
+  static constexpr int TIH = 8, TIW = 16;                   // input tile
+  static constexpr int HWW = TIW + 2, HP = (TIH + 2) * HWW; // 180 halo pixels
+  static constexpr int HPIECES = (HP + 15) / 16;            // 12
+  static constexpr int WPIECES = 16 * BN / 16;              // (phase, tap) x BN/16
+  static constexpr int HALO_B = HPIECES * 1024;
+  static constexpr int LDS_B = HALO_B + 16 * BN * 64;
+  static constexpr int NW = 8;
+  static constexpr int HPW = (HPIECES + NW - 1) / NW;
+  static constexpr int WPW = (WPIECES + NW - 1) / NW;
+  static constexpr int TN = BN / 16;                        // channel fragments per wave
+};
+
+struct HaloTArgs {
+  const bf16* x;
+  const bf16* w;      // [4][Npad][Kpad], K = (cb*4 + ty*2 + tx)*32 + c
+  bf16* y;
+  const float* scale;
+  const float* shift;
+  const bf16* res;
+  long wpar;          // Npad * Kpad
+  int H, W, Cin, ldx, N, Kpad, ldy, ldres;
+  float slope;
+  int tiles_x, tiles_y, nNt;
+};
+
+template <int BN>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) convT_halo_kernel(const HaloTArgs a) {
+  using G = HaloTCfg<BN>;
+  constexpr int HWW = G::HWW, HP = G::HP, HPIECES = G::HPIECES, WPIECES = G::WPIECES, HALO_B = G::HALO_B;
+  constexpr int NWAVES = G::NW, HPW = G::HPW, WPW = G::WPW, TN = G::TN;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[G::LDS_B];
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
+  const int ph = wid >> 1, py = ph >> 1, px = ph & 1, hf = wid & 1;
+  int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int nt = t % a.nNt;
+  t /= a.nNt;
+  const int tx = t % a.tiles_x;
+  t /= a.tiles_x;
+  const int ty = t % a.tiles_y;
+  const int b = t / a.tiles_y;
+  const int y0 = ty * G::TIH, x0 = tx * G::TIW, n0 = nt * BN;
+  const bf16* __restrict__ xs = a.x + (long)b * a.H * a.W * a.ldx;
+
+  const int prow = lane >> 2, slot = lane & 3;
+  int h_off[HPW];
+  unsigned h_ok = 0u;
+#pragma unroll
+  for (int j = 0; j < HPW; ++j) {
+    const int piece = wid + j * NWAVES;
+    const int P = piece * 16 + prow;
+    const int hy = P / HWW, hx = P - hy * HWW;
+    const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+    const bool ok = piece < HPIECES && P < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+    h_off[j] = ok ? (iy * a.W + ix) * a.ldx + ((slot ^ hswz(P)) * 8) : 0;
+    h_ok |= (ok ? 1u : 0u) << j;
+  }
+  const bf16* wsrc[WPW];
+#pragma unroll
+  for (int j = 0; j < WPW; ++j) {
+    const int piece = wid + j * NWAVES;               // = (phase*4 + tap) * BN/16 + row group
+    const int pt = piece / (BN / 16), n = (piece % (BN / 16)) * 16 + prow;
+    wsrc[j] = a.w + (pt >> 2) * a.wpar + (long)(n0 + n) * a.Kpad + (pt & 3) * 32 + ((slot ^ hswz(n)) * 8);
+  }
+
+  f32x4 acc[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ncb = a.Cin / 32;
+  for (int cb = 0; cb < ncb; ++cb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int j = 0; j < HPW; ++j) {
+      const int piece = wid + j * NWAVES;
+      if (piece < HPIECES) {
+        const void* src = ((h_ok >> j) & 1u) ? (const void*)(xs + h_off[j] + cb * 32) : (const void*)g_halo_zero;
+        __builtin_amdgcn_global_load_lds(src, lds + piece * 1024, 16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < WPW; ++j) {
+      const int piece = wid + j * NWAVES;
+      if (piece < WPIECES) __builtin_amdgcn_global_load_lds(wsrc[j] + cb * 128, lds + HALO_B + piece * 1024, 16, 0, 0);
+    }
+#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int tp = 0; tp < 4; ++tp) {
+      asm volatile("" ::: "memory");
+      const int dy = py - (tp >> 1), dx = px - (tp & 1);     // input offset of this tap
+      bf16x8 wf[TN], pf[4];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = j * 16 + lr;
+        wf[j] = *reinterpret_cast<const bf16x8*>(lds + HALO_B + ((ph * 4 + tp) * BN + n) * 64 + ((lq ^ hswz(n)) * 16));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int P = (hf * 4 + i + 1 + dy) * HWW + lr + 1 + dx;
+        pf[i] = *reinterpret_cast<const bf16x8*>(lds + P * 64 + ((lq ^ hswz(P)) * 16));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], pf[i], acc[j][i], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  const int Wo = 2 * a.W, Ho = 2 * a.H;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int oy = 2 * (y0 + hf * 4 + i) + py, ox = 2 * (x0 + lr) + px;
+    const long pix = ((long)b * Ho + oy) * Wo + ox;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + j * 16 + lq * 4;
+      if (n >= a.N) continue;
+      float rv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.res) {
+        const uint2 raw = *reinterpret_cast<const uint2*>(a.res + pix * a.ldres + n);
+        const bf16* e = reinterpret_cast<const bf16*>(&raw);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rv[r] = (float)e[r];
+      }
+      uint2 o;
+      bf16* oe = reinterpret_cast<bf16*>(&o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[j][i][r];
+        if (a.scale) v *= a.scale[n + r];
+        if (a.shift) v += a.shift[n + r];
+        v = v > 0.f ? v : v * a.slope;
+        oe[r] = (bf16)(v + rv[r]);
+      }
+      *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+    }
+  }
+}
+
+bool convT_halo_supported(const ConvDesc& d) {
+  static const int enabled = [] {
+    const char* e = getenv("GHOST_CONVT_HALO");
+    return e ? atoi(e) : 1;
+  }();
+  if (!enabled || d.kind != CONV_T4S2 || d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD) return false;
+  if (d.u8 || d.tanh_out || d.force_split || d.Cin % 32 || d.ldx % 8 || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
+  if (d.Hi % HaloTCfg<64>::TIH || d.Wi % HaloTCfg<64>::TIW || d.Kpad < 4 * d.Cin) return false;
+  if (!(d.N % 64 == 0 || d.N == 32) || d.Npad < d.N) return false;
+  if ((uintptr_t)d.x % 16 || (uintptr_t)d.w % 16 || (uintptr_t)d.y % 8 || (d.res && (uintptr_t)d.res % 8)) return false;
+  return (long)d.Hi * d.Wi * d.ldx < (1L << 31);
+}
+
+template <int BN>
+static int haloT_launch(const ConvDesc& d, hipStream_t s) {
+  HaloTArgs a{};
+  a.x = (const bf16*)d.x; a.w = (const bf16*)d.w; a.y = (bf16*)d.y;
+  a.scale = d.scale; a.shift = d.shift; a.res = (const bf16*)d.res;
+  a.wpar = (long)d.Npad * d.Kpad;
+  a.H = d.Hi; a.W = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx; a.N = d.N; a.Kpad = d.Kpad;
+  a.ldy = d.ldy; a.ldres = d.ldres; a.slope = d.slope;
+  a.tiles_x = d.Wi / HaloTCfg<BN>::TIW; a.tiles_y = d.Hi / HaloTCfg<BN>::TIH; a.nNt = (d.N + BN - 1) / BN;
+  const long ntiles = (long)d.B * a.tiles_x * a.tiles_y * a.nNt;
+  hipLaunchKernelGGL(convT_halo_kernel<BN>, dim3((unsigned)ntiles), dim3(512), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int convT_halo(const ConvDesc& d, hipStream_t s) {
+  if (!convT_halo_supported(d)) return -1;
+  return d.N == 32 ? haloT_launch<32>(d, s) : haloT_launch<64>(d, s);
+}
+
 bool conv3x3_halo_supported(const ConvDesc& d) {
   static const int enabled = [] {
     const char* e = getenv("GHOST_CONV_HALO");

@@ -12,6 +12,7 @@
 #include <cstdlib>
 
 #include "conv_igemm.h"
+#include "conv_first.h"
 #include "conv_halo.h"
 #include "ghost_common.h"
 
@@ -726,7 +727,8 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
 }  // namespace
 
 size_t conv_workspace_bytes(const ConvDesc& d) {
-  if (conv3x3_halo_supported(d)) return 0;
+  if (conv3x3_halo_supported(d) || convT_halo_supported(d)) return 0;
+  if (conv_first_supported(d)) return conv_first_workspace_bytes();
   Plan p = make_plan(d);
   if (p.nsplit <= 1) return 0;
   return (size_t)p.npar * p.nsplit * p.M * p.NT * sizeof(float);
@@ -738,6 +740,8 @@ int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream
   if (d.epi == EPI_AAD && (d.C_aad % 16 != 0 || d.N != 2 * d.C_aad || !d.hin || !d.stat || !d.idgb || !d.mask || !d.shift))
     return -1;
   if (conv3x3_halo_supported(d)) return conv3x3_halo(d, stream);
+  if (conv_first_supported(d)) return conv_first(d, ws, ws_bytes, stream);
+  if (convT_halo_supported(d)) return convT_halo(d, stream);
   Plan p = make_plan(d);
   if (p.NT > d.Npad) return -1;  // weight rows read by the last tile must exist
   const int K = d.kind == CONV_T4S2 ? 4 * d.Cin : d.kh * d.kw * d.Cin;

@@ -28,12 +28,14 @@ int aad_mask2(int dt, const void* h, int ldh, int B, int HW, int C, const float*
 int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C, hipStream_t s);
 
 // Xt [B,C,H,W] of dtype xdt with arbitrary element strides -> NHWC (ld = C) of dtype dt
+// ldy >= C: channel stride of y; channels C..ldy-1 are written as zero
 int input_to_nhwc(int xdt, const void* x, const int64_t strides[4], int B, int C, int H, int W, int dt, void* y,
-                  hipStream_t s);
+                  hipStream_t s, int ldy);
 
 // uint8 BGR NHWC crops -> RGB NHWC in [-1,1]: (v/255 - 0.5)/0.5  (core.py:13-26)
+// ldy = 3, or 4 with a zero fourth channel
 int crops_u8_to_input(const uint8_t* crops, int64_t batch_stride, int B, int H, int W, int dt, void* y,
-                      hipStream_t s);
+                      hipStream_t s, int ldy);
 
 // Y NHWC (3 channels, ld) -> uint8 BGR NHWC: ((Y*0.5+0.5)*255)[..., [2,1,0]].uint8  (faceshifter_run.py:20-21)
 int y_to_u8_bgr(int dt, const void* y, int ldy, int B, int H, int W, uint8_t* out, hipStream_t s);

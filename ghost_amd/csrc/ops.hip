@@ -272,45 +272,52 @@ int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, i
 // ---------------------------------------------------------------------------
 template <typename TX, typename T>
 __global__ void __launch_bounds__(256)
-input_to_nhwc_kernel(const TX* __restrict__ x, long sb, long sc, long sh, long sw, int B, int C, int H, int W, T* __restrict__ y) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  const long total = (long)B * C * H * W;
+input_to_nhwc_kernel(const TX* __restrict__ x, long sb, long sc, long sh, long sw, int B, int C, int H, int W, int ldy,
+                     T* __restrict__ y) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;   // one output element (channels >= C are zero)
+  const long total = (long)B * ldy * H * W;
   if (idx >= total) return;
-  const int c = (int)(idx % C);
-  const long pix = idx / C;
+  const int c = (int)(idx % ldy);
+  const long pix = idx / ldy;
   const int w = (int)(pix % W);
   const int h = (int)((pix / W) % H);
   const int b = (int)(pix / ((long)W * H));
-  y[idx] = from_f<T>(to_f(x[b * sb + c * sc + h * sh + w * sw]));
+  y[idx] = c < C ? from_f<T>(to_f(x[b * sb + c * sc + h * sh + w * sw])) : from_f<T>(0.f);
 }
 
 template <typename TX>
-static int input_dispatch(const TX* x, const int64_t* st, int B, int C, int H, int W, int dt, void* y, hipStream_t s) {
-  const long total = (long)B * C * H * W;
+static int input_dispatch(const TX* x, const int64_t* st, int B, int C, int H, int W, int dt, void* y, int ldy,
+                          hipStream_t s) {
+  const long total = (long)B * ldy * H * W;
   dim3 grid((unsigned)((total + 255) / 256));
   if (dt == GHOST_F32)
-    hipLaunchKernelGGL((input_to_nhwc_kernel<TX, float>), grid, dim3(256), 0, s, x, (long)st[0], (long)st[1], (long)st[2], (long)st[3], B, C, H, W, (float*)y);
+    hipLaunchKernelGGL((input_to_nhwc_kernel<TX, float>), grid, dim3(256), 0, s, x, (long)st[0], (long)st[1],
+                       (long)st[2], (long)st[3], B, C, H, W, ldy, (float*)y);
   else if (dt == GHOST_BF16)
-    hipLaunchKernelGGL((input_to_nhwc_kernel<TX, bf16>), grid, dim3(256), 0, s, x, (long)st[0], (long)st[1], (long)st[2], (long)st[3], B, C, H, W, (bf16*)y);
+    hipLaunchKernelGGL((input_to_nhwc_kernel<TX, bf16>), grid, dim3(256), 0, s, x, (long)st[0], (long)st[1],
+                       (long)st[2], (long)st[3], B, C, H, W, ldy, (bf16*)y);
   else
     return -1;
   return (int)hipGetLastError();
 }
 
 int input_to_nhwc(int xdt, const void* x, const int64_t strides[4], int B, int C, int H, int W, int dt, void* y,
-                  hipStream_t s) {
+                  hipStream_t s, int ldy) {
+  if (ldy < C) return -1;
   switch (xdt) {
-    case GHOST_F32: return input_dispatch((const float*)x, strides, B, C, H, W, dt, y, s);
-    case GHOST_BF16: return input_dispatch((const bf16*)x, strides, B, C, H, W, dt, y, s);
-    case GHOST_F16: return input_dispatch((const _Float16*)x, strides, B, C, H, W, dt, y, s);
-    case GHOST_U8: return input_dispatch((const uint8_t*)x, strides, B, C, H, W, dt, y, s);
+    case GHOST_F32: return input_dispatch((const float*)x, strides, B, C, H, W, dt, y, ldy, s);
+    case GHOST_BF16: return input_dispatch((const bf16*)x, strides, B, C, H, W, dt, y, ldy, s);
+    case GHOST_F16: return input_dispatch((const _Float16*)x, strides, B, C, H, W, dt, y, ldy, s);
+    case GHOST_U8: return input_dispatch((const uint8_t*)x, strides, B, C, H, W, dt, y, ldy, s);
   }
   return -1;
 }
 
+// ldy = 3: plain RGB; ldy = 4: RGB + a zero fourth channel (8-byte bf16 pixels: the layout the
+// encoder's first conv reads as aligned rows, conv_first.hip)
 template <typename T>
 __global__ void __launch_bounds__(256)
-crops_kernel(const uint8_t* __restrict__ crops, long bstride, int B, int H, int W, T* __restrict__ y) {
+crops_kernel(const uint8_t* __restrict__ crops, long bstride, int B, int H, int W, T* __restrict__ y, int ldy) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;   // one output pixel
   const long HW = (long)H * W;
   if (idx >= (long)B * HW) return;
@@ -321,17 +328,20 @@ crops_kernel(const uint8_t* __restrict__ crops, long bstride, int B, int H, int 
   for (int c = 0; c < 3; ++c) {
     float t = (float)src[2 - c] / 255.0f;   // BGR -> RGB, /255.
     t = (t - 0.5f) / 0.5f;
-    y[idx * 3 + c] = from_f<T>(t);
+    y[idx * ldy + c] = from_f<T>(t);
   }
+  if (ldy == 4) y[idx * 4 + 3] = from_f<T>(0.f);
 }
 
-int crops_u8_to_input(const uint8_t* crops, int64_t batch_stride, int B, int H, int W, int dt, void* y, hipStream_t s) {
+int crops_u8_to_input(const uint8_t* crops, int64_t batch_stride, int B, int H, int W, int dt, void* y, hipStream_t s,
+                      int ldy) {
+  if (ldy != 3 && ldy != 4) return -1;
   const long total = (long)B * H * W;
   dim3 grid((unsigned)((total + 255) / 256));
   if (dt == GHOST_F32)
-    hipLaunchKernelGGL(crops_kernel<float>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (float*)y);
+    hipLaunchKernelGGL(crops_kernel<float>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (float*)y, ldy);
   else if (dt == GHOST_BF16)
-    hipLaunchKernelGGL(crops_kernel<bf16>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (bf16*)y);
+    hipLaunchKernelGGL(crops_kernel<bf16>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (bf16*)y, ldy);
   else
     return -1;
   return (int)hipGetLastError();

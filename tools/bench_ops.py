@@ -62,6 +62,46 @@ def conv_cases(lib, iters, dt=torch.bfloat16):
         print(f"conv  {name:22s} {us:9.1f} us  {fl / us / 1e6:7.1f} TF/s  {by / us / 1e3:7.1f} GB/s(io)", flush=True)
 
 
+def enc_cases(lib, iters, dt=torch.bfloat16):
+    """Every encoder contraction of unet at B = 64: Conv4x4/s2 (conv1..7) and ConvT4x4/s2 (deconv1..6)."""
+    B = 64
+    ws = torch.empty(1 << 30, dtype=torch.uint8, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    down = [(3, 32), (32, 64), (64, 128), (128, 256), (256, 512), (512, 1024), (1024, 1024)]
+    H = 256
+    tot = 0.0
+    for i, (ci, co) in enumerate(down, 1):
+        ldx = 4 if ci == 3 else ci      # the runtime's network input has a zero fourth channel
+        x = torch.randn(B, H, H, ldx, device=DEV).to(dt)
+        w = pack_conv(torch.randn(co, ci, 4, 4, device=DEV) * 0.05, dt)
+        y = torch.empty(B, H // 2, H // 2, co, dtype=dt, device=DEV)
+
+        def run():
+            _lib.check(lib.ghost_conv2d_nhwc(_lib.gdtype(dt), x.data_ptr(), B, H, H, ci, ldx, w.data_ptr(), co,
+                                             w.shape[0], w.shape[1], 4, 4, 2, 1, None, None, 0.1, None, 0, 0,
+                                             y.data_ptr(), co, ws.data_ptr(), ws.numel(), st))
+        us = timeit(run, iters)
+        tot += us
+        fl = 2.0 * B * (H // 2) ** 2 * co * ci * 16
+        print(f"enc   conv{i} {ci:4d}->{co:4d} @{H // 2:3d} {us:9.1f} us  {fl / us / 1e6:7.1f} TF/s", flush=True)
+        H //= 2
+    up = [(1024, 1024, 2), (2048, 512, 4), (1024, 256, 8), (512, 128, 16), (256, 64, 32), (128, 32, 64)]
+    for i, (ci, co, H) in enumerate(up, 1):
+        x = torch.randn(B, H, H, ci, device=DEV).to(dt)
+        w = pack_convT4x4(torch.randn(ci, co, 4, 4, device=DEV) * 0.05, dt)
+        y = torch.empty(B, 2 * H, 2 * H, 2 * co, dtype=dt, device=DEV)
+
+        def run():
+            _lib.check(lib.ghost_conv_transpose4x4s2_nhwc(_lib.gdtype(dt), x.data_ptr(), B, H, H, ci, ci, w.data_ptr(),
+                                                          co, w.shape[1], w.shape[2], None, None, 0.1, None, 0,
+                                                          y.data_ptr(), 2 * co, ws.data_ptr(), ws.numel(), st))
+        us = timeit(run, iters)
+        tot += us
+        fl = 2.0 * B * (2 * H) ** 2 * co * ci * 4
+        print(f"enc   deconv{i} {ci:4d}->{co:4d} @{2 * H:3d} {us:9.1f} us  {fl / us / 1e6:7.1f} TF/s", flush=True)
+    print(f"enc   total {tot:9.1f} us", flush=True)
+
+
 def aad_cases(lib, iters, dt=torch.bfloat16):
     B = 64
     st = torch.cuda.current_stream().cuda_stream
@@ -184,6 +224,8 @@ def main():
         ceiling_cases(a.iters)
     if a.only in ("", "conv"):
         conv_cases(lib, a.iters)
+    if a.only in ("", "enc"):
+        enc_cases(lib, a.iters)
     if a.only in ("", "aad"):
         aad_cases(lib, a.iters)
     if a.only in ("", "aad", "aadv3"):
