@@ -1,4 +1,4 @@
-// ghost_amd — AADLayer kernel for the wide stages (bf16, C in {256, 512, 1024}, Ca <= 256):
+// ghost_amd — AADLayer kernel for the wide stages (bf16, C in {256, 512, 1024}, Ca <= 512):
 // one workgroup per (pixel block, 64-channel tile), weights in the pack_aad_v3 layout.
 #pragma once
 #include <hip/hip_runtime.h>

@@ -3,7 +3,7 @@
 // AADLayer.py:20-38 (+ the ReLU that follows it) as in aad_v3.hip (transposed MFMA whose
 // accumulators are gamma/beta of 16 channels of one pixel, register epilogue), but a
 // workgroup owns ONE 64-channel tile of a block of pixels: the tile's 128 permuted weight
-// rows (pack.py pack_aad_v3) fit LDS for any Ca <= 256, where all C/64 tiles would not.
+// rows (pack.py pack_aad_v3) fit LDS for any Ca <= 512, where all C/64 tiles would not.
 // The mask needs every channel of the pixel: it comes from one aad_mask pass over h_in
 // (ops.hip), so a 16-pixel tile here is one round trip: z_attr row, the tile's 64 channels of
 // h_in and the mask.  The C/64 workgroups of one pixel block are adjacent in launch order (and
@@ -39,7 +39,7 @@ GHOST_DEV int wide_xcd_tile(int bid, int nwg) {
 }
 
 template <int C, int CA>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_wide_kernel(const AadWideArgs a) {
+GHOST_DEV void aad_wide_body(const AadWideArgs& a) {
   constexpr int CT = C / 64;
   constexpr int KS = CA / 32;
   constexpr int WLD = CA + 8;
@@ -77,9 +77,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     asm volatile("" ::: "memory");
     const long p = p_begin + t * 16 + lr;
     const bf16* hrow = a.hin + p * a.ldh + ct * 64;
-    // one round trip: the z_attr row (Ca <= 256; deeper rows would stream inside the GEMM), this
-    // tile's two h_in chunks and the mask
-    constexpr bool ZEARLY = KS <= 8;
+    // one round trip: the z_attr row, this tile's two h_in chunks and the mask
+    constexpr bool ZEARLY = true;   // the whole z_attr row is in flight with the h_in chunks
     u32x4 zc[ZEARLY ? KS : 1];
     if constexpr (ZEARLY) {
 #pragma unroll
@@ -141,10 +140,23 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
 }
 
+// Ca <= 256: 4 waves per SIMD (<= 128 VGPRs), two workgroups per CU.  Ca = 512: the 133 KB of
+// weight rows allow one workgroup per CU, so the z_attr row (64 VGPRs) may use the registers.
+template <int C, int CA>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_wide_kernel(const AadWideArgs a) {
+  aad_wide_body<C, CA>(a);
+}
+template <int C, int CA>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 8))) aad_wide_deep_kernel(const AadWideArgs a) {
+  aad_wide_body<C, CA>(a);
+}
+
 namespace {
-int wide_ppw(int B, int HW, int C) {
-  // as many pixels per workgroup as keep >= 512 workgroups (two per CU): the 128 weight rows
-  // staged per workgroup are then amortised over as many 16-pixel tiles as possible
+int wide_ppw(int B, int HW, int C, int Ca) {
+  // as many pixels per workgroup as keep a full round of workgroups (two per CU; one for the
+  // 133 KB Ca = 512 rows): the weight rows staged per workgroup are then amortised over as
+  // many 16-pixel tiles as possible
+  const long minwg = Ca > 256 ? 256 : 512;
   static const int force = [] {
     const char* e = getenv("GHOST_AAD_WIDE_PPW");
     return e ? atoi(e) : 0;
@@ -152,16 +164,16 @@ int wide_ppw(int B, int HW, int C) {
   if (force > 0 && HW % force == 0 && force % 16 == 0) return force;
   int best = 0;
   for (int ppw = 16; ppw <= HW && ppw <= 4096; ppw *= 2)
-    if (HW % ppw == 0 && (best == 0 || (long)B * HW / ppw * (C / 64) >= 512)) best = ppw;
+    if (HW % ppw == 0 && (best == 0 || (long)B * HW / ppw * (C / 64) >= minwg)) best = ppw;
   return best;
 }
 }  // namespace
 
 bool aad_wide_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo) {
   if (dt != GHOST_BF16) return false;
-  const bool shape = (C == 256 || C == 512 || C == 1024) && (Ca == 64 || Ca == 128 || Ca == 256);
+  const bool shape = (C == 256 || C == 512 || C == 1024) && (Ca == 64 || Ca == 128 || Ca == 256 || Ca == 512);
   if (!shape || lda % 8 || ldh % 8 || ldo % 8) return false;
-  const int ppw = wide_ppw(B, HW, C);
+  const int ppw = wide_ppw(B, HW, C, Ca);
   return ppw > 0 && (long)B * HW / ppw * (C / 64) >= 256;
 }
 
@@ -171,7 +183,7 @@ int aad_wide(const AadWideDesc& d, hipStream_t s) {
   a.za = (const bf16*)d.za; a.hin = (const bf16*)d.hin; a.stat = d.stat;
   a.w3 = (const bf16*)d.w3; a.b3 = d.b3; a.wh = d.wh; a.bh = d.bh; a.idgb = d.idgb; a.mask = d.mask; a.out = (bf16*)d.out;
   a.lda = d.lda; a.ldh = d.ldh; a.ldo = d.ldo; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
-  a.PPW = wide_ppw(d.B, d.HW, d.C);
+  a.PPW = wide_ppw(d.B, d.HW, d.C, d.Ca);
   a.nblk = (int)((long)d.B * d.HW / a.PPW);
   dim3 grid((unsigned)(a.nblk * (d.C / 64)));
 #define GHOST_W(c, ca)                                                                 \
@@ -182,6 +194,13 @@ int aad_wide(const AadWideDesc& d, hipStream_t s) {
   GHOST_W(256, 64) GHOST_W(256, 128) GHOST_W(256, 256) GHOST_W(512, 64) GHOST_W(512, 128) GHOST_W(512, 256)
   GHOST_W(1024, 64) GHOST_W(1024, 128) GHOST_W(1024, 256)
 #undef GHOST_W
+#define GHOST_WD(c, ca)                                                                     \
+  if (d.C == c && d.Ca == ca) {                                                             \
+    hipLaunchKernelGGL((aad_wide_deep_kernel<c, ca>), grid, dim3(kWideWaves * 64), 0, s, a); \
+    return (int)hipGetLastError();                                                          \
+  }
+  GHOST_WD(512, 512) GHOST_WD(1024, 512)
+#undef GHOST_WD
   return -1;
 }
 

@@ -574,9 +574,9 @@ void declare_slots(ghost_aei* h) {
     int Ca_k, n_k;
     h->attr_geom(k, Ca_k, n_k);
     // permuted register-epilogue AAD layouts (pack.py pack_aad_v3): aad_v3 for C in {64, 128},
-    // aad_wide for C in {256, 512, 1024} with Ca <= 256
+    // aad_wide for C in {256, 512, 1024} with Ca <= 512
     const bool v3 = h->dt == GHOST_BF16 && (cin == 64 || cin == 128 ||
-                                            ((cin == 256 || cin == 512 || cin == 1024) && Ca_k <= 256));
+                                            ((cin == 256 || cin == 512 || cin == 1024) && Ca_k <= 512));
     for (int i = 0; i < h->nb; ++i) {
       const std::string an = blk + ".aad" + std::to_string(i);
       add(an + ".gbw"); add(an + ".gbb"); add(an + ".wh"); add(an + ".bh");
@@ -952,9 +952,9 @@ extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, con
   const int HW = H * W;
   if (L < 1 || L > 2) return fail(GHOST_EINVAL, "aad_v3: L must be 1 or 2");
   if (up2x && (H % 2 || W % 2 || C != 64)) return fail(GHOST_EINVAL, "aad_v3: up2x needs even H, W and C = 64");
-  const bool wide = C >= 256;   // aad_wide: one layer, C in {256, 512, 1024}, Ca <= 256
+  const bool wide = C >= 256;   // aad_wide: one layer, C in {256, 512, 1024}, Ca <= 512
   if (wide && (L != 1 || up2x || !aad_wide_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[0])))
-    return fail(GHOST_EINVAL, "aad_wide: unsupported shape (one layer, C in {256,512,1024}, Ca <= 256)");
+    return fail(GHOST_EINVAL, "aad_wide: unsupported shape (one layer, C in {256,512,1024}, Ca <= 512)");
   for (int l = 0; l < L && !wide; ++l)
     if (!aad_v3_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[l]))
       return fail(GHOST_EINVAL, "aad_v3: unsupported shape (bf16, C in {64,128}, enough pixels)");

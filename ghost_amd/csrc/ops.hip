@@ -173,28 +173,40 @@ aad_mask_kernel(const T* __restrict__ h, int ldh, int HW, int C, int G, int ppb,
   const int per = 256 / G, gl = t % G;
   const long base = (long)b * HW;
   const int pend = min(HW, (blockIdx.x + 1) * ppb);
-  // the G lanes of a pixel share q (and the trip count), so the in-group shuffles stay converged
-  for (int q = blockIdx.x * ppb + t / G; q < pend; q += per) {
-    float s0 = 0.f, s1 = 0.f;
-    {
-      const T* hp = h + (base + q) * ldh;
-      for (int ci = gl; ci < C / VEC; ci += G) {
-        float v[VEC];
-        load16_f(hp + ci * VEC, v);
+  // the G lanes of a pixel share q (and the trip count), so the in-group shuffles stay converged;
+  // four pixels per lane group are in flight at once (their loads issued before any FMA)
+  constexpr int U = 4;
+  for (int q0 = blockIdx.x * ppb + t / G; q0 < pend; q0 += U * per) {
+    float s0[U], s1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) { s0[u] = 0.f; s1[u] = 0.f; }
+    for (int ci = gl; ci < C / VEC; ci += G) {
+      float v[U][VEC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + u * per;
+        if (q < pend) load16_f(h + (base + q) * ldh + ci * VEC, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
           const int c = ci * VEC + e;
-          const float d = v[e] - s_mu[c];
-          s0 = fmaf(s_tab[c], d, s0);
-          if (L == 2) s1 = fmaf(s_tab[C + c], d, s1);
+          const float d = v[u][e] - s_mu[c];
+          s0[u] = fmaf(s_tab[c], d, s0[u]);
+          if (L == 2) s1[u] = fmaf(s_tab[C + c], d, s1[u]);
         }
       }
     }
-    s0 = group_sum(s0, G);
-    if (L == 2) s1 = group_sum(s1, G);
-    if (gl == 0) {
-      mask0[base + q] = sigmoidf_ref(s0 + bh0[0]);
-      if (L == 2) mask1[base + q] = sigmoidf_ref(s1 + bh1[0]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + u * per;
+      const float a0 = group_sum(s0[u], G);
+      const float a1 = L == 2 ? group_sum(s1[u], G) : 0.f;
+      if (gl == 0 && q < pend) {
+        mask0[base + q] = sigmoidf_ref(a0 + bh0[0]);
+        if (L == 2) mask1[base + q] = sigmoidf_ref(a1 + bh1[0]);
+      }
     }
   }
 }

@@ -139,8 +139,8 @@ def pack_aad_v3(sd, prefix: str, dtype) -> Dict[str, torch.Tensor]:
 
 def v3_layout(c: int, ca: int) -> bool:
     """AADLayers packed for the register-epilogue kernels too: aad_v3 (C in {64, 128}) and
-    aad_wide (C in {256, 512, 1024}, Ca <= 256); mirrors aei_runtime.hip declare_slots."""
-    return c in (64, 128) or (c in (256, 512, 1024) and ca <= 256)
+    aad_wide (C in {256, 512, 1024}, Ca <= 512); mirrors aei_runtime.hip declare_slots."""
+    return c in (64, 128) or (c in (256, 512, 1024) and ca <= 512)
 
 
 def aad_plan(backbone: str, num_blocks: int) -> List[Tuple[str, str]]:

@@ -431,7 +431,8 @@ def test_conv3x3_narrow_op(lib, dt, cin, cout, H, W, use_res):
                                               (64, 64, 256, 2, 2, 1), (64, 32, 128, 4, 2, 1), (64, 64, 64, 8, 1, 1),
                                               # aad_wide: one 64-channel tile per workgroup
                                               (256, 128, 64, 8, 1, 0), (512, 256, 32, 8, 1, 0),
-                                              (1024, 256, 16, 16, 1, 0), (512, 64, 32, 4, 1, 0)])
+                                              (1024, 256, 16, 16, 1, 0), (512, 64, 32, 4, 1, 0),
+                                              (1024, 512, 16, 8, 1, 0)])
 def test_aad_layers_v3_vs_oracle(lib, c_x, c_a, n, B, L, up):
     """Register-epilogue AAD kernel (1 or 2 layers sharing h_in / z_attr) against the oracle AADLayer;
     up = 1: h_in is read through the bilinear x2 upsample of an n/2 source (AEI_Net.py:137)."""
