@@ -23,8 +23,10 @@ def test_oracle_forward_matches_reference(name):
     p = aei_ref.make_weights(aei_ref.param_specs(backbone, nb))
     xt, z = aei_ref.make_inputs(B, int(g["seed"]))
     y, attr = aei_ref.aei_forward(p, xt, z, backbone, nb)
-    # same ATen ops on the same CPU: agreement far below the 1e-3 product gate
-    assert float((y - torch.from_numpy(g["Y"])).abs().max()) < 1e-5
+    # same ATen ops, but oneDNN picks different conv algorithms on different host CPUs
+    # (observed 5.7e-5 unet/2 and 4.3e-4 linknet/3 on an Intel host vs the AMD host that wrote
+    # the fixtures): gate at half the 1e-3 product gate
+    assert float((y - torch.from_numpy(g["Y"])).abs().max()) < 5e-4
     for i, a in enumerate(attr, 1):
         assert tuple(a.shape) == tuple(g[f"attr{i}_shape"])
         flat = a.reshape(-1).double()
@@ -40,7 +42,7 @@ def test_oracle_u8_pipeline_matches_reference(name):
     _, z = aei_ref.make_inputs(B, int(g["seed"]))
     target = aei_ref.transform_target(aei_ref.make_u8_crops(B, int(g["crops_seed"])))
     y, _ = aei_ref.aei_forward(p, target, torch.cat([z[:1]] * B), backbone, nb)
-    assert float((y - torch.from_numpy(g["Ypipe"])).abs().max()) < 1e-5
+    assert float((y - torch.from_numpy(g["Ypipe"])).abs().max()) < 5e-4
     u8 = aei_ref.y_to_u8_bgr(y)
     diff = np.abs(u8.astype(np.int16) - g["U8"].astype(np.int16))
     assert diff.max() <= 1 and (diff > 0).mean() < 1e-3
