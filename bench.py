@@ -183,8 +183,15 @@ def main():
                                          "mask, MFMA gamma/beta, blend, ReLU)",
                                "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kname),
+                               "bytes_note": "achieved counts SURVEY.md 8d bytes (|h_in|+|z_attr|+|out| per AADLayer, "
+                                             "h_in at 256x256); the kernel physically moves the 128x128 h_in once "
+                                             "for both layers: see physical_gbs / traffic",
                                "bytes_per_launch": per_launch_bytes, "avg_launch_us": round(per_launch_s * 1e6, 2),
                                "launches_timed": c["launches"]}
+            tr = res["roofline"]["traffic"]
+            if tr:
+                res["roofline"]["physical_gbs"] = round(tr["bytes_per_launch"] / per_launch_s / 1e9, 1)
+                res["roofline"]["physical_frac"] = round(res["roofline"]["physical_gbs"] / HBM_PEAK_GBS, 4)
             cc = classes["conv3x3_all"]
             if cc["launches"]:
                 tf = cc["flops"] / (cc["ms"] / 1e3) / 1e12
