@@ -45,6 +45,8 @@ _SIGS = {
                                      C.POINTER(C.c_double)]),
     "ghost_conv2d_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
                                 f32, vp, i32, i32, vp, i32, vp, i64, vp]),
+    "ghost_conv2d_ex_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
+                                   i32, vp, i64, vp]),
     "ghost_conv_transpose4x4s2_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, vp, vp, f32, vp,
                                              i32, vp, i32, vp, i64, vp]),
     "ghost_linear_f32": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, i32, vp, i64, vp]),
@@ -62,6 +64,12 @@ _SIGS = {
     "ghost_conv3x3_narrow_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, vp, i32, i32, vp, i32, vp,
                                         vp]),
 }
+
+
+class ConvEpi(C.Structure):
+    """struct ghost_conv_epi (include/ghost_amd.h)."""
+    _fields_ = [("scale", vp), ("shift", vp), ("slope", f32), ("prelu", vp), ("res", vp), ("ldres", i32),
+                ("res_first", i32), ("tanh_out", i32), ("y2", vp), ("ldy2", i32), ("scale2", vp), ("shift2", vp)]
 
 
 def header_symbols():

@@ -58,6 +58,7 @@ struct ProfClass {
 
 struct ghost_aei {
   bool linknet = false;
+  bool resnet = false;   // backbone='resnet': MLAttrEncoderResnet (resnet.py:81-149) + the unet generator
   int nb = 2, c_id = 512, dt = GHOST_F32, esz = 4;
   std::map<std::string, const void*> slots;   // name -> device pointer (nullptr = unbound)
   int id_total = 0;                            // sum over AAD layers of 2*c_x
@@ -224,8 +225,69 @@ struct Buf {
   int ld;
 };
 
+// one Conv2d + BatchNorm(eval) (+ ReLU) of the resnet encoder; NHWC in/out with channel strides
+void res_conv(Ctx& c, const std::string& name, const void* x, int ldx, int B, int H, int Cin, int Cout, int k,
+              int stride, void* y, int ldy, bool relu, const void* res = nullptr, int ldres = 0) {
+  ghost_aei* h = c.h;
+  ConvDesc d;
+  d.ti = d.to = h->dt;
+  d.x = x; d.B = B; d.Hi = H; d.Wi = H; d.Cin = Cin; d.ldx = ldx;
+  d.w = c.W(name + ".w");
+  d.N = Cout; d.Npad = rup(Cout, 128); d.Kpad = rup(k * k * Cin, 32);
+  d.kind = CONV_FWD; d.kh = d.kw = k; d.stride = stride; d.pad = k / 2;
+  d.y = y; d.ldy = ldy;
+  d.scale = (const float*)c.W(name + ".scale");
+  d.shift = (const float*)c.W(name + ".shift");
+  d.slope = relu ? 0.f : 1.f;
+  if (res) { d.res = res; d.ldres = ldres; d.res_first = 1; }
+  const double Ho = (H + 2 * (k / 2) - k) / stride + 1;
+  run_conv(c, d, 5, -1, 2.0 * B * Ho * Ho * Cout * k * k * Cin);
+}
+
+// MLAttrEncoderResnet = ResNet(Bottleneck, [2]*6) (resnet.py:81-149): returns
+// (x7, x6, x5, x4, x3, x2, x1, x0) = z_attr1..8, the same geometry as the unet encoder
+void encoder_resnet(Ctx& c, const void* xin, int B, void* const attr[8]) {
+  ghost_aei* h = c.h;
+  const int es = h->esz;
+  // x0 = relu(bn0(conv0 7x7/s1/p3)) -> z_attr8;  x1 = relu(bn1(conv1 7x7/s2/p3)) -> z_attr7
+  res_conv(c, "enc.r.conv0", xin, 4, B, 256, 3, 64, 7, 1, attr[7], 64, true);
+  res_conv(c, "enc.r.conv1", attr[7], 64, B, 256, 64, 64, 7, 2, attr[6], 64, true);
+  static const int planes_of[6] = {32, 64, 128, 256, 512, 256};
+  const void* x = attr[6];
+  int C = 64, H = 128;
+  for (int li = 1; li <= 6; ++li) {
+    const int pl = planes_of[li - 1], co = 4 * pl;
+    for (int blk = 0; blk < 2; ++blk) {
+      const int stride = blk == 0 ? 2 : 1;
+      const int Ho = H / stride;
+      const std::string pre = "enc.r.l" + std::to_string(li) + ".b" + std::to_string(blk);
+      void* t1 = c.alloc((size_t)B * Ho * Ho * pl * es);
+      void* t2 = c.alloc((size_t)B * Ho * Ho * pl * es);
+      // Bottleneck.forward (resnet.py:57-78): conv1 1x1/s carries the stride
+      res_conv(c, pre + ".c1", x, C, B, H, C, pl, 1, stride, t1, pl, true);
+      res_conv(c, pre + ".c2", t1, pl, B, Ho, pl, pl, 3, 1, t2, pl, true);
+      const void* res = x;
+      if (blk == 0) {
+        void* r = c.alloc((size_t)B * Ho * Ho * co * es);
+        res_conv(c, pre + ".down", x, C, B, H, C, co, 1, stride, r, co, false);
+        res = r;
+      }
+      void* out = blk == 1 ? attr[6 - li] : c.alloc((size_t)B * Ho * Ho * co * es);
+      // relu(bn3(conv3(t2)) + residual)
+      res_conv(c, pre + ".c3", t2, pl, B, Ho, pl, co, 1, 1, out, co, true, res, co);
+      x = out;
+      C = co;
+      H = Ho;
+    }
+  }
+}
+
 void encoder(Ctx& c, const void* xin, int B, void* const attr[8]) {
   ghost_aei* h = c.h;
+  if (h->resnet) {
+    encoder_resnet(c, xin, B, attr);
+    return;
+  }
   const int es = h->esz;
   // where feat_1..feat_6 live: unet -> inside z_attr_{8-j} after the deconv channels
   Buf feat[7];
@@ -556,12 +618,23 @@ int check_handle(ghost_aei* h) {
 
 void declare_slots(ghost_aei* h) {
   auto add = [&](const std::string& s) { h->slots[s] = nullptr; };
-  for (int i = 1; i <= 7; ++i) {
+  auto add_conv = [&](const std::string& s) { add(s + ".w"); add(s + ".scale"); add(s + ".shift"); };
+  if (h->resnet) {
+    add_conv("enc.r.conv0");
+    add_conv("enc.r.conv1");
+    for (int li = 1; li <= 6; ++li)
+      for (int blk = 0; blk < 2; ++blk) {
+        const std::string pre = "enc.r.l" + std::to_string(li) + ".b" + std::to_string(blk);
+        add_conv(pre + ".c1"); add_conv(pre + ".c2"); add_conv(pre + ".c3");
+        if (blk == 0) add_conv(pre + ".down");
+      }
+  }
+  for (int i = 1; i <= 7 && !h->resnet; ++i) {
     add("enc.conv" + std::to_string(i) + ".w");
     add("enc.conv" + std::to_string(i) + ".scale");
     add("enc.conv" + std::to_string(i) + ".shift");
   }
-  for (int i = 1; i <= 6; ++i) {
+  for (int i = 1; i <= 6 && !h->resnet; ++i) {
     add("enc.deconv" + std::to_string(i) + ".w");
     add("enc.deconv" + std::to_string(i) + ".scale");
     add("enc.deconv" + std::to_string(i) + ".shift");
@@ -673,12 +746,14 @@ int run(ghost_aei* h, Mode mode, int B, const Io& io, void* ws, int64_t ws_bytes
 extern "C" int ghost_aei_create(const char* backbone, int num_blocks, int c_id, int dtype, ghost_aei** out) {
   if (!out || !backbone) return fail(GHOST_EINVAL, "null argument");
   std::string bb(backbone);
-  if (bb != "unet" && bb != "linknet") return fail(GHOST_EINVAL, "backbone must be 'unet' or 'linknet' (got " + bb + ")");
+  if (bb != "unet" && bb != "linknet" && bb != "resnet")
+    return fail(GHOST_EINVAL, "backbone must be 'unet', 'linknet' or 'resnet' (got " + bb + ")");
   if (num_blocks < 1 || num_blocks > 8) return fail(GHOST_EINVAL, "num_blocks out of range");
   if (c_id <= 0 || c_id % 32) return fail(GHOST_EINVAL, "c_id must be a positive multiple of 32");
   if (dtype != GHOST_F32 && dtype != GHOST_BF16) return fail(GHOST_EINVAL, "dtype must be f32 or bf16");
   ghost_aei* h = new ghost_aei();
   h->linknet = bb == "linknet";
+  h->resnet = bb == "resnet";
   h->nb = num_blocks;
   h->c_id = c_id;
   h->dt = dtype;
@@ -845,6 +920,23 @@ extern "C" int ghost_conv2d_nhwc(int dtype, const void* x, int B, int H, int W, 
   d.scale = scale; d.shift = shift; d.slope = slope; d.res = res; d.ldres = ldres; d.tanh_out = tanh_out;
   d.y = y; d.ldy = ldy;
   return conv_op(d, ws, ws_bytes, stream, "ghost_conv2d_nhwc");
+}
+
+extern "C" int ghost_conv2d_ex_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx,
+                                    const void* w_packed, int Cout, int Npad, int Kpad, int kh, int kw, int stride,
+                                    int pad, const ghost_conv_epi* epi, void* y, int ldy, void* ws, int64_t ws_bytes,
+                                    void* stream) {
+  if (!epi) return fail(GHOST_EINVAL, "ghost_conv2d_ex_nhwc: null epilogue");
+  ConvDesc d;
+  d.ti = d.to = dtype;
+  d.x = x; d.B = B; d.Hi = H; d.Wi = W; d.Cin = Cin; d.ldx = ldx;
+  d.w = w_packed; d.N = Cout; d.Npad = Npad; d.Kpad = Kpad;
+  d.kind = CONV_FWD; d.kh = kh; d.kw = kw; d.stride = stride; d.pad = pad;
+  d.scale = epi->scale; d.shift = epi->shift; d.slope = epi->slope; d.prelu = epi->prelu;
+  d.res = epi->res; d.ldres = epi->ldres; d.res_first = epi->res_first; d.tanh_out = epi->tanh_out;
+  d.y2 = epi->y2; d.ldy2 = epi->ldy2; d.scale2 = epi->scale2; d.shift2 = epi->shift2;
+  d.y = y; d.ldy = ldy;
+  return conv_op(d, ws, ws_bytes, stream, "ghost_conv2d_ex_nhwc");
 }
 
 extern "C" int ghost_conv_transpose4x4s2_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx,

@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(256) first_weights_kernel(const T* __restrict_
 
 bool conv_first_supported(const ConvDesc& d) {
   return d.kind == CONV_FWD && d.kh == 4 && d.kw == 4 && d.stride == 2 && d.pad == 1 && d.Cin == 3 &&
-         d.N == 32 && d.ti == d.to && (d.ti == GHOST_BF16 || d.ti == GHOST_F32) && d.epi == EPI_STD && !d.res &&
+         d.N == 32 && d.ti == d.to && (d.ti == GHOST_BF16 || d.ti == GHOST_F32) && d.epi == EPI_STD && !d.res && !d.prelu && !d.y2 &&
          !d.tanh_out && !d.u8 && d.ldy % (d.to == GHOST_F32 ? 4 : 8) == 0 && (uintptr_t)d.y % 16 == 0 &&
          d.Kpad >= 48 && !d.force_split;
 }

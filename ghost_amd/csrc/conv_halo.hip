@@ -352,6 +352,7 @@ bool convT_halo_supported(const ConvDesc& d) {
   }();
   if (!enabled || d.kind != CONV_T4S2 || d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD) return false;
   if (d.u8 || d.tanh_out || d.force_split || d.Cin % 32 || d.ldx % 8 || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
+  if (d.res_first || d.prelu || d.y2) return false;   // epilogue variants only the implicit GEMM has
   if (d.Hi % HaloTCfg<64>::TIH || d.Wi % HaloTCfg<64>::TIW || d.Kpad < 4 * d.Cin) return false;
   if (!(d.N % 64 == 0 || d.N == 32) || d.Npad < d.N) return false;
   if ((uintptr_t)d.x % 16 || (uintptr_t)d.w % 16 || (uintptr_t)d.y % 8 || (d.res && (uintptr_t)d.res % 8)) return false;
@@ -384,6 +385,7 @@ bool conv3x3_halo_supported(const ConvDesc& d) {
   }();
   if (!enabled || d.kind != CONV_FWD || d.kh != 3 || d.kw != 3 || d.stride != 1 || d.pad != 1) return false;
   if (d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD || d.u8 || d.force_split) return false;
+  if (d.res_first || d.prelu || d.y2) return false;   // epilogue variants only the implicit GEMM has
   if (d.Cin % 32 || d.ldx % 8 || d.N % 64 || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
   const bool wide = d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0;
   const bool small = d.Wi == HaloSmall::TW && d.Hi % HaloSmall::TH == 0;

@@ -31,12 +31,20 @@ struct ConvDesc {
   void* y = nullptr;
   int ldy = 0;
   // standard epilogue: v = acc*scale[n] + shift[n]; v = v>0 ? v : v*slope; v += res; tanh
+  // (res_first moves the residual before the activation)
   const float* scale = nullptr;
   const float* shift = nullptr;
   float slope = 1.0f;
   const void* res = nullptr;         // same dtype as the output
   int ldres = 0;
   int tanh_out = 0;
+  int res_first = 0;                 // 1: v = act(acc*scale + shift + res)  (ResNet Bottleneck, resnet.py:74-76)
+  const float* prelu = nullptr;      // per-channel negative slope (nn.PReLU), overrides `slope`
+  // optional second output y2 = v*scale2 + shift2 (the BatchNorm that opens the next IBasicBlock)
+  void* y2 = nullptr;
+  int ldy2 = 0;
+  const float* scale2 = nullptr;
+  const float* shift2 = nullptr;
   uint8_t* u8 = nullptr;             // optional BGR uint8 NHWC copy of a 3-channel output (faceshifter_run.py:20-21)
   // AAD epilogue (epi == EPI_AAD): output channel c pairs weight columns (gamma, beta)
   int epi = EPI_STD;

@@ -25,6 +25,10 @@ struct ConvArgs {
   const float* scale;
   const float* shift;
   const void* res;
+  const float* prelu;
+  void* y2;
+  const float* scale2;
+  const float* shift2;
   const void* hin;
   const float* stat;
   const float* idgb;
@@ -36,7 +40,7 @@ struct ConvArgs {
   int Ho, Wo, M;        // GEMM pixel grid (the sub-pixel grid for CONV_T4S2)
   int N, Kpad, K, NT;   // NT = padded channel extent covered by tiles
   int nNt;              // number of channel tiles
-  int ldy, ldres, ldh, id_ld, C_aad;
+  int ldy, ldres, ldh, id_ld, C_aad, ldy2, res_first;
   int stride, ntx, ntaps, tbase, tsign;   // input coord = out*stride + tbase + tsign*tap  (per dim)
   int deconv;           // 1: four parity phases in blockIdx.z, output pixel (2qy+py, 2qx+px)
   int nsplit, kt_per_split;
@@ -51,8 +55,11 @@ template <typename TO>
 GHOST_DEV float epi_std(const ConvArgs& a, float v, int n, long opix) {
   if (a.scale) v *= a.scale[n];
   if (a.shift) v += a.shift[n];
-  v = v > 0.f ? v : v * a.slope;
-  if (a.res) v += to_f(reinterpret_cast<const TO*>(a.res)[opix * a.ldres + n]);
+  const float r = a.res ? to_f(reinterpret_cast<const TO*>(a.res)[opix * a.ldres + n]) : 0.f;
+  if (a.res_first) v += r;
+  const float sl = a.prelu ? a.prelu[n] : a.slope;
+  v = v > 0.f ? v : v * sl;
+  if (!a.res_first) v += r;
   if (a.tanh_out) v = tanhf(v);
   return v;
 }
@@ -60,6 +67,7 @@ GHOST_DEV float epi_std(const ConvArgs& a, float v, int n, long opix) {
 template <typename TO>
 GHOST_DEV void store_std(const ConvArgs& a, float v, int n, long opix) {
   reinterpret_cast<TO*>(a.y)[opix * a.ldy + n] = from_f<TO>(v);
+  if (a.y2) reinterpret_cast<TO*>(a.y2)[opix * a.ldy2 + n] = from_f<TO>(v * a.scale2[n] + a.shift2[n]);
   if (a.u8) {
     // ((Y*0.5+0.5)*255)[..., [2,1,0]].type(uint8)   (faceshifter_run.py:20-21)
     float t = (v * 0.5f + 0.5f) * 255.0f;
@@ -154,25 +162,25 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
   const int tbx = a.deconv ? px : a.tbase;
   const int nty = a.K / (a.Cin * a.ntx);
   long a_off[AP];
-  unsigned a_mask[AP];
+  uint64_t a_mask[AP];   // one bit per tap: kernels up to 8x8 (7x7 = 49 taps)
 #pragma unroll
   for (int p = 0; p < AP; ++p) {
     const int m = m0 + crow + p * RPP;
     a_off[p] = 0;
-    a_mask[p] = 0u;
+    a_mask[p] = 0ull;
     if (m < a.M) {
       const int b = m / HoWo;
       const int r = m - b * HoWo;
       const int oy = r / a.Wo, ox = r - oy * a.Wo;
       const int iyb = oy * a.stride + tby, ixb = ox * a.stride + tbx;
       a_off[p] = ((long)(b * a.Hi + iyb) * a.Wi + ixb) * a.ldx;
-      unsigned mk = 0u;
+      uint64_t mk = 0ull;
       for (int ty = 0; ty < nty; ++ty) {
         const int iy = iyb + a.tsign * ty;
         if (iy < 0 || iy >= a.Hi) continue;
         for (int tx = 0; tx < a.ntx; ++tx) {
           const int ix = ixb + a.tsign * tx;
-          if (ix >= 0 && ix < a.Wi) mk |= 1u << (ty * a.ntx + tx);
+          if (ix >= 0 && ix < a.Wi) mk |= 1ull << (ty * a.ntx + tx);
         }
       }
       a_mask[p] = mk;
@@ -200,7 +208,7 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
       const long toff = ((long)a.tsign * ty * a.Wi + a.tsign * tx) * a.ldx + cb * 32 + ((cch * VEC) & 31);
 #pragma unroll
       for (int p = 0; p < AP; ++p) {
-        if ((a_mask[p] >> tap) & 1u)
+        if ((a_mask[p] >> tap) & 1ull)
           ra[p] = *reinterpret_cast<const u32x4*>(x + a_off[p] + toff);
         else
           ra[p] = u32x4{0u, 0u, 0u, 0u};
@@ -217,7 +225,7 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
             const int tap = k / a.Cin;
             const int c = k - tap * a.Cin;
             const int ty = tap / a.ntx, tx = tap - ty * a.ntx;
-            if ((a_mask[p] >> tap) & 1u)
+            if ((a_mask[p] >> tap) & 1ull)
               v = to_f(x[a_off[p] + ((long)a.tsign * ty * a.Wi + a.tsign * tx) * a.ldx + c]);
           }
           e[j] = from_f<TI>(v);
@@ -380,7 +388,7 @@ GHOST_DEV void wait_vmcnt() {
 // issue the LDS-DMA of K tile `kt` into ring slot `sb` (one 16-row piece per instruction)
 template <int BM, int NA, int NB>
 GHOST_DEV void glds_issue(const ConvArgs& a, const bf16* __restrict__ x, const bf16* const (&b_src)[NB],
-                          const long (&a_off)[NA], const unsigned (&a_mask)[NA], const int (&a_gc)[NA], int wid,
+                          const long (&a_off)[NA], const uint64_t (&a_mask)[NA], const int (&a_gc)[NA], int wid,
                           int kt, unsigned char* sb) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the amdgcn builtin does not exist in the host pass of this TU
   const int k0 = kt * 32;
@@ -389,7 +397,7 @@ GHOST_DEV void glds_issue(const ConvArgs& a, const bf16* __restrict__ x, const b
   const long toff = ((long)a.tsign * ty * a.Wi + a.tsign * tx) * a.ldx + cb * 32;
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
-    const void* src = ((a_mask[j] >> tap) & 1u) ? (const void*)(x + a_off[j] + toff + a_gc[j])
+    const void* src = ((a_mask[j] >> tap) & 1ull) ? (const void*)(x + a_off[j] + toff + a_gc[j])
                                                  : (const void*)g_zero_line;
     __builtin_amdgcn_global_load_lds(src, sb + (wid * NA + j) * 1024, 16, 0, 0);
   }
@@ -429,7 +437,7 @@ __global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
   const int tby = a.deconv ? py : a.tbase, tbx = a.deconv ? px : a.tbase;
   const int nty = a.K / (a.Cin * a.ntx);
   long a_off[NA];
-  unsigned a_mask[NA];
+  uint64_t a_mask[NA];
   int a_gc[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
@@ -437,20 +445,20 @@ __global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
     const int m = m0 + r;
     a_gc[j] = swz(r, pc) * 8;
     a_off[j] = 0;
-    a_mask[j] = 0u;
+    a_mask[j] = 0ull;
     if (m < a.M) {
       const int b = m / HoWo;
       const int rr = m - b * HoWo;
       const int oy = rr / a.Wo, ox = rr - oy * a.Wo;
       const int iyb = oy * a.stride + tby, ixb = ox * a.stride + tbx;
       a_off[j] = ((long)(b * a.Hi + iyb) * a.Wi + ixb) * a.ldx;
-      unsigned mk = 0u;
+      uint64_t mk = 0ull;
       for (int ty = 0; ty < nty; ++ty) {
         const int iy = iyb + a.tsign * ty;
         if (iy < 0 || iy >= a.Hi) continue;
         for (int tx = 0; tx < a.ntx; ++tx) {
           const int ix = ixb + a.tsign * tx;
-          if (ix >= 0 && ix < a.Wi) mk |= 1u << (ty * a.ntx + tx);
+          if (ix >= 0 && ix < a.Wi) mk |= 1ull << (ty * a.ntx + tx);
         }
       }
       a_mask[j] = mk;
@@ -612,6 +620,8 @@ ConvArgs make_args(const ConvDesc& d, const Plan& p, float* partial) {
   ConvArgs a{};
   a.x = d.x; a.w = d.w; a.y = d.y;
   a.scale = d.scale; a.shift = d.shift; a.res = d.res;
+  a.prelu = d.prelu; a.y2 = d.y2; a.scale2 = d.scale2; a.shift2 = d.shift2; a.ldy2 = d.ldy2;
+  a.res_first = d.res_first;
   a.hin = d.hin; a.stat = d.stat; a.idgb = d.idgb; a.mask = d.mask;
   a.partial = partial; a.u8 = d.u8;
   a.wpar_stride = (long)d.Npad * d.Kpad;
@@ -737,6 +747,8 @@ size_t conv_workspace_bytes(const ConvDesc& d) {
 int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream) {
   if (!d.x || !d.w || !d.y || d.B <= 0 || d.Cin <= 0 || d.N <= 0) return -1;
   if (d.Kpad % 32 != 0 || d.Npad < d.N) return -1;
+  if (d.y2 && (!d.scale2 || !d.shift2 || d.epi != EPI_STD)) return -1;
+  if (d.kind == CONV_FWD && (d.kh * d.kw > 64 || d.kh < 1 || d.kw < 1 || d.stride < 1)) return -1;   // 64-bit tap masks
   if (d.epi == EPI_AAD && (d.C_aad % 16 != 0 || d.N != 2 * d.C_aad || !d.hin || !d.stat || !d.idgb || !d.mask || !d.shift))
     return -1;
   if (conv3x3_halo_supported(d)) return conv3x3_halo(d, stream);

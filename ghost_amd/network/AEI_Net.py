@@ -29,6 +29,7 @@ import torch.nn as nn
 from .. import _lib
 from .AADLayer import AAD_ResBlk, AADLayer, AddBlocksSequential  # noqa: F401  (reference re-exports)
 from .pack import pack_all
+from .resnet import MLAttrEncoderResnet
 
 
 def weight_init(m):
@@ -165,7 +166,7 @@ class AEI_Net(nn.Module):
         if backbone in ['unet', 'linknet']:
             self.encoder = MLAttrEncoder(backbone)
         elif backbone == 'resnet':
-            raise NotImplementedError("ghost_amd: backbone='resnet' has no MI355X path yet (SURVEY.md §8f row 4)")
+            self.encoder = MLAttrEncoderResnet()
         else:
             raise ValueError(f"unknown backbone {backbone!r}")
         self.generator = AADGenerator(backbone, c_id, num_blocks)

@@ -38,6 +38,9 @@ GEN_BLOCKS = {
 }
 
 
+GEN_BLOCKS["resnet"] = GEN_BLOCKS["unet"]   # AEI_Net.py:111-118: only linknet changes the generator
+
+
 def rup(v: int, m: int) -> int:
     return (v + m - 1) // m * m
 
@@ -154,17 +157,43 @@ def aad_plan(backbone: str, num_blocks: int) -> List[Tuple[str, str]]:
     return out
 
 
+RESNET_PLANES = [32, 64, 128, 256, 512, 256]   # resnet.py:93-98 (Bottleneck expansion 4)
+
+
+def pack_resnet_encoder(sd, dtype) -> Dict[str, torch.Tensor]:
+    """MLAttrEncoderResnet (resnet.py:81-149): every conv + its eval BatchNorm as scale/shift."""
+    slots: Dict[str, torch.Tensor] = {}
+
+    def conv_bn(slot, wkey, bnkey):
+        w = sd[wkey]
+        slots[f"{slot}.w"] = pack_conv(w, dtype)
+        slots[f"{slot}.scale"], slots[f"{slot}.shift"] = bn_fold(sd, bnkey, rup(w.shape[0], 128))
+
+    conv_bn("enc.r.conv0", "encoder.conv0.weight", "encoder.bn0")
+    conv_bn("enc.r.conv1", "encoder.conv1.weight", "encoder.bn1")
+    for li in range(1, 7):
+        for blk in range(2):
+            pre, slot = f"encoder.layer{li}.{blk}", f"enc.r.l{li}.b{blk}"
+            for j in (1, 2, 3):
+                conv_bn(f"{slot}.c{j}", f"{pre}.conv{j}.weight", f"{pre}.bn{j}")
+            if blk == 0:
+                conv_bn(f"{slot}.down", f"{pre}.downsample.0.weight", f"{pre}.downsample.1")
+    return slots
+
+
 def pack_all(sd: Dict[str, torch.Tensor], backbone: str, num_blocks: int, c_id: int,
              dtype: torch.dtype) -> Dict[str, torch.Tensor]:
     """Every runtime slot -> a contiguous device tensor."""
     if backbone not in GEN_BLOCKS:
         raise NotImplementedError(f"ghost_amd: backbone {backbone!r} has no MI355X path yet")
     slots: Dict[str, torch.Tensor] = {}
-    for i, (_ci, co) in enumerate(ENC_DOWN, 1):
+    if backbone == "resnet":
+        slots.update(pack_resnet_encoder(sd, dtype))
+    for i, (_ci, co) in enumerate(ENC_DOWN if backbone != "resnet" else [], 1):
         slots[f"enc.conv{i}.w"] = pack_conv(sd[f"encoder.conv{i}.0.weight"], dtype)
         s, t = bn_fold(sd, f"encoder.conv{i}.1", rup(co, 128))
         slots[f"enc.conv{i}.scale"], slots[f"enc.conv{i}.shift"] = s, t
-    for i, (_ci, co) in enumerate(ENC_UP[backbone], 1):
+    for i, (_ci, co) in enumerate(ENC_UP.get(backbone, []), 1):
         slots[f"enc.deconv{i}.w"] = pack_convT4x4(sd[f"encoder.deconv{i}.deconv.weight"], dtype)
         s, t = bn_fold(sd, f"encoder.deconv{i}.bn", rup(co, 128))
         slots[f"enc.deconv{i}.scale"], slots[f"enc.deconv{i}.shift"] = s, t

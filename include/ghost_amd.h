@@ -45,7 +45,7 @@ const char* ghost_version(void);
 const char* ghost_last_error(void);
 
 /* ---- whole-network handle (one per device) ---------------------------------------- */
-/* backbone: "unet" | "linknet"; dtype: compute/storage dtype of activations and
+/* backbone: "unet" | "linknet" | "resnet" (MLAttrEncoderResnet, network/resnet.py:147-149); dtype: compute/storage dtype of activations and
  * conv weights (GHOST_DTYPE_F32 = parity path, GHOST_DTYPE_BF16 = throughput path). */
 int ghost_aei_create(const char* backbone, int num_blocks, int c_id, int dtype, ghost_aei** out);
 void ghost_aei_destroy(ghost_aei* h);
@@ -92,6 +92,29 @@ int ghost_conv2d_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, in
                       int Npad, int Kpad, int kh, int kw, int stride, int pad, const float* scale, const float* shift,
                       float slope, const void* res, int ldres, int tanh_out, void* y, int ldy, void* ws,
                       int64_t ws_bytes, void* stream);
+/* Epilogue of ghost_conv2d_ex_nhwc, applied per output (pixel, channel n):
+ *   v = acc*scale[n] + shift[n];  if res_first: v += res;  v = v > 0 ? v : v*(prelu ? prelu[n] : slope);
+ *   if !res_first: v += res;  if tanh_out: v = tanh(v);  y = v;  if y2: y2 = v*scale2[n] + shift2[n]
+ * Covers Conv+BN+LeakyReLU (AEI_Net.py:19-24), the ResNet Bottleneck tail relu(bn3(conv3) + residual)
+ * (network/resnet.py:72-78), and the ArcFace IBasicBlock (conv + BN + PReLU; BN of the next block's
+ * input written as the second output).  Pointers may be NULL (scale/shift default 1/0). */
+typedef struct ghost_conv_epi {
+  const float* scale;
+  const float* shift;
+  float slope;
+  const float* prelu;
+  const void* res;
+  int ldres;
+  int res_first;
+  int tanh_out;
+  void* y2;
+  int ldy2;
+  const float* scale2;
+  const float* shift2;
+} ghost_conv_epi;
+int ghost_conv2d_ex_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx, const void* w_packed,
+                         int Cout, int Npad, int Kpad, int kh, int kw, int stride, int pad, const ghost_conv_epi* epi,
+                         void* y, int ldy, void* ws, int64_t ws_bytes, void* stream);
 /* Conv2d 3x3/p1 to Cout <= 3 channels (the generator's RGB output): halo-tiled per-tap partial
  * sums; w_narrow [32][Kpad], row (ky*3+kx)*Cout + o; optional residual, tanh and BGR uint8 copy. */
 int ghost_conv3x3_narrow_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx, const void* w_narrow,

@@ -11,6 +11,7 @@ It is a from-scratch restatement, written with ``torch.nn.functional`` ops on CP
 * ``conv4x4``            -> /root/reference/network/AEI_Net.py:19-24
 * ``deconv4x4``          -> /root/reference/network/AEI_Net.py:27-41
 * ``MLAttrEncoder``      -> /root/reference/network/AEI_Net.py:44-95
+* ``MLAttrEncoderResnet`` (backbone='resnet') -> /root/reference/network/resnet.py:43-149
 * ``AADGenerator``       -> /root/reference/network/AEI_Net.py:98-139
 * ``AEI_Net``            -> /root/reference/network/AEI_Net.py:143-159
 * ``AADLayer.forward``   -> /root/reference/network/AADLayer.py:20-38
@@ -52,9 +53,26 @@ ENC_UP = {
 GEN_BLOCKS = {
     "unet": [(1024, 1024, 1024), (1024, 1024, 2048), (1024, 1024, 1024), (1024, 512, 512),
              (512, 256, 256), (256, 128, 128), (128, 64, 64), (64, 3, 64)],
+    # AEI_Net.py:111-118: every backbone but linknet takes the unet channel plan
+    "resnet": [(1024, 1024, 1024), (1024, 1024, 2048), (1024, 1024, 1024), (1024, 512, 512),
+               (512, 256, 256), (256, 128, 128), (128, 64, 64), (64, 3, 64)],
     "linknet": [(1024, 1024, 1024), (1024, 1024, 1024), (1024, 1024, 512), (1024, 512, 256),
                 (512, 256, 128), (256, 128, 64), (128, 64, 32), (64, 3, 32)],
 }
+
+
+RESNET_PLANES = [32, 64, 128, 256, 512, 256]   # resnet.py:93-98, Bottleneck expansion 4
+
+
+def resnet_blocks():
+    """(layer, inplanes, planes, stride, block index) of MLAttrEncoderResnet (resnet.py:101-116, 147-149):
+    two Bottlenecks per layer; the first has stride 2 (on its 1x1 conv1) and a 1x1/s2 + BN downsample."""
+    out, inplanes = [], 64
+    for li, planes in enumerate(RESNET_PLANES, 1):
+        for blk in range(2):
+            out.append((li, inplanes, planes, 2 if blk == 0 else 1, blk))
+            inplanes = 4 * planes
+    return out
 
 
 def param_specs(backbone: str = "unet", num_blocks: int = 2, c_id: int = 512) -> List[Tuple[str, Tuple[int, ...], str]]:
@@ -71,12 +89,30 @@ def param_specs(backbone: str = "unet", num_blocks: int = 2, c_id: int = 512) ->
                       (f"{prefix}.running_mean", (c,), "bn_rm"), (f"{prefix}.running_var", (c,), "bn_rv"),
                       (f"{prefix}.num_batches_tracked", (), "bn_nbt")])
 
-    for i, (ci, co) in enumerate(ENC_DOWN, 1):
-        specs.append((f"encoder.conv{i}.0.weight", (co, ci, 4, 4), "conv"))
-        bn(f"encoder.conv{i}.1", co)
-    for i, (ci, co) in enumerate(ENC_UP[backbone], 1):
-        specs.append((f"encoder.deconv{i}.deconv.weight", (ci, co, 4, 4), "convT"))
-        bn(f"encoder.deconv{i}.bn", co)
+    if backbone == "resnet":
+        # ResNet(Bottleneck, [2]*6) (resnet.py:81-149): stem conv0 7x7/s1, conv1 7x7/s2, six layers
+        specs.append(("encoder.conv0.weight", (64, 3, 7, 7), "conv"))
+        bn("encoder.bn0", 64)
+        specs.append(("encoder.conv1.weight", (64, 64, 7, 7), "conv"))
+        bn("encoder.bn1", 64)
+        for li, cin, planes, stride, blk in resnet_blocks():
+            pre = f"encoder.layer{li}.{blk}"
+            specs.append((f"{pre}.conv1.weight", (planes, cin, 1, 1), "conv"))
+            bn(f"{pre}.bn1", planes)
+            specs.append((f"{pre}.conv2.weight", (planes, planes, 3, 3), "conv"))
+            bn(f"{pre}.bn2", planes)
+            specs.append((f"{pre}.conv3.weight", (4 * planes, planes, 1, 1), "conv"))
+            bn(f"{pre}.bn3", 4 * planes)
+            if blk == 0:
+                specs.append((f"{pre}.downsample.0.weight", (4 * planes, cin, 1, 1), "conv"))
+                bn(f"{pre}.downsample.1", 4 * planes)
+    else:
+        for i, (ci, co) in enumerate(ENC_DOWN, 1):
+            specs.append((f"encoder.conv{i}.0.weight", (co, ci, 4, 4), "conv"))
+            bn(f"encoder.conv{i}.1", co)
+        for i, (ci, co) in enumerate(ENC_UP[backbone], 1):
+            specs.append((f"encoder.deconv{i}.deconv.weight", (ci, co, 4, 4), "convT"))
+            bn(f"encoder.deconv{i}.bn", co)
     specs.append(("generator.up1.weight", (c_id, 1024, 2, 2), "convT"))
     specs.append(("generator.up1.bias", (1024,), "bias"))
 
@@ -169,8 +205,35 @@ def up2x(x):
     return F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=True)
 
 
+def _bottleneck(x, p, pre, stride, has_down):
+    """Bottleneck.forward (resnet.py:57-78): 1x1/s -> BN -> ReLU -> 3x3 -> BN -> ReLU -> 1x1 -> BN, + residual, ReLU."""
+    out = F.relu(_bn_eval(F.conv2d(x, p[f"{pre}.conv1.weight"].to(x.dtype), None, stride=stride), p, f"{pre}.bn1"))
+    out = F.relu(_bn_eval(F.conv2d(out, p[f"{pre}.conv2.weight"].to(x.dtype), None, padding=1), p, f"{pre}.bn2"))
+    out = _bn_eval(F.conv2d(out, p[f"{pre}.conv3.weight"].to(x.dtype), None), p, f"{pre}.bn3")
+    res = x
+    if has_down:
+        res = _bn_eval(F.conv2d(x, p[f"{pre}.downsample.0.weight"].to(x.dtype), None, stride=stride), p,
+                       f"{pre}.downsample.1")
+    return F.relu(out + res)
+
+
+def encoder_resnet(xt, p):
+    """ResNet.forward (resnet.py:122-144) -> (x7, x6, x5, x4, x3, x2, x1, x0)."""
+    x0 = F.relu(_bn_eval(F.conv2d(xt, p["encoder.conv0.weight"].to(xt.dtype), None, padding=3), p, "encoder.bn0"))
+    x = F.relu(_bn_eval(F.conv2d(x0, p["encoder.conv1.weight"].to(xt.dtype), None, stride=2, padding=3), p,
+                        "encoder.bn1"))
+    feats = [x0, x]
+    for li, _cin, _planes, stride, blk in resnet_blocks():
+        x = _bottleneck(x, p, f"encoder.layer{li}.{blk}", stride, blk == 0)
+        if blk == 1:
+            feats.append(x)
+    return tuple(reversed(feats))
+
+
 def encoder(xt, p, backbone="unet"):
     """MLAttrEncoder.forward (AEI_Net.py:72-95) -> 8-tuple z_attr1..z_attr8."""
+    if backbone == "resnet":
+        return encoder_resnet(xt, p)
     feats = []
     x = xt
     for i in range(1, 8):

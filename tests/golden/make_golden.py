@@ -119,11 +119,18 @@ def main():
     sys.dont_write_bytecode = True
     sys.path.insert(0, REF)
     torch.set_num_threads(os.cpu_count() or 8)
-    forward_case("aei_unet2_b2", "unet", 2, 2, pipeline=True)
-    forward_case("aei_linknet3_b2", "linknet", 3, 2, pipeline=True)
-    forward_case("aei_unet1_b1", "unet", 1, 1)
-    forward_case("aei_unet3_b1", "unet", 3, 1)
-    aad_cases()
+    jobs = {
+        "aei_unet2_b2": lambda: forward_case("aei_unet2_b2", "unet", 2, 2, pipeline=True),
+        "aei_linknet3_b2": lambda: forward_case("aei_linknet3_b2", "linknet", 3, 2, pipeline=True),
+        "aei_unet1_b1": lambda: forward_case("aei_unet1_b1", "unet", 1, 1),
+        "aei_unet3_b1": lambda: forward_case("aei_unet3_b1", "unet", 3, 1),
+        "aei_resnet2_b1": lambda: forward_case("aei_resnet2_b1", "resnet", 2, 1),
+        "aad_layer_cases": aad_cases,
+    }
+    only = [a for a in sys.argv[1:] if not a.startswith("-")]   # regenerate a subset by name
+    for name, job in jobs.items():
+        if not only or name in only:
+            job()
 
 
 if __name__ == "__main__":

@@ -104,6 +104,83 @@ def test_conv2d_op(lib, dt, cin, cout, k, s, p, H):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin,ldx,cout,k,s,p,H,mode", [
+    (3, 4, 64, 7, 1, 3, 32, "relu"),          # resnet encoder conv0 on the 4-channel input layout
+    (64, 64, 64, 7, 2, 3, 32, "relu"),        # resnet encoder conv1 7x7/s2
+    (64, 64, 32, 1, 2, 0, 16, "relu"),        # Bottleneck conv1 1x1/s2
+    (128, 128, 512, 1, 2, 0, 16, "none"),     # downsample 1x1/s2 + BN
+    (32, 32, 128, 1, 1, 0, 16, "res_relu"),   # Bottleneck tail relu(bn3(conv3) + residual)
+    (64, 64, 64, 3, 1, 1, 28, "prelu_y2"),    # IBasicBlock conv + BN + PReLU, with a BN'd second output
+    (64, 64, 128, 3, 2, 1, 28, "res_y2"),     # IBasicBlock conv2/s2 + BN + residual, second output = next BN
+])
+def test_conv2d_ex_epilogues(lib, dt, cin, ldx, cout, k, s, p, H, mode):
+    """ghost_conv2d_ex_nhwc: residual-before-activation, per-channel PReLU and the dual output."""
+    from ghost_amd import _lib
+    from ghost_amd.network.pack import pack_conv, rup
+    g = torch.Generator().manual_seed(cin * 13 + cout + k)
+    B = 2
+    x = torch.randn(B, cin, H, H, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    sc, sh = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g) * 0.1
+    pr = torch.rand(cout, generator=g) * 0.5
+    sc2, sh2 = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g) * 0.1
+    Ho = (H + 2 * p - k) // s + 1
+    res = torch.randn(B, cout, Ho, Ho, generator=g)
+    xr, wr, rr = x.to(dt).float(), w.to(dt).float(), res.to(dt).float()
+    v = F.conv2d(xr, wr, stride=s, padding=p) * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)
+    if mode == "relu":
+        ref = F.relu(v)
+    elif mode == "none":
+        ref = v
+    elif mode == "res_relu":
+        ref = F.relu(v + rr)
+    elif mode == "prelu_y2":
+        ref = F.prelu(v, pr)
+    else:
+        ref = v + rr
+    ref2 = ref * sc2.view(1, -1, 1, 1) + sh2.view(1, -1, 1, 1)
+    xin = torch.zeros(B, H, H, ldx)
+    xin[..., :cin] = nhwc(x)
+    if ldx > cin:
+        xin[..., cin:] = 7.0          # padding channels must not contribute
+    xd = xin.to(dt).to(DEV)
+    wp = pack_conv(w, dt).to(DEV)
+
+    def padv(t):
+        o = torch.zeros(rup(cout, 128), device=DEV)
+        o[:cout] = t.to(DEV)
+        return o
+    scp, shp, prp, sc2p, sh2p = padv(sc), padv(sh), padv(pr), padv(sc2), padv(sh2)
+    rd = nhwc(res).to(dt).to(DEV)
+    y = torch.empty(B, Ho, Ho, cout, dtype=dt, device=DEV)
+    y2 = torch.empty(B, Ho, Ho, cout, dtype=dt, device=DEV)
+    e = _lib.ConvEpi()
+    e.scale, e.shift = scp.data_ptr(), shp.data_ptr()
+    e.slope = 0.0 if mode in ("relu", "res_relu") else 1.0
+    if mode == "prelu_y2":
+        e.prelu = prp.data_ptr()
+    if mode in ("res_relu", "res_y2"):
+        e.res, e.ldres, e.res_first = rd.data_ptr(), cout, 1
+    if mode.endswith("y2"):
+        e.y2, e.ldy2, e.scale2, e.shift2 = y2.data_ptr(), cout, sc2p.data_ptr(), sh2p.data_ptr()
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=DEV)
+    _lib.check(lib.ghost_conv2d_ex_nhwc(_lib.gdtype(dt), xd.data_ptr(), B, H, H, cin, ldx, wp.data_ptr(), cout,
+                                        wp.shape[0], wp.shape[1], k, k, s, p, C_byref(e), y.data_ptr(), cout,
+                                        ws.data_ptr(), ws.numel(), stream(lib)))
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    assert float((got - ref).abs().max()) <= tol * max(1.0, float(ref.abs().max()))
+    if mode.endswith("y2"):
+        got2 = y2.float().cpu().permute(0, 3, 1, 2)
+        assert float((got2 - ref2).abs().max()) <= tol * max(1.0, float(ref2.abs().max()))
+
+
+def C_byref(x):
+    import ctypes
+    return ctypes.byref(x)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_first_conv_padded_input(lib, dt):
     """Encoder conv1 (3 -> 32, 4x4/s2) on the runtime's 4-channel input layout (channel 3 is padding
     and must not contribute: filled with finite junk here); bf16 runs the MFMA kernel."""
@@ -250,7 +327,8 @@ def test_aad_layer_module_vs_reference_golden(lib):
 # ----------------------------------------------------------------------------------------
 # whole network
 # ----------------------------------------------------------------------------------------
-@pytest.mark.parametrize("name", ["aei_unet2_b2", "aei_linknet3_b2", "aei_unet1_b1", "aei_unet3_b1"])
+@pytest.mark.parametrize("name", ["aei_unet2_b2", "aei_linknet3_b2", "aei_unet1_b1", "aei_unet3_b1",
+                                  "aei_resnet2_b1"])
 def test_forward_fp32_matches_reference(lib, name):
     g = gold(name)
     backbone, nb, B = str(g["backbone"]), int(g["num_blocks"]), int(g["batch"])
@@ -303,6 +381,19 @@ def test_forward_bf16_close_to_oracle(lib):
     Y, attr = G(xt.to(DEV), z.to(DEV))
     assert Y.dtype == torch.bfloat16
     bf16_gate(Y.float().cpu(), torch.from_numpy(g["Y"]))
+
+
+def test_resnet_backbone_bf16_batch(lib):
+    """backbone='resnet' (MLAttrEncoderResnet) on the bf16 path at B=8 against the fp32 oracle."""
+    G = model("resnet", 2, compute_dtype=torch.bfloat16)
+    xt, z = aei_ref.make_inputs(8, 21)
+    Y, attr = G(xt.to(DEV), z.to(DEV))
+    y_ref, a_ref = aei_ref.aei_forward(weights("resnet", 2), xt, z, "resnet", 2)
+    bf16_gate(Y.float().cpu(), y_ref)
+    for a, r in zip(attr, a_ref):
+        assert a.shape == r.shape
+        rel = float((a.float().cpu() - r).abs().mean()) / max(1e-6, float(r.abs().mean()))
+        assert rel < 0.05, rel
 
 
 @pytest.mark.parametrize("backbone,nb", [("unet", 2), ("linknet", 3)])

@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol(lib):
     assert set(declared) == set(_lib._SIGS), "ctypes signature table out of sync with include/ghost_amd.h"
 
 
-@pytest.mark.parametrize("backbone,nb", [("unet", 2), ("linknet", 3), ("unet", 1), ("unet", 3)])
+@pytest.mark.parametrize("backbone,nb", [("unet", 2), ("linknet", 3), ("unet", 1), ("unet", 3), ("resnet", 2)])
 def test_pack_slots_match_runtime_plan(lib, backbone, nb):
     specs = aei_ref.param_specs(backbone, nb)
     sd = aei_ref.make_weights(specs)
@@ -55,9 +55,17 @@ def test_pack_slots_match_runtime_plan(lib, backbone, nb):
         lib.ghost_aei_destroy(h)
 
 
+def test_resnet_module_state_dict_matches_oracle_specs():
+    """AEI_Net('resnet') exposes the reference's 497 state_dict keys (resnet.py:81-149 names)."""
+    from ghost_amd.network import AEI_Net
+    sd = AEI_Net("resnet", num_blocks=2, c_id=512).state_dict()
+    specs = aei_ref.param_specs("resnet", 2)
+    assert [(k, tuple(v.shape)) for k, v in sd.items()] == [(k, tuple(s)) for k, s, _ in specs]
+
+
 def test_create_rejects_bad_arguments(lib):
     h = C.c_void_p()
-    assert lib.ghost_aei_create(b"resnet", 2, 512, 0, C.byref(h)) != 0
+    assert lib.ghost_aei_create(b"vgg", 2, 512, 0, C.byref(h)) != 0
     assert b"backbone" in lib.ghost_last_error()
     assert lib.ghost_aei_create(b"unet", 0, 512, 0, C.byref(h)) != 0
     assert lib.ghost_aei_create(b"unet", 2, 512, 7, C.byref(h)) != 0

@@ -9,7 +9,7 @@ import torch
 from oracle import aei_ref
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-CASES = ["aei_unet2_b2", "aei_linknet3_b2", "aei_unet1_b1", "aei_unet3_b1"]
+CASES = ["aei_unet2_b2", "aei_linknet3_b2", "aei_unet1_b1", "aei_unet3_b1", "aei_resnet2_b1"]
 
 
 def _load(name):
