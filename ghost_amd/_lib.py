@@ -45,6 +45,14 @@ _SIGS = {
                                      C.POINTER(C.c_double)]),
     "ghost_conv2d_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
                                 f32, vp, i32, i32, vp, i32, vp, i64, vp]),
+    "ghost_arc_create": (i32, [C.POINTER(i32), i32, i32, C.POINTER(vp)]),
+    "ghost_arc_destroy": (None, [vp]),
+    "ghost_arc_bind": (i32, [vp, C.c_char_p, vp, i64]),
+    "ghost_arc_missing": (i32, [vp]),
+    "ghost_arc_workspace_bytes": (i64, [vp, i32]),
+    "ghost_arc_forward": (i32, [vp, vp, i32, i64p, i32, vp, vp, i64, vp]),
+    "ghost_arc_embed_u8": (i32, [vp, vp, i64, i32, i32, i32, vp, vp, i64, vp]),
+    "ghost_arc_match": (i32, [vp, i32, vp, i32, i32, f32, vp, vp, vp, vp]),
     "ghost_conv2d_ex_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
                                    i32, vp, i64, vp]),
     "ghost_conv_transpose4x4s2_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, vp, vp, f32, vp,

@@ -30,6 +30,10 @@ static int fail(int rc, const std::string& msg) {
   g_err = msg;
   return rc == 0 ? GHOST_EINVAL : rc;
 }
+namespace ghost {
+// shared with the other runtimes of the library (arc_runtime.hip): one ghost_last_error() per thread
+int set_last_error(int rc, const std::string& msg) { return fail(rc, msg); }
+}  // namespace ghost
 
 extern "C" const char* ghost_version(void) { return "ghost_amd 0.1 (gfx950)"; }
 extern "C" const char* ghost_last_error(void) { return g_err.c_str(); }

@@ -549,6 +549,7 @@ namespace {
 struct Plan {
   int BM, BN, BK, nNt, nMt, npar, nsplit, kt_per_split, NT, M, Ho, Wo;
   bool fast;
+  bool partial;   // GEMM writes fp32 partials, splitk_reduce_kernel applies the epilogue
 };
 
 int env_int(const char* name, int dflt) {
@@ -613,6 +614,9 @@ Plan make_plan(const ConvDesc& d) {
   if (s > nk) s = nk;
   p.kt_per_split = (nk + s - 1) / s;
   p.nsplit = (nk + p.kt_per_split - 1) / p.kt_per_split;
+  // bf16 operands with an fp32 output (the ArcFace embedding layer): the GEMM always writes fp32
+  // partials and the reduction kernel applies the epilogue in fp32
+  p.partial = p.nsplit > 1 || (d.ti == GHOST_BF16 && d.to == GHOST_F32);
   return p;
 }
 
@@ -700,10 +704,21 @@ bool launch_glds(const ConvArgs& a, const Plan& p, hipStream_t s) {
 template <typename TI, typename TO>
 int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStream_t s) {
   int rc;
+  if constexpr (sizeof(TI) == 2 && sizeof(TO) == 4) {
+    // bf16 GEMM, fp32 epilogue: the partial-sum GEMM does not depend on the output type, so it
+    // shares the bf16 instantiations; the reduction writes fp32
+    if (!p.partial || d.epi != EPI_STD) return -1;
+    rc = p.fast ? dispatch_tile<TI, TI, KEPI_SPLIT, true>(a, p, s) : dispatch_tile<TI, TI, KEPI_SPLIT, false>(a, p, s);
+    if (rc) return rc;
+    const long total = (long)p.M * d.N;
+    dim3 grid((unsigned)((total + 255) / 256), 1, p.npar);
+    hipLaunchKernelGGL((splitk_reduce_kernel<float, KEPI_STD>), grid, dim3(256), 0, s, a);
+    return 0;
+  } else {
   static const int use_v2 = env_int("GHOST_CONV_V2", 1);
   if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
     // measured (tools/bench_ops.py): the DMA ring wins on the 128-row tiles, loses on 256x64
-    if (use_v2 && p.fast && p.BK == 32 && d.epi != EPI_AAD && p.BM <= 128) {
+    if (use_v2 && p.fast && p.BK == 32 && d.epi != EPI_AAD && p.BM <= 128 && p.partial == (p.nsplit > 1)) {
       const bool ok = p.nsplit > 1 ? launch_glds<KEPI_SPLIT>(a, p, s) : launch_glds<KEPI_STD>(a, p, s);
       if (ok) {
         if (p.nsplit > 1) {
@@ -715,7 +730,7 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
       }
     }
   }
-  if (p.nsplit > 1) {
+  if (p.partial) {
     rc = p.fast ? dispatch_tile<TI, TO, KEPI_SPLIT, true>(a, p, s) : dispatch_tile<TI, TO, KEPI_SPLIT, false>(a, p, s);
     if (rc) return rc;
     const int ncols = d.epi == EPI_AAD ? d.C_aad : d.N;
@@ -732,6 +747,7 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
     return dispatch_tile<TI, TO, KEPI_AAD, true>(a, p, s);
   }
   return p.fast ? dispatch_tile<TI, TO, KEPI_STD, true>(a, p, s) : dispatch_tile<TI, TO, KEPI_STD, false>(a, p, s);
+  }
 }
 
 }  // namespace
@@ -740,7 +756,7 @@ size_t conv_workspace_bytes(const ConvDesc& d) {
   if (conv3x3_halo_supported(d) || convT_halo_supported(d)) return 0;
   if (conv_first_supported(d)) return conv_first_workspace_bytes();
   Plan p = make_plan(d);
-  if (p.nsplit <= 1) return 0;
+  if (!p.partial) return 0;
   return (size_t)p.npar * p.nsplit * p.M * p.NT * sizeof(float);
 }
 
@@ -759,7 +775,7 @@ int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream
   const int K = d.kind == CONV_T4S2 ? 4 * d.Cin : d.kh * d.kw * d.Cin;
   if (d.Kpad < K) return -1;
   float* partial = nullptr;
-  if (p.nsplit > 1) {
+  if (p.partial) {
     size_t need = (size_t)p.npar * p.nsplit * p.M * p.NT * sizeof(float);
     if (!ws || ws_bytes < need) return -1;
     partial = reinterpret_cast<float*>(ws);
@@ -769,6 +785,7 @@ int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream
   if (d.ti == GHOST_F32 && d.to == GHOST_F32) rc = dispatch_types<float, float>(d, a, p, stream);
   else if (d.ti == GHOST_BF16 && d.to == GHOST_BF16) rc = dispatch_types<bf16, bf16>(d, a, p, stream);
   else if (d.ti == GHOST_F32 && d.to == GHOST_BF16) rc = dispatch_types<float, bf16>(d, a, p, stream);
+  else if (d.ti == GHOST_BF16 && d.to == GHOST_F32 && !d.res && !d.y2) rc = dispatch_types<bf16, float>(d, a, p, stream);
   else return -1;
   if (rc) return rc;
   return (int)hipGetLastError();

@@ -162,6 +162,30 @@ int ghost_set_split_k(int n);
  * AADBlk8's first AADLayer pair instead of materialising it; 0 materialises it */
 int ghost_set_fuse_upsample(int on);
 
+/* ---- ArcFace identity encoder (IResNet, the netArc GHOST loads) ------------------------
+ * Replaces: inference.py:33-36 iresnet100(fp16=False) + load_state_dict + .cuda().eval();
+ *   core.py:43-54 / video_processing.py:136-140 netArc(F.interpolate(normalize_and_torch_batch(crops),
+ *   scale_factor=0.5, bilinear, align_corners=True)); video_processing.py:126,139-148 face matching.
+ * The IResNet definition itself is not in the reference tree (download_models.sh:3): parity unpinned. */
+typedef struct ghost_arc ghost_arc;
+/* layers: blocks per stage ({3,13,30,3} = iresnet100); num_features: embedding size (512) */
+int ghost_arc_create(const int layers[4], int num_features, int dtype, ghost_arc** out);
+void ghost_arc_destroy(ghost_arc* h);
+int ghost_arc_bind(ghost_arc* h, const char* name, const void* dev_ptr, int64_t numel);
+int ghost_arc_missing(ghost_arc* h);
+int64_t ghost_arc_workspace_bytes(ghost_arc* h, int N);
+/* x: [N,3,112,112] with element strides (f32/f16/bf16/u8) -> emb fp32 [N, num_features] */
+int ghost_arc_forward(ghost_arc* h, const void* x, int x_dtype, const int64_t x_strides[4], int N, float* emb,
+                      void* ws, int64_t ws_bytes, void* stream);
+/* uint8 aligned crops [N,H,W,3] (H = W = 224, channel order as given): normalize_and_torch_batch
+ * (divide by 255 only if the batch max > 1) -> bilinear 0.5x align_corners -> IResNet -> emb */
+int ghost_arc_embed_u8(ghost_arc* h, const uint8_t* crops, int64_t crop_batch_stride, int N, int H, int W,
+                       float* emb, void* ws, int64_t ws_bytes, void* stream);
+/* per target j: best_idx[j] = argmax_i cos(face_i, target_j) (first on ties), best_sim[j] = that
+ * cosine, accepted[j] = best_sim[j] > similarity_th */
+int ghost_arc_match(const float* face_emb, int F, const float* target_emb, int T, int dim, float similarity_th,
+                    int32_t* best_idx, float* best_sim, int32_t* accepted, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
