@@ -38,7 +38,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA spec
-AAD_BYTES_PER_FRAME = {"unet": 135.58e6, "linknet": 156.02e6}
+AAD_BYTES_PER_FRAME = {"unet": 135.58e6, "linknet": 156.02e6, "resnet": 135.58e6}
 
 
 def parse():
@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
+    ap.add_argument("--arc-batch", type=int, default=64,
+                    help="faces per ArcFace (iresnet100) embedding batch in the side measurement (0 = skip)")
     return ap.parse_args()
 
 
@@ -68,6 +70,49 @@ def pmc_traffic(kernel_substr):
             return {"bytes_per_launch": k["hbm_bytes"], "read": k["read_bytes"], "write": k["write_bytes"],
                     "source": "profiles/traffic_latest.json (" + data.get("source", "rocprofv3 --pmc") + ")"}
     return None
+
+
+def arcface_flops_per_face(layers=(3, 13, 30, 3)):
+    """2*MAC of IResNet at 112x112: stem, per block conv1 (s1) + conv2 (stride) + downsample, fc."""
+    fl = 2.0 * 112 * 112 * 64 * 27
+    inp, H = 64, 112
+    for planes, n in zip((64, 128, 256, 512), layers):
+        for b in range(n):
+            s = 2 if b == 0 else 1
+            Ho = H // s
+            fl += 2.0 * H * H * planes * 9 * inp + 2.0 * Ho * Ho * planes * 9 * planes
+            if b == 0:
+                fl += 2.0 * Ho * Ho * planes * inp
+            inp, H = planes, Ho
+    return fl + 2.0 * 512 * 49 * 512
+
+
+def arcface_leg(dev, n, steps):
+    """Side measurement (not the headline): iresnet100 bf16 embeddings/s on device u8 224x224 crops
+    (normalise + 0.5x resize + network), the per-frame identity path of config 5."""
+    from ghost_amd.arcface import iresnet100
+    from oracle.arcface_ref import make_weights, param_specs
+    net = iresnet100(fp16=False, compute_dtype=torch.bfloat16).eval()
+    net.load_state_dict(make_weights(param_specs()))
+    net = net.to(dev)
+    crops = torch.from_numpy(np.random.Generator(np.random.PCG64(5)).integers(0, 256, (n, 224, 224, 3),
+                                                                           dtype=np.uint8)).to(dev)
+    for _ in range(2):
+        net.embed_u8(crops)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        net.embed_u8(crops)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    fl = arcface_flops_per_face() * n
+    return {"model": "iresnet100 bf16 (synthetic weights), u8 224x224 crops -> 512-d embeddings", "batch": n,
+            "ms_per_batch": round(ms, 3), "embeddings_per_s": round(n / (ms / 1e3), 1),
+            "gflop_per_face": round(arcface_flops_per_face() / 1e9, 2),
+            "mfma_tflops": round(fl / (ms / 1e3) / 1e12, 1),
+            "mfma_frac": round(fl / (ms / 1e3) / 1e12 / BF16_PEAK_TFLOPS, 4)}
 
 
 def cpu_baseline(backbone, nb, seconds):
@@ -162,7 +207,8 @@ def main():
         frames = world * B * a.steps
         value = frames / el
         res = {
-            "metric": "swapped frames/sec at 256x256 bf16 (AEI_Net unet/2 swap forward, device-resident u8 crops)",
+            "metric": f"swapped frames/sec at 256x256 {'bf16' if a.dtype == 'bf16' else 'fp32'} (AEI_Net "
+                      f"{a.backbone}/{a.num_blocks} swap forward, device-resident u8 crops)",
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.dtype if a.dtype == "fp32" else "bf16", "data": "synthetic",
@@ -177,7 +223,8 @@ def main():
             per_launch_bytes = c["bytes"] / c["launches"]
             per_launch_s = c["ms"] / c["launches"] / 1e3
             ach = per_launch_bytes / per_launch_s / 1e9
-            kname = "aad_v3_kernel<64, 64, 2, true>"
+            ca8 = 32 if a.backbone == "linknet" else 64     # z_attr8 channels (AEI_Net.py:110,118)
+            kname = f"aad_v3_kernel<64, {ca8}, 2, true>"
             res["roofline"] = {"kernel": f"{kname}: two AADLayers sharing h_in/z_attr at 256x256, h_in = bilinear "
                                          "x2 of the 128x128 block output sampled in-kernel (IN-normalise, sigmoid "
                                          "mask, MFMA gamma/beta, blend, ReLU)",
@@ -206,6 +253,8 @@ def main():
             res["kernel_ms_per_step"] = {k: round(v["ms"] / a.steps, 3) for k, v in classes.items()}
             res["kernel_ms_per_step_note"] = ("aad_dual_256 from the timed region; the other classes from an "
                                               "untimed pass with every class bracketed by HIP events")
+        if world == 1 and a.arc_batch > 0:
+            res["arcface"] = arcface_leg(dev, a.arc_batch, max(3, a.steps // 2))
         if world == 1 and a.cpu_seconds > 0:
             res["cpu_baseline"] = cpu_baseline(a.backbone, a.num_blocks, a.cpu_seconds)
         print(json.dumps(res), flush=True)
