@@ -33,6 +33,7 @@ static int fail(int rc, const std::string& msg) {
 namespace ghost {
 // shared with the other runtimes of the library (arc_runtime.hip): one ghost_last_error() per thread
 int set_last_error(int rc, const std::string& msg) { return fail(rc, msg); }
+int set_last_error(int rc, const char* msg) { return fail(rc, std::string(msg)); }
 }  // namespace ghost
 
 extern "C" const char* ghost_version(void) { return "ghost_amd 0.1 (gfx950)"; }

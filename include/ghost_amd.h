@@ -186,6 +186,16 @@ int ghost_arc_embed_u8(ghost_arc* h, const uint8_t* crops, int64_t crop_batch_st
 int ghost_arc_match(const float* face_emb, int F, const float* target_emb, int T, int dim, float similarity_th,
                     int32_t* best_idx, float* best_sim, int32_t* accepted, void* stream);
 
+/* ---- paste-back blend (get_final_video, utils/inference/video_processing.py:218-227) ----
+ * For each frame f with valid[f] != 0 (valid may be NULL): warp the crop-space swap [Hs,Ws,3] u8 and
+ * mask [Hs,Ws] f32 back into the frame with kornia.warp_affine semantics (bilinear, zeros,
+ * align_corners=True, destination pixel sampled at mats[f] (x, y, 1), mats = the crop <- frame tfm
+ * [F][2][3] fp32) and composite in place: frame = uint8(mask_t*swap_t + (1-mask_t)*frame).
+ * Several identities on one frame: call once per identity, in the reference's order. */
+int ghost_blend_swaps_u8(uint8_t* frames, int64_t frame_stride, int F, int H, int W, const uint8_t* swaps,
+                         int64_t swap_stride, int Hs, int Ws, const float* masks, int64_t mask_stride,
+                         const float* mats, const int32_t* valid, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
