@@ -15,6 +15,7 @@
 // Every BatchNorm that precedes a zero-padded conv is applied by its producer's second output, never
 // folded into the conv weights (folding is wrong on the padded border).
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <map>
 #include <vector>
@@ -81,8 +82,17 @@ struct ArcCtx {
   }
 };
 
+static int arc_min_wgs() {
+  static const int v = [] {
+    const char* e = getenv("GHOST_ARC_MINWG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 void run_conv(ArcCtx& c, ConvDesc& d, const std::string& what) {
   if (!c.ok()) return;
+  d.min_wgs = arc_min_wgs();
   if (c.dry) {
     const size_t need = conv_workspace_bytes(d);
     if (need > c.scratch_need) c.scratch_need = need;
@@ -202,14 +212,25 @@ int64_t arc_bytes(ghost_arc* h, int N, size_t* scratch) {
 // pre-processing: normalize_and_torch_batch (image_processing.py:37-48) + F.interpolate(0.5,
 // bilinear, align_corners=True) (core.py:44; video_processing.py:138) in one pass
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) u8_max_kernel(const uint8_t* __restrict__ p, long bstride, int N, long per,
+__global__ void __launch_bounds__(256) u8_max_kernel(const uint8_t* __restrict__ p, long bstride, int per,
                                                       int* out) {
-  // one flag for the whole batch: the reference divides by 255 only if batch.max() > 1
+  // one flag for the whole batch: the reference divides by 255 only if batch.max() > 1.
+  // blockIdx.y = sample; 16-byte loads where the sample base is aligned, bytes otherwise
+  const uint8_t* s = p + (long)blockIdx.y * bstride;
   int m = 0;
-  const long total = (long)N * per;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long n = i / per;
-    const int v = p[n * bstride + (i - n * per)];
+  const int nvec = ((uintptr_t)s % 16 == 0) ? per / 16 : 0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += gridDim.x * 256) {
+    const u32x4 v = reinterpret_cast<const u32x4*>(s)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned w = v[k];
+      const unsigned b0 = w & 255u, b1 = (w >> 8) & 255u, b2 = (w >> 16) & 255u, b3 = w >> 24;
+      const unsigned mm = max(max(b0, b1), max(b2, b3));
+      m = (int)mm > m ? (int)mm : m;
+    }
+  }
+  for (int i = nvec * 16 + blockIdx.x * 256 + threadIdx.x; i < per; i += gridDim.x * 256) {
+    const int v = s[i];
     m = v > m ? v : m;
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -300,7 +321,7 @@ __global__ void __launch_bounds__(256) arc_match_kernel(const float* __restrict_
 int run_arc(ghost_arc* h, int N, const void* xt, int xt_dtype, const int64_t* st, const uint8_t* crops,
             int64_t crop_bs, int Hs, int Ws, float* emb, void* ws, int64_t ws_bytes, void* stream) {
   if (!h) return arc_fail(GHOST_EINVAL, "null handle");
-  if (N <= 0) return arc_fail(GHOST_EINVAL, "batch must be positive");
+  if (N <= 0 || N > 65535) return arc_fail(GHOST_EINVAL, "batch must be in 1..65535");
   for (auto& kv : h->slots)
     if (!kv.second) return arc_fail(GHOST_ENOTREADY, "unbound weight slot " + kv.first);
   size_t scratch = 0;
@@ -323,10 +344,8 @@ int run_arc(ghost_arc* h, int N, const void* xt, int xt_dtype, const int64_t* st
   c.scratch_cap = scratch;
   if (crops) {
     if (hipMemsetAsync(flag, 0, sizeof(int), c.s) != hipSuccess) return arc_fail(GHOST_EINVAL, "memset failed");
-    const long per = (long)Hs * Ws * 3;
-    const long total = (long)N * per;
-    const unsigned g = (unsigned)std::min<long>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(u8_max_kernel, dim3(g), dim3(256), 0, c.s, crops, (long)crop_bs, N, per, flag);
+    const int per = Hs * Ws * 3;
+    hipLaunchKernelGGL(u8_max_kernel, dim3(8, (unsigned)N), dim3(256), 0, c.s, crops, (long)crop_bs, per, flag);
     const float sh = (float)(Hs - 1) / (float)(112 - 1), sw = (float)(Ws - 1) / (float)(112 - 1);
     const long P = (long)N * 112 * 112;
     dim3 grid((unsigned)((P + 255) / 256));
@@ -414,7 +433,7 @@ extern "C" int ghost_arc_match(const float* face_emb, int F, const float* target
                                float similarity_th, int32_t* best_idx, float* best_sim, int32_t* accepted,
                                void* stream) {
   if (!face_emb || !target_emb || !best_idx || !best_sim || !accepted) return arc_fail(GHOST_EINVAL, "null argument");
-  if (F <= 0 || T <= 0 || dim <= 0 || dim > 1024) return arc_fail(GHOST_EINVAL, "bad sizes");
+  if (F <= 0 || T <= 0 || dim <= 0 || dim > 1024 || T > 65535) return arc_fail(GHOST_EINVAL, "bad sizes");
   hipLaunchKernelGGL(arc_match_kernel, dim3(T), dim3(256), 0, (hipStream_t)stream, face_emb, F, target_emb, dim,
                      similarity_th, best_idx, best_sim, accepted);
   const int rc = (int)hipGetLastError();

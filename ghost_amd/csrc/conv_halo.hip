@@ -47,6 +47,7 @@ struct HaloArgs {
   int H, W, Cin, ldx, N, Kpad, ldy, ldres, tanh_out;
   float slope;
   int tiles_x, tiles_y, nNt, ntiles;
+  int dbg;   // experiment mask (GHOST_HALO_DBG): 2 no halo DMA, 4 no weight DMA, 8 no MFMA
 };
 
 __device__ __attribute__((aligned(16))) unsigned int g_halo_zero[64] = {0};
@@ -190,6 +191,230 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
       *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent, double-buffered form of the 16 x 32 halo conv (the 32x32 .. 256x256 stages).
+//
+// The kernel above stages one channel block, waits for it and computes it: with two workgroups
+// per CU each one's DMA latency is exposed about half the time (measured 0.54-0.92 PF on the
+// generator stages against a 124 us MFMA floor per 309 GFLOP).  Here ONE workgroup per CU walks
+// a strided list of (tile, channel block) stages and keeps the DMA of stage s+1 in flight while it
+// computes stage s: two 75 KB LDS stages (halo + the block's 9 x 64 weight rows) = 150 KB.
+//   top of stage s:  s_waitcnt vmcnt(0)        (or vmcnt(16) when the previous stage ended a tile:
+//                                               its 16 epilogue stores are the wave's youngest ops)
+//                    raw s_barrier             (every wave's DMA(s) landed; stage s-1 buffer free)
+//                    issue DMA(s+1) -> buffer (s+1)&1
+//                    9 taps x 16 MFMA from buffer s&1;  last block of a tile -> epilogue stores
+// Barriers are raw __builtin_amdgcn_s_barrier: __syncthreads() would drain the in-flight DMA
+// (cdna_hip_programming.md, glds notes).  Scale/shift live in LDS so the epilogue issues no
+// ordinary global load while a DMA is outstanding (hipcc would wait vmcnt(0) for its result).
+// ---------------------------------------------------------------------------
+template <bool RESW>
+__global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) {
+  // RESW: Cin <= 64 and N == 64 — the whole weight tensor (<= 2 blocks x 36 KB) stays resident in
+  // LDS for the kernel and only the halo (39 KB) streams per stage; otherwise every stage carries
+  // its channel block's 9 x 64 weight rows too (75 KB).
+  using G = HaloWide;
+  constexpr int TW = G::TW, HWW = G::HWW, HP = G::HP, HPIECES = G::HPIECES, WPIECES = G::WPIECES;
+  constexpr int HALO_B = G::HALO_B, NW = G::NW, HPW = G::HPW, WPW = G::WPW, RPW = 64 / TW;
+  constexpr int WBLK_B = 9 * 64 * 64;                           // one channel block of weights
+  constexpr int STAGE_B = RESW ? HALO_B : HALO_B + WBLK_B;
+  // two stage buffers as DISTINCT objects, read/written in an unrolled ping-pong: hipcc then proves
+  // that the LDS reads of stage s do not alias the DMA into stage s+1 and does not drain it with a
+  // vmcnt(0) before the first read (one object indexed by s & 1 gets that drain)
+  __shared__ __attribute__((aligned(1024))) unsigned char lds0[STAGE_B];
+  __shared__ __attribute__((aligned(1024))) unsigned char lds1[STAGE_B];
+  __shared__ __attribute__((aligned(1024))) unsigned char ldsw[RESW ? 2 * WBLK_B : 16];
+  __shared__ float s_sc[512], s_sh[512];
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
+  const int prow = lane >> 2, slot = lane & 3;
+
+  for (int n = tid; n < a.N; n += 512) {
+    s_sc[n] = a.scale ? a.scale[n] : 1.f;
+    s_sh[n] = a.shift ? a.shift[n] : 0.f;
+  }
+  const int ncb = a.Cin / 32;
+  // per-lane weight source offsets within a channel block (tap, row) — independent of the tile
+  int w_off[WPW];
+#pragma unroll
+  for (int j = 0; j < WPW; ++j) {
+    const int piece = wid + j * NW;
+    const int tap = piece / 4, n = (piece % 4) * 16 + prow;
+    w_off[j] = n * a.Kpad + tap * 32 + ((slot ^ hswz(n)) * 8);
+  }
+  unsigned char* wres = ldsw;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (RESW) {
+    for (int cb = 0; cb < ncb; ++cb)
+#pragma unroll
+      for (int j = 0; j < WPW; ++j) {
+        const int piece = wid + j * NW;
+        if (piece < WPIECES)
+          __builtin_amdgcn_global_load_lds(a.w + w_off[j] + cb * 288, wres + cb * WBLK_B + piece * 1024, 16, 0, 0);
+      }
+  }
+#endif
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int G_ = gridDim.x;
+  const int xt = xcd_tile(blockIdx.x, G_);
+  const int nmine = a.ntiles > xt ? (a.ntiles - xt + G_ - 1) / G_ : 0;
+  const int nst = nmine * ncb;
+
+  // tile of this WG's k-th item, and this lane's halo DMA sources for it (element offsets from the
+  // sample base; bit j of ok = piece j inside the image)
+  struct Tile { long base; int y0, x0, n0; };
+  auto tile_of = [&](int k) {
+    int t = k * G_ + xt;
+    Tile r;
+    const int nt = t % a.nNt;
+    t /= a.nNt;
+    const int tx = t % a.tiles_x;
+    t /= a.tiles_x;
+    const int ty = t % a.tiles_y;
+    r.base = (long)(t / a.tiles_y) * a.H * a.W;
+    r.y0 = ty * G::TH;
+    r.x0 = tx * TW;
+    r.n0 = nt * 64;
+    return r;
+  };
+  int h_off[HPW];
+  unsigned h_ok = 0u;
+  long dma_base = 0;
+  int dma_n0 = 0;
+  auto set_dma_tile = [&](const Tile& t) {
+    dma_base = t.base * a.ldx;
+    dma_n0 = t.n0;
+    h_ok = 0u;
+#pragma unroll
+    for (int j = 0; j < HPW; ++j) {
+      const int piece = wid + j * NW;
+      const int P = piece * 16 + prow;
+      const int hy = P / HWW, hx = P - hy * HWW;
+      const int iy = t.y0 - 1 + hy, ix = t.x0 - 1 + hx;
+      const bool ok = piece < HPIECES && P < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      h_off[j] = ok ? (iy * a.W + ix) * a.ldx + ((slot ^ hswz(P)) * 8) : 0;
+      h_ok |= (ok ? 1u : 0u) << j;
+    }
+  };
+  auto issue = [&](unsigned char* buf, int cb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const bf16* __restrict__ xs = a.x + dma_base + cb * 32;
+#pragma unroll
+    for (int j = 0; j < HPW; ++j) {
+      const int piece = wid + j * NW;
+      if (piece < HPIECES && !(a.dbg & 2)) {
+        const void* src = ((h_ok >> j) & 1u) ? (const void*)(xs + h_off[j]) : (const void*)g_halo_zero;
+        __builtin_amdgcn_global_load_lds(src, buf + piece * 1024, 16, 0, 0);
+      }
+    }
+    if constexpr (!RESW) {
+      const bf16* __restrict__ ws = a.w + (long)dma_n0 * a.Kpad + cb * 288;
+#pragma unroll
+      for (int j = 0; j < WPW; ++j) {
+        const int piece = wid + j * NW;
+        if (piece < WPIECES && !(a.dbg & 4))
+          __builtin_amdgcn_global_load_lds(ws + w_off[j], buf + HALO_B + piece * 1024, 16, 0, 0);
+      }
+    }
+#endif
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Stage order: tile k = 0..nmine-1, channel blocks cb = 0..ncb-1 (ncb even): even blocks read
+  // lds0 and prefetch into lds1, odd blocks the reverse, so every wait below is static:
+  //   first block of a tile  -> vmcnt(16): the previous tile's 16 epilogue stores are the youngest
+  //   other blocks           -> vmcnt(0)
+  // and the compiler's own waitcnt pass sees the same program order (no drain of the prefetch).
+  if (nmine == 0) return;
+  Tile cur = tile_of(0);
+  set_dma_tile(cur);
+  issue(lds0, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0): DMA(0) (nothing to overlap it with yet)
+  int nk = 0, ncb_next = 1;                 // (tile, block) of the next DMA
+  auto step = [&](bool first, int cb, const unsigned char* buf, unsigned char* nbuf) {
+    // gfx9 simm16: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] at [15:14]
+    if (first)
+      __builtin_amdgcn_s_waitcnt(0x4F70);   // vmcnt(16)
+    else
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    if (nk < nmine) {
+      if (ncb_next == 0) set_dma_tile(tile_of(nk));   // first block of the next tile
+      issue(nbuf, ncb_next);
+      if (++ncb_next == ncb) { ncb_next = 0; ++nk; }
+    }
+    const unsigned char* wb = RESW ? wres + cb * WBLK_B : buf + HALO_B;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      if (a.dbg & 8) break;
+      asm volatile("" ::: "memory");
+      const int dy = tap / 3, dx = tap - dy * 3;
+      bf16x8 wf[4], pf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = j * 16 + lr;
+        wf[j] = *reinterpret_cast<const bf16x8*>(wb + (tap * 64 + n) * 64 + ((lq ^ hswz(n)) * 16));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int P = (wid * RPW + (i * 16) / TW + dy) * HWW + (i * 16) % TW + lr + dx;
+        pf[i] = *reinterpret_cast<const bf16x8*>(buf + P * 64 + ((lq ^ hswz(P)) * 16));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], pf[i], acc[j][i], 0, 0, 0);
+    }
+  };
+  if (ncb == 1) { ncb_next = 0; nk = 1; }
+  for (int k = 0; k < nmine; ++k) {
+    step(true, 0, lds0, lds1);
+    step(false, 1, lds1, lds0);
+    for (int cb = 2; cb < ncb; cb += 2) {
+      step(false, cb, lds0, lds1);
+      step(false, cb + 1, lds1, lds0);
+    }
+    // epilogue: exactly 16 vector stores per wave (N % 64 == 0, full tiles), the youngest VM ops
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int oy = cur.y0 + wid * RPW + (i * 16) / TW, ox = cur.x0 + (i * 16) % TW + lr;
+      const long pix = cur.base + (long)oy * a.W + ox;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = cur.n0 + j * 16 + lq * 4;
+        float rv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (a.res) {
+          const uint2 raw = *reinterpret_cast<const uint2*>(a.res + pix * a.ldres + n);
+          const bf16* e = reinterpret_cast<const bf16*>(&raw);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rv[r] = (float)e[r];
+        }
+        uint2 o;
+        bf16* oe = reinterpret_cast<bf16*>(&o);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = fmaf(acc[j][i][r], s_sc[n + r], s_sh[n + r]);
+          v = v > 0.f ? v : v * a.slope;
+          v += rv[r];
+          if (a.tanh_out) v = tanhf(v);
+          oe[r] = (bf16)v;
+          acc[j][i][r] = 0.f;
+        }
+        *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+      }
+    }
+    if (k + 1 < nmine) cur = tile_of(k + 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -414,9 +639,49 @@ static int halo_launch(const ConvDesc& d, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+static int num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
+  HaloArgs a{};
+  a.x = (const bf16*)d.x; a.w = (const bf16*)d.w; a.y = (bf16*)d.y;
+  a.scale = d.scale; a.shift = d.shift; a.res = (const bf16*)d.res;
+  a.H = d.Hi; a.W = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx; a.N = d.N; a.Kpad = d.Kpad;
+  a.ldy = d.ldy; a.ldres = d.ldres; a.tanh_out = d.tanh_out; a.slope = d.slope;
+  a.tiles_x = d.Wi / HaloWide::TW; a.tiles_y = d.Hi / HaloWide::TH; a.nNt = d.N / 64;
+  a.ntiles = d.B * a.tiles_x * a.tiles_y * a.nNt;
+  static const int dbg = [] {
+    const char* e = getenv("GHOST_HALO_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = dbg;
+  const int g = a.ntiles < num_cus() ? a.ntiles : num_cus();
+  if (d.Cin <= 64 && d.N == 64)
+    hipLaunchKernelGGL(conv3x3_halo_pp_kernel<true>, dim3((unsigned)g), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL(conv3x3_halo_pp_kernel<false>, dim3((unsigned)g), dim3(512), 0, s, a);
+  return (int)hipGetLastError();
+}
+
 int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
   if (!conv3x3_halo_supported(d)) return -1;
-  if (d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0) return halo_launch<HaloWide>(d, s);
+  static const int pp = [] {
+    const char* e = getenv("GHOST_HALO_PP");
+    return e ? atoi(e) : 1;
+  }();
+  const bool wide = d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0;
+  // measured A/B (B = 64): the persistent form wins up to Cin = 256 (256x256: -23 %, 128x128: -7 %,
+  // 64x64 256->256: -9 %); at Cin >= 512 the per-stage barrier costs more than the prefetch saves
+  if (wide && pp && d.N <= 512 && d.Cin % 64 == 0 && d.Cin <= 256) return halo_pp_launch(d, s);
+  if (wide) return halo_launch<HaloWide>(d, s);
   return halo_launch<HaloSmall>(d, s);
 }
 

@@ -54,6 +54,7 @@ struct ConvDesc {
   const float* mask = nullptr;               // [B*H*W] sigmoid mask
   int C_aad = 0;
   int force_split = 0;                       // >0: override the split-K heuristic (tests)
+  int min_wgs = 0;                           // split K while the grid has fewer tiles (0 = 256)
 };
 
 // bytes of fp32 split-K workspace the launch may use

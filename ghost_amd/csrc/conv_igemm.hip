@@ -606,8 +606,9 @@ Plan make_plan(const ConvDesc& d) {
   int s = 1;
   if (d.force_split > 0) {
     s = d.force_split;
-  } else if (tiles < 256 && nk >= 16) {
-    s = (512 + tiles - 1) / tiles;          // aim for >= 2 workgroups per CU
+  } else if (tiles < (d.min_wgs > 0 ? d.min_wgs : 256) && nk >= 16) {
+    const int target = 2 * (d.min_wgs > 0 ? d.min_wgs : 256);
+    s = (target + tiles - 1) / tiles;       // aim for >= 2 workgroups per CU
     s = s < nk / 8 ? s : nk / 8;            // keep >= 8 K steps per split
     if (s < 1) s = 1;
   }

@@ -62,6 +62,33 @@ def conv_cases(lib, iters, dt=torch.bfloat16):
         print(f"conv  {name:22s} {us:9.1f} us  {fl / us / 1e6:7.1f} TF/s  {by / us / 1e3:7.1f} GB/s(io)", flush=True)
 
 
+def arc_cases(lib, iters, dt=torch.bfloat16):
+    """ArcFace (iresnet100 at B=64) conv shapes through ghost_conv2d_nhwc."""
+    B = 64
+    ws = torch.empty(512 << 20, dtype=torch.uint8, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    for name, H, ci, co, k, s, p in [("arc112 64->64", 112, 64, 64, 3, 1, 1), ("arc56 64->64", 56, 64, 64, 3, 1, 1),
+                                     ("arc28 128->128", 28, 128, 128, 3, 1, 1),
+                                     ("arc14 256->256", 14, 256, 256, 3, 1, 1),
+                                     ("arc7 512->512", 7, 512, 512, 3, 1, 1),
+                                     ("arc28s2 128->256", 28, 128, 256, 3, 2, 1),
+                                     ("gen32 512->512", 32, 512, 512, 3, 1, 1),
+                                     ("gen16 1024->1024", 16, 1024, 1024, 3, 1, 1)]:
+        x = torch.randn(B, H, H, ci, device=DEV).to(dt)
+        w = pack_conv(torch.randn(co, ci, k, k, device=DEV) * 0.05, dt)
+        Ho = (H + 2 * p - k) // s + 1
+        y = torch.empty(B, Ho, Ho, co, dtype=dt, device=DEV)
+
+        def run():
+            _lib.check(lib.ghost_conv2d_nhwc(_lib.gdtype(dt), x.data_ptr(), B, H, H, ci, ci, w.data_ptr(), co,
+                                             w.shape[0], w.shape[1], k, k, s, p, None, None, 1.0, None, 0, 0,
+                                             y.data_ptr(), co, ws.data_ptr(), ws.numel(), st))
+        us = timeit(run, iters)
+        fl = 2.0 * B * Ho * Ho * co * ci * k * k
+        print(f"conv  {name:22s} M={B * Ho * Ho:7d} N={co:4d} K={ci * k * k:5d} {us:9.1f} us  "
+              f"{fl / us / 1e6:7.1f} TF/s", flush=True)
+
+
 def enc_cases(lib, iters, dt=torch.bfloat16):
     """Every encoder contraction of unet at B = 64: Conv4x4/s2 (conv1..7) and ConvT4x4/s2 (deconv1..6)."""
     B = 64
@@ -224,6 +251,8 @@ def main():
         ceiling_cases(a.iters)
     if a.only in ("", "conv"):
         conv_cases(lib, a.iters)
+    if a.only in ("", "arc"):
+        arc_cases(lib, a.iters)
     if a.only in ("", "enc"):
         enc_cases(lib, a.iters)
     if a.only in ("", "aad"):
