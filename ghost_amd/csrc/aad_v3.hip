@@ -203,9 +203,9 @@ template <int C, int CA, int L, bool UP>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v3_kernel(const AadV3Args a) {
   aad_v3_body<C, CA, L, UP>(a);
 }
-template <int C, int CA, int L>
+template <int C, int CA, int L, bool UP>
 __global__ void __launch_bounds__(512) aad_v3_wide_kernel(const AadV3Args a) {
-  aad_v3_body<C, CA, L, false>(a);
+  aad_v3_body<C, CA, L, UP>(a);
 }
 
 bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo) {
@@ -230,7 +230,7 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   a.PPW = d.HW >= 65536 ? 1024 : 512;
   const bool up = d.up_H > 0;
   if (up) {
-    if (4 * d.up_H * d.up_W != d.HW || d.up_W * 2 < 16 || d.C != 64) return -1;
+    if (4 * d.up_H * d.up_W != d.HW || d.up_W * 2 < 16 || (d.C != 64 && d.C != 128)) return -1;
     a.up = up2x_src(d.up_H, d.up_W);
   }
   dim3 grid((unsigned)((long)d.B * d.HW / a.PPW));
@@ -239,15 +239,17 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
     hipLaunchKernelGGL((aad_v3_kernel<c, ca, l, u>), grid, dim3(kWaves * 64), 0, s, a);         \
     return (int)hipGetLastError();                                                              \
   }
-#define GHOST_V3W(c, ca, l)                                                                     \
-  if (d.C == c && d.Ca == ca && d.L == l && !up) {                                              \
-    hipLaunchKernelGGL((aad_v3_wide_kernel<c, ca, l>), grid, dim3(kWaves * 64), 0, s, a);       \
+#define GHOST_V3W(c, ca, l, u)                                                                  \
+  if (d.C == c && d.Ca == ca && d.L == l && up == u) {                                          \
+    hipLaunchKernelGGL((aad_v3_wide_kernel<c, ca, l, u>), grid, dim3(kWaves * 64), 0, s, a);    \
     return (int)hipGetLastError();                                                              \
   }
   GHOST_V3(64, 64, 1, false) GHOST_V3(64, 64, 2, false) GHOST_V3(64, 32, 1, false) GHOST_V3(64, 32, 2, false)
   // through-upsample forms: the block-input AADLayers of AADBlk8 (first add_block + last_add_block)
   GHOST_V3(64, 64, 2, true) GHOST_V3(64, 32, 2, true) GHOST_V3(64, 64, 1, true) GHOST_V3(64, 32, 1, true)
-  GHOST_V3W(128, 128, 1) GHOST_V3W(128, 64, 1) GHOST_V3W(128, 32, 1)
+  GHOST_V3W(128, 128, 1, false) GHOST_V3W(128, 64, 1, false) GHOST_V3W(128, 32, 1, false)
+  // AADBlk7's block-input AADLayers read upsample2x(AADBlk6 output) on the fly (C = 128)
+  GHOST_V3W(128, 128, 1, true) GHOST_V3W(128, 64, 1, true) GHOST_V3W(128, 32, 1, true)
 #undef GHOST_V3W
 #undef GHOST_V3
   return -1;

@@ -599,6 +599,8 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
       int Ca_n, n_n;
       h->attr_geom(k + 1, Ca_n, n_n);
       const int cout_n = h->gen()[k][1];
+      // C = 64 only: at C = 128 (AADBlk7) the two single-layer kernels re-reading the upsample
+      // cost more (+110 us) than the materialised upsample they replace (-85 us), measured B = 64
       const bool fuse = g_fuse_upsample && cout != cout_n && cout == 64 && Ca_n % 32 == 0 &&
                         aad_v3_supported(h->dt, B, n_n * n_n, cout, Ca_n, Ca_n, cout, 8);
       if (fuse) {
@@ -1048,7 +1050,8 @@ extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, con
   hipStream_t s = (hipStream_t)stream;
   const int HW = H * W;
   if (L < 1 || L > 2) return fail(GHOST_EINVAL, "aad_v3: L must be 1 or 2");
-  if (up2x && (H % 2 || W % 2 || C != 64)) return fail(GHOST_EINVAL, "aad_v3: up2x needs even H, W and C = 64");
+  if (up2x && (H % 2 || W % 2 || (C != 64 && C != 128)))
+    return fail(GHOST_EINVAL, "aad_v3: up2x needs even H, W and C in {64, 128}");
   const bool wide = C >= 256;   // aad_wide: one layer, C in {256, 512, 1024}, Ca <= 512
   if (wide && (L != 1 || up2x || !aad_wide_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[0])))
     return fail(GHOST_EINVAL, "aad_wide: unsupported shape (one layer, C in {256,512,1024}, Ca <= 512)");

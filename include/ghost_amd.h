@@ -143,7 +143,7 @@ int ghost_aad_layer_nhwc(int dtype, const void* h_in, int ldh, const void* z_att
 /* One or two AADLayers (bf16, C in {64,128}) that read the same h_in and z_attr, in one pass:
  * w3/b3 per layer in the permuted layout of pack.py pack_aad_v3; InstanceNorm statistics of h_in
  * are computed into the workspace first.  up2x = 1: h_in is upsample2x of the [B, H/2, W/2, C]
- * tensor passed as h_in (F.interpolate of AEI_Net.py:137 fused into the AADLayer read; C = 64).
+ * tensor passed as h_in (F.interpolate of AEI_Net.py:135-137 fused into the AADLayer read; C in {64, 128}).
  * C in {256, 512, 1024} (L = 1, Ca <= 512) runs the per-channel-tile kernel of aad_wide.hip. */
 int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, const void* z_attr, int lda, int B, int H, int W,
                              int C, int Ca, int L, const void* const w3[], const float* const b3[],

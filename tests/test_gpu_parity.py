@@ -520,6 +520,7 @@ def test_conv3x3_narrow_op(lib, dt, cin, cout, H, W, use_res):
 @pytest.mark.parametrize("c_x,c_a,n,B,L,up", [(64, 64, 256, 2, 2, 0), (64, 64, 256, 2, 1, 0), (128, 128, 128, 2, 1, 0),
                                               (64, 32, 128, 4, 2, 0), (128, 64, 64, 8, 1, 0), (128, 32, 64, 8, 1, 0),
                                               (64, 64, 256, 2, 2, 1), (64, 32, 128, 4, 2, 1), (64, 64, 64, 8, 1, 1),
+                                              (128, 64, 128, 2, 1, 1), (128, 32, 64, 8, 1, 1),
                                               # aad_wide: one 64-channel tile per workgroup
                                               (256, 128, 64, 8, 1, 0), (512, 256, 32, 8, 1, 0),
                                               (1024, 256, 16, 16, 1, 0), (512, 64, 32, 4, 1, 0),
