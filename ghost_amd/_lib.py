@@ -67,6 +67,8 @@ _SIGS = {
     "ghost_crops_to_input_nhwc": (i32, [vp, i64, i32, i32, i32, i32, vp, vp]),
     "ghost_set_split_k": (i32, [i32]),
     "ghost_set_fuse_upsample": (i32, [i32]),
+
+    "ghost_set_fuse_stats": (i32, [i32]),
     "ghost_aad_layers_v3_nhwc": (i32, [vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp), C.POINTER(vp),
                                        C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), i32, f32, C.POINTER(vp),
                                        C.POINTER(i32), vp, i64, vp]),

@@ -16,6 +16,8 @@
 // beta of 16 *contiguous-in-pairs-of-8* channels of ONE pixel: the blend needs no LDS
 // round trip and every global access is a 16-byte vector along channels.
 // HBM bytes per launch = |h_in| + |z_attr| + L * |out|  (the algorithmic minimum).
+#include <cstdlib>
+
 #include "aad_v3.h"
 #include "ghost_common.h"
 #include "up2x.h"
@@ -208,6 +210,245 @@ __global__ void __launch_bounds__(512) aad_v3_wide_kernel(const AadV3Args a) {
   aad_v3_body<C, CA, L, UP>(a);
 }
 
+// ---------------------------------------------------------------------------------------------
+// v4: the C = 64 kernel with the next tile's inputs in flight while the current one computes.
+//
+// v3 issues a tile's loads and waits for them: PMC shows its waves parked on memory 57-67 % of the
+// time (SQ_WAIT_ANY).  Here every wave keeps TWO 16-pixel tiles in flight: at the top of tile t it
+// issues tile t+1's z_attr fragments (to registers) and its h_in pixels (LDS-DMA into a wave-private
+// slot; for the through-upsample form the <= 10 source pixels of each of the two source rows), then
+// computes tile t.  The two slots are distinct LDS objects and the loop is unrolled by two, so the
+// compiler's own waitcnt pass knows which DMA a read depends on: the waits it emits leave tile t+1's
+// loads (and tile t-1's stores) in flight.  The h_in slot is XOR-swizzled on the source side
+// (chunk c of pixel p lands at chunk c ^ (p & 7)) so the 16 pixels a lane group reads hit 16 bank
+// groups.
+// ---------------------------------------------------------------------------------------------
+template <int CA, int L, bool UP>
+struct V4Cfg {
+  static constexpr int C = 64, KS = CA / 32, WLD = CA + 8, NH = 2;
+  static constexpr int SPX = UP ? 10 : 16;        // h pixels per row held in a slot
+  static constexpr int ROWS = UP ? 2 : 1;
+  static constexpr int SLOT_B = ROWS * SPX * 128;  // bytes per wave per slot
+};
+
+template <int CA, int L, bool UP>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v4_kernel(const AadV3Args a) {
+  using K = V4Cfg<CA, L, UP>;
+  constexpr int C = 64, KS = K::KS, WLD = K::WLD, SPX = K::SPX, SLOT_B = K::SLOT_B;
+  __shared__ __attribute__((aligned(16))) bf16 s_w[L * 128 * WLD];
+  __shared__ __attribute__((aligned(16))) float s_b[L * 128];
+  __shared__ __attribute__((aligned(16))) float s_rs[C];
+  __shared__ __attribute__((aligned(16))) float s_nm[C];
+  __shared__ __attribute__((aligned(16))) float s_cf[L * C];
+  __shared__ float s_k[L];
+  __shared__ __attribute__((aligned(16))) float s_gi[L * C];
+  __shared__ __attribute__((aligned(16))) float s_bi[L * C];
+  __shared__ __attribute__((aligned(1024))) unsigned char s_hA[kWaves * SLOT_B];
+  __shared__ __attribute__((aligned(1024))) unsigned char s_hB[kWaves * SLOT_B];
+
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const long p_begin = (long)blockIdx.x * a.PPW;
+  const int b = (int)(p_begin / a.HW);
+
+  for (int l = 0; l < L; ++l) {
+    for (int idx = tid; idx < 128 * (CA / 8); idx += kWaves * 64) {
+      const int row = idx / (CA / 8), kc = idx - row * (CA / 8);
+      *reinterpret_cast<u32x4*>(&s_w[(l * 128 + row) * WLD + kc * 8]) =
+          *reinterpret_cast<const u32x4*>(a.w3[l] + (long)row * CA + kc * 8);
+    }
+    for (int idx = tid; idx < 128; idx += kWaves * 64) s_b[l * 128 + idx] = a.b3[l][idx];
+    for (int c = tid; c < C; c += kWaves * 64) {
+      const float rs = a.stat[((long)b * C + c) * 2 + 1];
+      s_cf[l * C + c] = a.wh[l][c] * rs;
+      s_gi[l * C + c] = a.idgb[l][(long)b * a.id_ld + c];
+      s_bi[l * C + c] = a.idgb[l][(long)b * a.id_ld + C + c];
+    }
+  }
+  for (int c = tid; c < C; c += kWaves * 64) {
+    const float mu = a.stat[((long)b * C + c) * 2], rs = a.stat[((long)b * C + c) * 2 + 1];
+    s_rs[c] = rs;
+    s_nm[c] = -mu * rs;
+  }
+  __syncthreads();
+  if (wid < L) {
+    float k = 0.f;
+    for (int c = lane; c < C; c += 64) k = fmaf(a.wh[wid][c], s_nm[c], k);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) k += __shfl_xor(k, o, 64);
+    if (lane == 0) s_k[wid] = k;
+  }
+  __syncthreads();
+  float bh[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) bh[l] = a.bh[l][0] + s_k[l];
+
+  const bf16* src = UP ? a.hin + (long)b * a.up.H * a.up.W * a.ldh : nullptr;
+  const int ntiles = a.PPW / 16;
+  // this wave's tiles: t = wid + 8 i, i = 0 .. nw-1 (nw even: PPW is a multiple of 256)
+  const int nw = ntiles / kWaves;
+
+  // z fragments of tile t (registers) + its h_in pixels (DMA into slot `slot` of this wave)
+  auto issue = [&](int t, u32x4 (&zc)[KS], unsigned char* slot) {
+    const long p = p_begin + t * 16 + lr;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + ks * 32 + lq * 8);
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned char* dst = slot + wid * SLOT_B;
+    if constexpr (UP) {
+      const int r = (int)(p_begin - (long)b * a.HW) + t * 16;     // first output pixel of the tile
+      const int oy = r / (2 * a.up.W), ox0 = r - oy * (2 * a.up.W);
+      float ry = a.up.sh * (float)oy, rx = a.up.sw * (float)ox0;
+      asm volatile("" : "+v"(ry), "+v"(rx));
+      const int y0 = (int)ry, x_lo = (int)rx;
+      const int y1 = y0 + (y0 < a.up.H - 1 ? 1 : 0);
+#pragma unroll
+      for (int row = 0; row < 2; ++row) {
+        const int sy = row ? y1 : y0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int pl = k * 8 + (lane >> 3), cl = lane & 7;     // LDS pixel / chunk this lane fills
+          if (k == 1 && lane >= 16) continue;                    // 10 pixels per row
+          const int sx = min(x_lo + pl, a.up.W - 1);
+          const bf16* g = src + ((long)sy * a.up.W + sx) * a.ldh + ((cl ^ (pl & 7)) * 8);
+          __builtin_amdgcn_global_load_lds(g, dst + row * SPX * 128 + k * 1024, 16, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int pl = k * 8 + (lane >> 3), cl = lane & 7;
+        const bf16* g = a.hin + (p_begin + t * 16 + pl) * a.ldh + ((cl ^ (pl & 7)) * 8);
+        __builtin_amdgcn_global_load_lds(g, dst + k * 1024, 16, 0, 0);
+      }
+    }
+#endif
+  };
+
+  // phase 1: tile t's h_in chunks out of its LDS slot (through the bilinear x2 when UP)
+  auto hload = [&](int t, const unsigned char* slot, u32x4 (&hc)[2]) {
+    const long p = p_begin + t * 16 + lr;
+    const unsigned char* hs = slot + wid * SLOT_B;
+    if constexpr (UP) {
+      const int r = (int)(p - (long)b * a.HW);
+      const int oy = r / (2 * a.up.W), ox = r - oy * (2 * a.up.W);
+      const int ox0 = ox - lr;
+      float rx0 = a.up.sw * (float)ox0;
+      asm volatile("" : "+v"(rx0));
+      const int x_lo = (int)rx0;
+      const Up2xTap tp = up2x_tap(a.up, oy, ox);
+      // tap offsets o00 = y0*W + x0 etc.: recover the columns relative to the slot's first pixel
+      const int x0 = tp.o00 % a.up.W, x1 = tp.o01 % a.up.W;
+      const int c0 = x0 - x_lo, c1 = x1 - x_lo;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ch = j * 4 + lq;                    // 16-byte chunk of channels 8ch .. 8ch+7
+        auto ld = [&](int row, int col) {
+          return *reinterpret_cast<const u32x4*>(hs + row * SPX * 128 + col * 128 + ((ch ^ (col & 7)) * 16));
+        };
+        // same arithmetic as up2x_load16_f: l0y*(l0x*v00 + l1x*v01) + l1y*(l0x*v10 + l1x*v11)
+        const u32x4 r00 = ld(0, c0), r01 = ld(0, c1), r10 = ld(1, c0), r11 = ld(1, c1);
+        const bf16 *e00 = reinterpret_cast<const bf16*>(&r00), *e01 = reinterpret_cast<const bf16*>(&r01);
+        const bf16 *e10 = reinterpret_cast<const bf16*>(&r10), *e11 = reinterpret_cast<const bf16*>(&r11);
+        bf16* hv = reinterpret_cast<bf16*>(&hc[j]);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          hv[q] = (bf16)(tp.ly0 * (tp.lx0 * (float)e00[q] + tp.lx1 * (float)e01[q]) +
+                         tp.ly1 * (tp.lx0 * (float)e10[q] + tp.lx1 * (float)e11[q]));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ch = j * 4 + lq;
+        hc[j] = *reinterpret_cast<const u32x4*>(hs + lr * 128 + ((ch ^ (lr & 7)) * 16));
+      }
+    }
+  };
+  // phase 2: mask, gamma/beta MFMAs, blend and the stores of tile t
+  auto compute = [&](int t, const u32x4 (&zc)[KS], const u32x4 (&hc)[2]) {
+    const long p = p_begin + t * 16 + lr;
+    float ms[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) ms[l] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c0 = j * 32 + lq * 8;
+      const bf16* hv = reinterpret_cast<const bf16*>(&hc[j]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int l = 0; l < L; ++l) ms[l] = fmaf(s_cf[l * C + c0 + e], (float)hv[e], ms[l]);
+    }
+    float Mk[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      float sm = ms[l];
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      Mk[l] = sigmoidf_ref(sm + bh[l]);
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      asm volatile("" ::: "memory");
+      const bf16* W = s_w + l * 128 * WLD;
+#pragma unroll
+      for (int sh = 0; sh < 2; ++sh) {
+        asm volatile("" ::: "memory");
+        f32x4 acc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
+          acc[i] = *reinterpret_cast<const f32x4*>(&s_b[l * 128 + rt * 16 + lq * 4]);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          bf16x8 bfrag;
+          __builtin_memcpy(&bfrag, &zc[ks], 16);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
+            const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&W[(rt * 16 + lr) * WLD + ks * 32 + lq * 8]);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i], 0, 0, 0);
+          }
+        }
+        const int c0 = sh * 32 + lq * 8;
+        const bf16* hv = reinterpret_cast<const bf16*>(&hc[sh]);
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float hh = fmaf((float)hv[e], s_rs[c0 + e], s_nm[c0 + e]);
+          const float g = acc[e >> 2][e & 3];
+          const float be = acc[2 + (e >> 2)][e & 3];
+          const float A = fmaf(g, hh, be);
+          const float I = fmaf(s_gi[l * C + c0 + e], hh, s_bi[l * C + c0 + e]);
+          const float v = fmaf(Mk[l], I - A, A);
+          o[e] = v > 0.f ? v : v * a.slope;
+        }
+        store16_f(a.out[l] + p * a.ldo[l] + c0, o);
+      }
+    }
+  };
+
+  // loop: read tile t's h_in out of its slot (the wait the compiler puts before that read covers
+  // tile t's DMA and z loads), THEN issue tile t+1 into the other slot, then compute tile t while
+  // those loads are in flight
+  u32x4 zc[KS], zn[KS];
+  issue(wid, zc, s_hA);
+  for (int i = 0; i < nw; ++i) {
+    const int t = wid + i * kWaves;
+    unsigned char* cur = (i & 1) ? s_hB : s_hA;
+    unsigned char* nxt = (i & 1) ? s_hA : s_hB;
+    asm volatile("" ::: "memory");
+    u32x4 hc[2];
+    hload(t, cur, hc);
+    asm volatile("" ::: "memory");
+    if (i + 1 < nw) issue(t + kWaves, zn, nxt);
+    asm volatile("" ::: "memory");
+    compute(t, zc, hc);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) zc[ks] = zn[ks];
+  }
+}
+
 bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo) {
   if (dt != GHOST_BF16) return false;
   const bool shape = (C == 64 && (Ca == 64 || Ca == 32)) || (C == 128 && (Ca == 128 || Ca == 64 || Ca == 32));
@@ -234,6 +475,22 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
     a.up = up2x_src(d.up_H, d.up_W);
   }
   dim3 grid((unsigned)((long)d.B * d.HW / a.PPW));
+  static const int use_v4 = [] {
+    const char* e = getenv("GHOST_AAD_V4");
+    return e ? atoi(e) : 1;
+  }();
+  // v4 (prefetching) only for the through-upsample form: measured B = 64, 256x256 L = 2: 724 vs 734 us
+  // with the upsample, 604 vs 550 us without it (there v3's register loads win)
+  if (use_v4 && up && d.C == 64 && a.PPW % 256 == 0 && d.ldh % 8 == 0) {
+#define GHOST_V4(ca, l, u)                                                                       \
+    if (d.Ca == ca && d.L == l && up == u) {                                                     \
+      hipLaunchKernelGGL((aad_v4_kernel<ca, l, u>), grid, dim3(kWaves * 64), 0, s, a);           \
+      return (int)hipGetLastError();                                                             \
+    }
+    GHOST_V4(64, 1, false) GHOST_V4(64, 2, false) GHOST_V4(32, 1, false) GHOST_V4(32, 2, false)
+    GHOST_V4(64, 1, true) GHOST_V4(64, 2, true) GHOST_V4(32, 1, true) GHOST_V4(32, 2, true)
+#undef GHOST_V4
+  }
 #define GHOST_V3(c, ca, l, u)                                                                   \
   if (d.C == c && d.Ca == ca && d.L == l && up == u) {                                          \
     hipLaunchKernelGGL((aad_v3_kernel<c, ca, l, u>), grid, dim3(kWaves * 64), 0, s, a);         \

@@ -17,6 +17,7 @@
 #include "../../include/ghost_amd.h"
 #include "aad_fused.h"
 #include "aad_v3.h"
+#include "conv_halo.h"
 #include "aad_wide.h"
 #include "conv_igemm.h"
 #include "conv_narrow.h"
@@ -181,6 +182,10 @@ void run_conv(Ctx& c, ConvDesc& d, int cls_all, int cls_big, double flops) {
 }
 
 static int g_fuse_upsample = 1;   // ghost_set_fuse_upsample (testing knob)
+static int g_fuse_stats = [] {     // GHOST_FUSE_STATS=0: statistics by a separate pass (A/B, tests)
+  const char* e = getenv("GHOST_FUSE_STATS");
+  return e ? atoi(e) : 1;
+}();
 
 void run_stats(Ctx& c, const void* x, int ldx, int B, int HW, int C, float* stat) {
   if (!c.ok()) return;
@@ -493,19 +498,20 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
   }
 }
 
-void conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, int B, int n, int Cout, void* y,
-             int ldy, const void* res, int ldres, int tanh_out, uint8_t* u8) {
+// returns true when `stat` (if given) was produced from partials written by the conv itself
+bool conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, int B, int n, int Cout, void* y,
+             int ldy, const void* res, int ldres, int tanh_out, uint8_t* u8, float* stat = nullptr) {
   const double flops = 2.0 * B * n * n * Cout * 9.0 * Cin;
   if (Cout <= 3 && conv3x3_narrow_supported(c.h->dt, n, n, Cin, ldx, Cout)) {
     const void* wn = c.W(wname + "n");   // "...conv{i}.w" + "n" = the narrow layout slot
-    if (!c.ok() || c.dry) return;
+    if (!c.ok() || c.dry) return false;
     int e_all = c.prof_begin(2);
     int e_big = n == 256 ? c.prof_begin(3) : -1;
     c.check(conv3x3_narrow(c.h->dt, x, B, n, n, Cin, ldx, wn, rup(Cin, 32), Cout, res, ldres, tanh_out, y, ldy, u8, c.s),
             "conv3x3_narrow");
     if (e_big >= 0) c.prof_end(3, e_big, 0, flops);
     if (e_all >= 0) c.prof_end(2, e_all, 0, flops);
-    return;
+    return false;
   }
   ConvDesc d;
   d.ti = d.to = c.h->dt;
@@ -516,7 +522,16 @@ void conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, 
   d.y = y; d.ldy = ldy;
   d.res = res; d.ldres = ldres;
   d.tanh_out = tanh_out; d.u8 = u8;
+  int nrec = 0;
+  const bool fused = stat && g_fuse_stats && conv3x3_pp_takes(d, &nrec);
+  if (fused) d.in_part = (float*)c.alloc((size_t)B * nrec * Cout * 2 * sizeof(float));
   run_conv(c, d, 2, 3, flops);
+  if (fused && c.ok() && !c.dry) {
+    int e = c.prof_begin(4);
+    c.check(in_stats_from_tiles(d.in_part, B, nrec, Cout, stat, c.s), "in_stats_from_tiles");
+    c.prof_end(4, e, 0, 0);
+  }
+  return fused;
 }
 
 void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, void* y_out, uint8_t* u8) {
@@ -581,9 +596,11 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
       aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb, i == 0 && m_virtual);
       if (!last) {
         void* xn = c.alloc(P * cin * es);
-        conv3x3(c, cn, a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr);
         float* st = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
-        run_stats(c, xn, cin, B, n * n, cin, st);
+        // the persistent conv writes the InstanceNorm partials of its output in its epilogue
+        // (one pass less over xn); other conv kernels: a separate statistics pass
+        if (!conv3x3(c, cn, a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr, st))
+          run_stats(c, xn, cin, B, n * n, cin, st);
         x = xn;
         stat_x = st;
       } else if (!split) {
@@ -893,6 +910,11 @@ extern "C" int ghost_aei_profile_read(ghost_aei* h, int cls, double* ms, int64_t
 // ---------------------------------------------------------------------------
 // C ABI: single operators
 // ---------------------------------------------------------------------------
+extern "C" int ghost_set_fuse_stats(int on) {
+  g_fuse_stats = on ? 1 : 0;
+  return 0;
+}
+
 extern "C" int ghost_set_fuse_upsample(int on) {
   g_fuse_upsample = on ? 1 : 0;
   return 0;

@@ -9,6 +9,9 @@ namespace ghost {
 // true when conv3x3_halo takes this descriptor (3x3/s1/p1, bf16, standard epilogue without the
 // uint8 copy, H % 16 == 0, W % 32 == 0, K ordered (channel block, tap, channel) as pack.py packs it)
 bool conv3x3_halo_supported(const ConvDesc& d);
+// true when conv3x3_halo runs the persistent kernel for d, which can also emit InstanceNorm
+// partials of its output (d.in_part): count of partial records per (sample, channel) in *nrec
+bool conv3x3_pp_takes(const ConvDesc& d, int* nrec);
 int conv3x3_halo(const ConvDesc& d, hipStream_t s);
 
 // ConvTranspose2d 4x4/s2/p1 on 8 x 16 input tiles (bf16, Cin % 32 == 0, N % 64 == 0 or N == 32,

@@ -13,6 +13,7 @@
 // 8 waves, each 2 output rows (64 pixels) x 64 channels; 75 KB LDS -> two workgroups per CU,
 // which overlap one workgroup's DMA with the other's MFMAs.
 #include <cstdlib>
+#include <type_traits>
 
 #include "conv_halo.h"
 #include "ghost_common.h"
@@ -48,6 +49,7 @@ struct HaloArgs {
   float slope;
   int tiles_x, tiles_y, nNt, ntiles;
   int dbg;   // experiment mask (GHOST_HALO_DBG): 2 no halo DMA, 4 no weight DMA, 8 no MFMA
+  float* in_part;   // pp kernel: InstanceNorm partials [B][tiles/sample][8 waves][N][2] or null
 };
 
 __device__ __attribute__((aligned(16))) unsigned int g_halo_zero[64] = {0};
@@ -210,7 +212,7 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
 // (cdna_hip_programming.md, glds notes).  Scale/shift live in LDS so the epilogue issues no
 // ordinary global load while a DMA is outstanding (hipcc would wait vmcnt(0) for its result).
 // ---------------------------------------------------------------------------
-template <bool RESW>
+template <bool RESW, bool STATS>
 __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) {
   // RESW: Cin <= 64 and N == 64 — the whole weight tensor (<= 2 blocks x 36 KB) stays resident in
   // LDS for the kernel and only the halo (39 KB) streams per stage; otherwise every stage carries
@@ -261,7 +263,6 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
   const int G_ = gridDim.x;
   const int xt = xcd_tile(blockIdx.x, G_);
   const int nmine = a.ntiles > xt ? (a.ntiles - xt + G_ - 1) / G_ : 0;
-  const int nst = nmine * ncb;
 
   // tile of this WG's k-th item, and this lane's halo DMA sources for it (element offsets from the
   // sample base; bit j of ok = piece j inside the image)
@@ -305,7 +306,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
 #pragma unroll
     for (int j = 0; j < HPW; ++j) {
       const int piece = wid + j * NW;
-      if (piece < HPIECES && !(a.dbg & 2)) {
+      if (piece < HPIECES) {
         const void* src = ((h_ok >> j) & 1u) ? (const void*)(xs + h_off[j]) : (const void*)g_halo_zero;
         __builtin_amdgcn_global_load_lds(src, buf + piece * 1024, 16, 0, 0);
       }
@@ -315,7 +316,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
 #pragma unroll
       for (int j = 0; j < WPW; ++j) {
         const int piece = wid + j * NW;
-        if (piece < WPIECES && !(a.dbg & 4))
+        if (piece < WPIECES)
           __builtin_amdgcn_global_load_lds(ws + w_off[j], buf + HALO_B + piece * 1024, 16, 0, 0);
       }
     }
@@ -328,23 +329,20 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Stage order: tile k = 0..nmine-1, channel blocks cb = 0..ncb-1 (ncb even): even blocks read
-  // lds0 and prefetch into lds1, odd blocks the reverse, so every wait below is static:
-  //   first block of a tile  -> vmcnt(16): the previous tile's 16 epilogue stores are the youngest
-  //   other blocks           -> vmcnt(0)
-  // and the compiler's own waitcnt pass sees the same program order (no drain of the prefetch).
+  // Stage order: tile k = 0..nmine-1, channel blocks cb = 0..ncb-1 (ncb even), so even stages read
+  // lds0 and prefetch into lds1 and odd stages the reverse: the loop body holds the two steps with
+  // their buffers fixed, and every wait is the same static vmcnt(0) (it also retires the previous
+  // tile's epilogue stores), which the compiler's waitcnt pass sees — it then puts no drain of the
+  // prefetch in front of the reads of the other buffer.
   if (nmine == 0) return;
   Tile cur = tile_of(0);
   set_dma_tile(cur);
   issue(lds0, 0);
-  __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0): DMA(0) (nothing to overlap it with yet)
   int nk = 0, ncb_next = 1;                 // (tile, block) of the next DMA
-  auto step = [&](bool first, int cb, const unsigned char* buf, unsigned char* nbuf) {
-    // gfx9 simm16: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] at [15:14]
-    if (first)
-      __builtin_amdgcn_s_waitcnt(0x4F70);   // vmcnt(16)
-    else
-      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+  if (ncb == 1) { ncb_next = 0; nk = 1; }
+  int k = 0, cb = 0;                        // (tile, block) being computed
+  auto step = [&](const unsigned char* buf, unsigned char* nbuf) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0)   (gfx9 simm16: vm[3:0] exp[6:4] lgkm[11:8] vm[5:4]@[15:14])
     __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
     if (nk < nmine) {
@@ -355,7 +353,6 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
     const unsigned char* wb = RESW ? wres + cb * WBLK_B : buf + HALO_B;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      if (a.dbg & 8) break;
       asm volatile("" ::: "memory");
       const int dy = tap / 3, dx = tap - dy * 3;
       bf16x8 wf[4], pf[4];
@@ -374,16 +371,12 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], pf[i], acc[j][i], 0, 0, 0);
     }
-  };
-  if (ncb == 1) { ncb_next = 0; nk = 1; }
-  for (int k = 0; k < nmine; ++k) {
-    step(true, 0, lds0, lds1);
-    step(false, 1, lds1, lds0);
-    for (int cb = 2; cb < ncb; cb += 2) {
-      step(false, cb, lds0, lds1);
-      step(false, cb + 1, lds1, lds0);
+    if (cb + 1 < ncb) {
+      ++cb;
+      return;
     }
-    // epilogue: exactly 16 vector stores per wave (N % 64 == 0, full tiles), the youngest VM ops
+    // epilogue: exactly 16 vector stores per wave (N % 64 == 0, full tiles) + 1 with STATS, the
+    // youngest VM ops when the next tile's first stage waits
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int oy = cur.y0 + wid * RPW + (i * 16) / TW, ox = cur.x0 + (i * 16) % TW + lr;
@@ -407,12 +400,90 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
           v += rv[r];
           if (a.tanh_out) v = tanhf(v);
           oe[r] = (bf16)v;
-          acc[j][i][r] = 0.f;
+          acc[j][i][r] = STATS ? (float)oe[r] : 0.f;   // the stored (rounded) value, for the statistics
         }
         *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
       }
     }
-    if (k + 1 < nmine) cur = tile_of(k + 1);
+    if constexpr (STATS) {
+      // InstanceNorm partials of this wave's 64 pixels (AADLayer.py:16,24 reads this tensor next):
+      // per channel the mean and the centred sum of squares of the stored (bf16-rounded) values,
+      // two passes over registers; in_stats_from_tiles merges them in fp64 (Chan).  The 16 channel
+      // sums of a lane are reduced over the 16 lanes of its row by a transpose-reduce (8+4+2+1 DPP
+      // exchanges) that leaves channel k = lr in lane lr; the mean goes back by the reverse.
+      // S1 first, then S2 (one 16-value set live at a time)
+      // partner lanes by DPP within the 16-lane row: row_mirror (i ^ 15), row_half_mirror (i ^ 7),
+      // quad_perm [2,3,0,1] (i ^ 2), quad_perm [1,0,3,2] (i ^ 1); round m keeps the half of the
+      // values selected by lane bit m, so lane lr ends with the full row sum of value index lr
+      auto round = [&](float (&v)[16], auto mtag, auto ctl) {
+        constexpr int m = decltype(mtag)::value;
+        const bool hi = (lr & m) != 0;
+#pragma unroll
+        for (int q = 0; q < m; ++q) {
+          const float keep = hi ? v[q + m] : v[q], send = hi ? v[q] : v[q + m];
+          const int got = __builtin_amdgcn_update_dpp(0, __float_as_int(send), decltype(ctl)::value, 0xF, 0xF, false);
+          v[q] = keep + __int_as_float(got);
+        }
+      };
+      auto reduce16 = [&](float (&v)[16]) {
+        round(v, std::integral_constant<int, 8>{}, std::integral_constant<int, 0x140>{});
+        round(v, std::integral_constant<int, 4>{}, std::integral_constant<int, 0x141>{});
+        round(v, std::integral_constant<int, 2>{}, std::integral_constant<int, 0x4E>{});
+        round(v, std::integral_constant<int, 1>{}, std::integral_constant<int, 0xB1>{});
+        return v[0];
+      };
+      // the reverse butterfly: lane lr's value (index lr) to all 16 lanes of its row
+      auto bround = [&](float (&w)[16], auto mtag, auto ctl) {
+        constexpr int m = decltype(mtag)::value;
+        const int own = lr & m;                       // 0 or m: where this lane's current block goes
+#pragma unroll
+        for (int q = 0; q < m; ++q) {
+          const int got = __builtin_amdgcn_update_dpp(0, __float_as_int(w[q]), decltype(ctl)::value, 0xF, 0xF, false);
+          const float mine = w[q];
+          w[q] = own ? __int_as_float(got) : mine;    // block of index bit m = 0
+          w[q + m] = own ? mine : __int_as_float(got);
+        }
+      };
+      float v1[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v1[j * 4 + r] = acc[j][0][r] + acc[j][1][r] + acc[j][2][r] + acc[j][3][r];
+      const float mean = reduce16(v1) * (1.f / 64.f);   // channel lr of the row, over 64 pixels
+      v1[0] = mean;
+      bround(v1, std::integral_constant<int, 1>{}, std::integral_constant<int, 0xB1>{});
+      bround(v1, std::integral_constant<int, 2>{}, std::integral_constant<int, 0x4E>{});
+      bround(v1, std::integral_constant<int, 4>{}, std::integral_constant<int, 0x141>{});
+      bround(v1, std::integral_constant<int, 8>{}, std::integral_constant<int, 0x140>{});
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float s2 = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float d = acc[j][i][r] - v1[j * 4 + r];
+            s2 = fmaf(d, d, s2);
+            acc[j][i][r] = 0.f;
+          }
+          v1[j * 4 + r] = s2;
+        }
+      const float S1 = mean;            // record = (mean, centred sum of squares) of 64 pixels
+      const float S2 = reduce16(v1);
+      // lane (lr, lq) holds channel n0 + 16 (lr >> 2) + 4 lq + (lr & 3)
+      const int tile = (cur.y0 / G::TH) * a.tiles_x + cur.x0 / TW;
+      const long b = cur.base / ((long)a.H * a.W);
+      const int c = cur.n0 + (lr >> 2) * 16 + lq * 4 + (lr & 3);
+      float* dst = a.in_part + ((((b * a.tiles_x * a.tiles_y) + tile) * 8 + wid) * (long)a.N + c) * 2;
+      *reinterpret_cast<float2*>(dst) = make_float2(S1, S2);
+    }
+    cb = 0;
+    if (++k < nmine) cur = tile_of(k);
+  };
+  const int nst = nmine * ncb;               // even
+  for (int st = 0; st < nst; st += 2) {
+    step(lds0, lds1);
+    step(lds1, lds0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -664,23 +735,38 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   }();
   a.dbg = dbg;
   const int g = a.ntiles < num_cus() ? a.ntiles : num_cus();
-  if (d.Cin <= 64 && d.N == 64)
-    hipLaunchKernelGGL(conv3x3_halo_pp_kernel<true>, dim3((unsigned)g), dim3(512), 0, s, a);
+  a.in_part = d.in_part;
+  const bool resw = d.Cin <= 64 && d.N == 64;
+  if (resw && a.in_part)
+    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<true, true>), dim3((unsigned)g), dim3(512), 0, s, a);
+  else if (resw)
+    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<true, false>), dim3((unsigned)g), dim3(512), 0, s, a);
+  else if (a.in_part)
+    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<false, true>), dim3((unsigned)g), dim3(512), 0, s, a);
   else
-    hipLaunchKernelGGL(conv3x3_halo_pp_kernel<false>, dim3((unsigned)g), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<false, false>), dim3((unsigned)g), dim3(512), 0, s, a);
   return (int)hipGetLastError();
 }
 
-int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
-  if (!conv3x3_halo_supported(d)) return -1;
+bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
   static const int pp = [] {
     const char* e = getenv("GHOST_HALO_PP");
     return e ? atoi(e) : 1;
   }();
+  if (!conv3x3_halo_supported(d)) return false;
   const bool wide = d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0;
   // measured A/B (B = 64): the persistent form wins up to Cin = 256 (256x256: -23 %, 128x128: -7 %,
   // 64x64 256->256: -9 %); at Cin >= 512 the per-stage barrier costs more than the prefetch saves
-  if (wide && pp && d.N <= 512 && d.Cin % 64 == 0 && d.Cin <= 256) return halo_pp_launch(d, s);
+  const bool ok = wide && pp && d.N <= 512 && d.Cin % 64 == 0 && d.Cin <= 256 && !d.tanh_out;
+  if (ok && nrec) *nrec = (d.Hi / HaloWide::TH) * (d.Wi / HaloWide::TW) * 8;
+  return ok;
+}
+
+int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
+  if (!conv3x3_halo_supported(d)) return -1;
+  const bool wide = d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0;
+  if (conv3x3_pp_takes(d, nullptr)) return halo_pp_launch(d, s);
+  if (d.in_part) return -1;   // only the persistent kernel writes InstanceNorm partials
   if (wide) return halo_launch<HaloWide>(d, s);
   return halo_launch<HaloSmall>(d, s);
 }

@@ -55,6 +55,10 @@ struct ConvDesc {
   int C_aad = 0;
   int force_split = 0;                       // >0: override the split-K heuristic (tests)
   int min_wgs = 0;                           // split K while the grid has fewer tiles (0 = 256)
+  // optional InstanceNorm partials of the (bf16-rounded) output, written by the kernels that support
+  // it (conv3x3_pp_takes): per (sample, tile, wave, channel) the mean and centred sum of squares of
+  // 64 pixels; in_stats_from_tiles() merges them in fp64 into [B][C][2] mean / rstd
+  float* in_part = nullptr;
 };
 
 // bytes of fp32 split-K workspace the launch may use

@@ -17,6 +17,11 @@ int in_stats(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, 
 int in_stats_up2x(int dt, const void* x, int ldx, int B, int H, int W, int C, float* stat, void* ws, size_t ws_bytes,
                   hipStream_t s);
 
+// statistics from the per-(tile, wave) partials a producer kernel wrote (ConvDesc::in_part): nrec
+// records of (mean, centred sum of squares) over 64 pixels per (sample, channel), merged in fp64 (Chan)
+// -> stat = [B][C][2] mean, rstd
+int in_stats_from_tiles(const float* part, int B, int nrec, int C, float* stat, hipStream_t s);
+
 // AAD mask: M[p] = sigmoid(sum_c wh[c] * (h[p,c]-mu[b,c])*rstd[b,c] + bh)   (AADLayer.py:35)
 int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh,
              const float* bh, float* mask, hipStream_t s);

@@ -161,6 +161,9 @@ int ghost_set_split_k(int n);
 /* testing knob: 1 (default) lets the generator sample the upsample of AADBlk7's output inside
  * AADBlk8's first AADLayer pair instead of materialising it; 0 materialises it */
 int ghost_set_fuse_upsample(int on);
+/* testing knob: 1 (default) lets the persistent 3x3 conv emit the InstanceNorm partials of its
+ * output (no separate statistics pass); 0 computes them by a separate pass */
+int ghost_set_fuse_stats(int on);
 
 /* ---- ArcFace identity encoder (IResNet, the netArc GHOST loads) ------------------------
  * Replaces: inference.py:33-36 iresnet100(fp16=False) + load_state_dict + .cuda().eval();
