@@ -9,7 +9,7 @@ then (N > 1) an RCCL all-gather of every rank's swapped crops (frame order = ran
 Weak scaling: B frames per GPU; value = N*B*K / max-over-ranks wall time of the K timed steps.
 
 Besides the JSON line's throughput, it reports
-* roofline: the dominant AAD kernel, aad_v3_kernel<64,64,2,true> (the two AADLayers of AADBlk8 that
+* roofline: the dominant AAD kernel, aad_v4_kernel<64,2,true> (the two AADLayers of AADBlk8 that
   read the same h_in / z_attr at 256x256, h_in sampled through the bilinear x2 upsample of AADBlk7's
   128x128 output), HBM-bound: its algorithmic bytes per launch by SURVEY.md §8d's formula (fixed
   regardless of fusion: sum over its two AADLayers of |h_in| + |z_attr| + |out|, 64 frames at
@@ -227,10 +227,10 @@ def main():
             per_launch_s = c["ms"] / c["launches"] / 1e3
             ach = per_launch_bytes / per_launch_s / 1e9
             ca8 = 32 if a.backbone == "linknet" else 64     # z_attr8 channels (AEI_Net.py:110,118)
-            kname = f"aad_v3_kernel<64, {ca8}, 2, true>"
+            kname = f"aad_v4_kernel<{ca8}, 2, true>"
             res["roofline"] = {"kernel": f"{kname}: two AADLayers sharing h_in/z_attr at 256x256, h_in = bilinear "
                                          "x2 of the 128x128 block output sampled in-kernel (IN-normalise, sigmoid "
-                                         "mask, MFMA gamma/beta, blend, ReLU)",
+                                         "mask, MFMA gamma/beta, blend, ReLU), next tile's z_attr/h_in in flight",
                                "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kname),
                                "bytes_note": "achieved counts SURVEY.md 8d bytes (|h_in|+|z_attr|+|out| per AADLayer, "
