@@ -227,10 +227,14 @@ def main():
             per_launch_s = c["ms"] / c["launches"] / 1e3
             ach = per_launch_bytes / per_launch_s / 1e9
             ca8 = 32 if a.backbone == "linknet" else 64     # z_attr8 channels (AEI_Net.py:110,118)
-            kname = f"aad_v4_kernel<{ca8}, 2, true>"
-            res["roofline"] = {"kernel": f"{kname}: two AADLayers sharing h_in/z_attr at 256x256, h_in = bilinear "
-                                         "x2 of the 128x128 block output sampled in-kernel (IN-normalise, sigmoid "
-                                         "mask, MFMA gamma/beta, blend, ReLU), next tile's z_attr/h_in in flight",
+            # layers in the kernel: the formula bytes per launch are L * B*256^2*(2*64 + Ca)*2
+            nl = max(1, round(per_launch_bytes / (B * 65536 * (2 * 64 + ca8) * 2)))
+            kname = f"aad_v4_kernel<{ca8}, {nl}, true>"
+            what = ("two AADLayers sharing h_in/z_attr" if nl == 2 else
+                    "the first AADLayer (its last_add_block partner runs in the fused tail)")
+            res["roofline"] = {"kernel": f"{kname}: AADBlk8's block-input AAD kernel at 256x256, {what}, h_in = "
+                                         "bilinear x2 of the 128x128 block output sampled in-kernel (IN-normalise, "
+                                         "sigmoid mask, MFMA gamma/beta, blend, ReLU), next tile in flight",
                                "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kname),
                                "bytes_note": "achieved counts SURVEY.md 8d bytes (|h_in|+|z_attr|+|out| per AADLayer, "

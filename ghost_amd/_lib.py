@@ -69,6 +69,7 @@ _SIGS = {
     "ghost_set_fuse_upsample": (i32, [i32]),
 
     "ghost_set_fuse_stats": (i32, [i32]),
+    "ghost_set_fuse_tail": (i32, [i32]),
     "ghost_aad_layers_v3_nhwc": (i32, [vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp), C.POINTER(vp),
                                        C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), i32, f32, C.POINTER(vp),
                                        C.POINTER(i32), vp, i64, vp]),

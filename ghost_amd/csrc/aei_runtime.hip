@@ -17,6 +17,7 @@
 #include "../../include/ghost_amd.h"
 #include "aad_fused.h"
 #include "aad_v3.h"
+#include "aad_tail.h"
 #include "conv_halo.h"
 #include "aad_wide.h"
 #include "conv_igemm.h"
@@ -182,6 +183,13 @@ void run_conv(Ctx& c, ConvDesc& d, int cls_all, int cls_big, double flops) {
 }
 
 static int g_fuse_upsample = 1;   // ghost_set_fuse_upsample (testing knob)
+// GHOST_FUSE_TAIL=1: AADBlk8's tail as one kernel (aad_tail.hip).  Off by default: measured B = 64 it
+// saves 2 GB of HBM traffic but runs latency-bound at one 8-wave workgroup per CU (793 us against the
+// 586 us of the dual-layer AAD's second layer + separate AAD + narrow conv it replaces): +0.6 % only
+static int g_fuse_tail = [] {
+  const char* e = getenv("GHOST_FUSE_TAIL");
+  return e ? atoi(e) : 0;
+}();
 static int g_fuse_stats = [] {     // GHOST_FUSE_STATS=0: statistics by a separate pass (A/B, tests)
   const char* e = getenv("GHOST_FUSE_STATS");
   return e ? atoi(e) : 1;
@@ -491,7 +499,8 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     const double bytes = Pn * (double)d.L * (2.0 * C + Ca) * h->esz;
     const double flops = 2.0 * Pn * 2.0 * C * Ca * d.L;
     int e_all = c.prof_begin(0);
-    int e_big = (n == 256 && d.L == 2) ? c.prof_begin(1) : -1;   // class 1: the dual-layer kernel at 256x256
+    // class 1: the block-input AAD kernel at 256x256 (reads h_in through the x2 upsample; one or two layers)
+    int e_big = (n == 256 && up_src) ? c.prof_begin(1) : -1;
     c.check(aad_v3(d, c.s), "aad_v3");
     if (e_big >= 0) c.prof_end(1, e_big, bytes, flops);
     if (e_all >= 0) c.prof_end(0, e_all, bytes, flops);
@@ -580,18 +589,51 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     else
       run_stats(c, m, cin, B, n * n, cin, stat_m);
     void* y = last_k ? y_out : c.alloc(P * cout * es);
+    // AADBlk8 (-> RGB): its last add_blocks AADLayer, the last_add_block AADLayer and the fused
+    // 128 -> 3 output conv run as one kernel (aad_tail.hip): the two 64-channel AADLayer outputs
+    // never reach HBM
+    const bool tail = last_k && split && g_fuse_tail && h->dt == GHOST_BF16 && cin == 64 && cout <= 3 &&
+                      aad_tail_supported(h->dt, n, n, Ca, Ca, cin, cin);
     // x-branch and h'-branch share the output conv: conv(cat(a_x, a_h), [W_x | W_h]) = x + h'
-    void* cat = split ? c.alloc(P * 2 * cin * es) : nullptr;
+    void* cat = (split && !tail) ? c.alloc(P * 2 * cin * es) : nullptr;
     const void* x = m;
     const float* stat_x = stat_m;
     for (int i = 0; i < nb; ++i) {
       const bool last = i == nb - 1;
       const std::string cn = blk + ".conv" + std::to_string(i) + ".w";
+      if (last && tail) {
+        AadTailDesc d;
+        d.za = za; d.lda = Ca; d.Ca = Ca;
+        const std::string ln[2] = {blk + ".aad" + std::to_string(i), blk + ".aadlast"};
+        const int off[2] = {base + 2 * cin * i, base + 2 * cin * nb};
+        const void* hin[2] = {x, m};
+        const float* st[2] = {stat_x, stat_m};
+        const bool up[2] = {i == 0 && m_virtual, m_virtual};
+        for (int l = 0; l < 2; ++l) {
+          d.hin[l] = hin[l]; d.ldh[l] = cin; d.stat[l] = st[l];
+          if (up[l]) { d.up_H[l] = n / 2; d.up_W[l] = n / 2; }
+          d.w3[l] = c.W(ln[l] + ".w3");
+          d.b3[l] = (const float*)c.W(ln[l] + ".b3");
+          d.wh[l] = (const float*)c.W(ln[l] + ".wh");
+          d.bh[l] = (const float*)c.W(ln[l] + ".bh");
+          d.idgb[l] = idgb ? idgb + off[l] : nullptr;
+        }
+        d.id_ld = h->id_total;
+        d.wn = c.W(cn + "n");
+        d.y = y; d.u8 = u8; d.B = B; d.H = n; d.W = n; d.tanh_out = 1;
+        if (c.ok() && !c.dry) {
+          const double Pn = (double)B * n * n;
+          int e_all = c.prof_begin(0);
+          c.check(aad_tail(d, c.s), "aad_tail");
+          if (e_all >= 0) c.prof_end(0, e_all, Pn * 2.0 * (2.0 * cin + Ca) * es, 2.0 * Pn * 2.0 * 2.0 * cin * Ca);
+        }
+        break;
+      }
       std::vector<AadOut> group;
       void* a = (last && split) ? cat : c.alloc(P * cin * es);
       const int lda_out = (last && split) ? 2 * cin : cin;
       group.push_back({blk + ".aad" + std::to_string(i), base + 2 * cin * i, a, lda_out});
-      if (i == 0 && split)   // last_add_block's AADLayer reads the block input m as well
+      if (i == 0 && split && !tail)   // last_add_block's AADLayer reads the block input m as well
         group.push_back({blk + ".aadlast", base + 2 * cin * nb, (char*)cat + (size_t)cin * es, 2 * cin});
       aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb, i == 0 && m_virtual);
       if (!last) {
@@ -910,6 +952,11 @@ extern "C" int ghost_aei_profile_read(ghost_aei* h, int cls, double* ms, int64_t
 // ---------------------------------------------------------------------------
 // C ABI: single operators
 // ---------------------------------------------------------------------------
+extern "C" int ghost_set_fuse_tail(int on) {
+  g_fuse_tail = on ? 1 : 0;
+  return 0;
+}
+
 extern "C" int ghost_set_fuse_stats(int on) {
   g_fuse_stats = on ? 1 : 0;
   return 0;

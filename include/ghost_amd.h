@@ -78,8 +78,8 @@ int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_str
                       void* stream);
 
 /* per-kernel-class device timing with HIP events (bench instrumentation).
- * class_mask bit i enables class i; classes: 0 AAD kernels (all stages), 1 the dual-layer AAD
- * kernel at 256x256 (aad_v3<64,64,2>), 2 conv3x3 (all), 3 conv3x3 at 256x256, 4 IN stats + mask,
+ * class_mask bit i enables class i; classes: 0 AAD kernels (all stages), 1 the block-input AAD
+ * kernel at 256x256 (through-upsample, aad_v4), 2 conv3x3 (all), 3 conv3x3 at 256x256, 4 IN stats + mask,
  * 5 encoder, 6 upsample, 7 identity projections. */
 int ghost_aei_profile(ghost_aei* h, int class_mask);
 /* after the stream is synchronised: total ms, launches, algorithmic bytes and flops of class i */
@@ -164,6 +164,9 @@ int ghost_set_fuse_upsample(int on);
 /* testing knob: 1 (default) lets the persistent 3x3 conv emit the InstanceNorm partials of its
  * output (no separate statistics pass); 0 computes them by a separate pass */
 int ghost_set_fuse_stats(int on);
+/* experimental knob: 1 runs AADBlk8's last AADLayers + output conv as one kernel (aad_tail.hip);
+ * 0 (default) runs them as separate kernels */
+int ghost_set_fuse_tail(int on);
 
 /* ---- ArcFace identity encoder (IResNet, the netArc GHOST loads) ------------------------
  * Replaces: inference.py:33-36 iresnet100(fp16=False) + load_state_dict + .cuda().eval();

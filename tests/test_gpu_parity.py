@@ -437,6 +437,29 @@ def test_bf16_fused_conv_statistics_match_separate_pass(lib, backbone, nb):
     assert d01 <= 0.5 * d0r, (d01, d0r)
 
 
+@pytest.mark.parametrize("backbone,nb,B", [("unet", 2, 4), ("linknet", 3, 2), ("unet", 1, 2)])
+def test_bf16_fused_tail_matches_separate_kernels(lib, backbone, nb, B):
+    """AADBlk8's last AADLayers + output conv in one kernel (aad_tail.hip) vs the separate AAD
+    kernels and the narrow conv: same arithmetic, so only bf16 rounding flips may differ."""
+    G = model(backbone, nb, compute_dtype=torch.bfloat16)
+    xt, z = aei_ref.make_inputs(B, 13)
+    crops = torch.from_numpy(aei_ref.make_u8_crops(B, 3)).to(DEV)
+    _lib_mod().check(lib.ghost_set_fuse_tail(0))
+    Y0, _ = G(xt.to(DEV), z.to(DEV))
+    Y0 = Y0.float().cpu()
+    U0 = G.swap_u8(crops, z[:1].to(DEV)).cpu().numpy()
+    try:
+        _lib_mod().check(lib.ghost_set_fuse_tail(1))
+        Y1, _ = G(xt.to(DEV), z.to(DEV))
+        U1 = G.swap_u8(crops, z[:1].to(DEV)).cpu().numpy()
+    finally:
+        lib.ghost_set_fuse_tail(0)   # the default
+    d = (Y1.float().cpu() - Y0).abs()
+    assert float(d.mean()) <= 2e-3 and float(d.max()) <= 0.1, (float(d.mean()), float(d.max()))
+    du = np.abs(U1.astype(np.int16) - U0.astype(np.int16))
+    assert du.mean() <= 0.5 and du.max() <= 16, (du.mean(), du.max())
+
+
 def _lib_mod():
     from ghost_amd import _lib
     return _lib
