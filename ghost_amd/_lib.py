@@ -60,6 +60,7 @@ _SIGS = {
                                              i32, vp, i32, vp, i64, vp]),
     "ghost_linear_f32": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, i32, vp, i64, vp]),
     "ghost_instnorm_stats_nhwc": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, i64, vp]),
+    "ghost_instnorm_stats_up2x_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, i64, vp]),
     "ghost_aad_layer_nhwc": (i32, [i32, vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp, vp, vp, vp,
                                    i32, f32, vp, i32, vp, i64, vp]),
     "ghost_upsample2x_nhwc": (i32, [i32, vp, i32, vp, i32, i32, i32, i32, i32, vp]),
@@ -67,6 +68,7 @@ _SIGS = {
     "ghost_crops_to_input_nhwc": (i32, [vp, i64, i32, i32, i32, i32, vp, vp]),
     "ghost_set_split_k": (i32, [i32]),
     "ghost_set_fuse_upsample": (i32, [i32]),
+    "ghost_set_fuse_zup": (i32, [i32]),
 
     "ghost_set_fuse_stats": (i32, [i32]),
     "ghost_set_fuse_tail": (i32, [i32]),

@@ -212,8 +212,11 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
 // (cdna_hip_programming.md, glds notes).  Scale/shift live in LDS so the epilogue issues no
 // ordinary global load while a DMA is outstanding (hipcc would wait vmcnt(0) for its result).
 // ---------------------------------------------------------------------------
-template <bool RESW, bool STATS>
+template <bool RESW, bool STATS, int NCB, int DBG = 0>
 __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) {
+  static_assert(NCB % 2 == 0 && NCB <= 8 && (!RESW || NCB == 2), "channel blocks per tile");
+  // DBG (experiments only, GHOST_HALO_DBG): 2 no halo DMA, 4 no weight DMA, 8 no LDS reads/MFMA,
+  // 16 no output stores
   // RESW: Cin <= 64 and N == 64 — the whole weight tensor (<= 2 blocks x 36 KB) stays resident in
   // LDS for the kernel and only the halo (39 KB) streams per stage; otherwise every stage carries
   // its channel block's 9 x 64 weight rows too (75 KB).
@@ -236,7 +239,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
     s_sc[n] = a.scale ? a.scale[n] : 1.f;
     s_sh[n] = a.shift ? a.shift[n] : 0.f;
   }
-  const int ncb = a.Cin / 32;
+  constexpr int ncb = NCB;
   // per-lane weight source offsets within a channel block (tap, row) — independent of the tile
   int w_off[WPW];
 #pragma unroll
@@ -306,12 +309,12 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
 #pragma unroll
     for (int j = 0; j < HPW; ++j) {
       const int piece = wid + j * NW;
-      if (piece < HPIECES) {
+      if (piece < HPIECES && !(DBG & 2)) {
         const void* src = ((h_ok >> j) & 1u) ? (const void*)(xs + h_off[j]) : (const void*)g_halo_zero;
         __builtin_amdgcn_global_load_lds(src, buf + piece * 1024, 16, 0, 0);
       }
     }
-    if constexpr (!RESW) {
+    if constexpr (!RESW && !(DBG & 4)) {
       const bf16* __restrict__ ws = a.w + (long)dma_n0 * a.Kpad + cb * 288;
 #pragma unroll
       for (int j = 0; j < WPW; ++j) {
@@ -329,54 +332,92 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Stage order: tile k = 0..nmine-1, channel blocks cb = 0..ncb-1 (ncb even), so even stages read
-  // lds0 and prefetch into lds1 and odd stages the reverse: the loop body holds the two steps with
-  // their buffers fixed, and every wait is the same static vmcnt(0) (it also retires the previous
-  // tile's epilogue stores), which the compiler's waitcnt pass sees — it then puts no drain of the
-  // prefetch in front of the reads of the other buffer.
+  // Stage order: tile k = 0..nmine-1, channel blocks cb = 0..NCB-1 (NCB even, unrolled), so a tile's
+  // even stages read lds0 and prefetch into lds1 and its odd stages the reverse, with every wait
+  // static.  The first stage of a tile waits vmcnt(NST): the previous tile's NST epilogue stores are
+  // the wave's youngest VM ops (VM ops retire in issue order), so the wait covers this stage's DMA
+  // without waiting for the stores to reach memory; the later stages wait vmcnt(0).
+  constexpr int NST = (DBG & 16) ? 0 : 16 + (STATS ? 1 : 0);
   if (nmine == 0) return;
   Tile cur = tile_of(0);
   set_dma_tile(cur);
   issue(lds0, 0);
-  int nk = 0, ncb_next = 1;                 // (tile, block) of the next DMA
-  if (ncb == 1) { ncb_next = 0; nk = 1; }
-  int k = 0, cb = 0;                        // (tile, block) being computed
-  auto step = [&](const unsigned char* buf, unsigned char* nbuf) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0)   (gfx9 simm16: vm[3:0] exp[6:4] lgkm[11:8] vm[5:4]@[15:14])
+  __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0): tile 0 has no stores in front of its DMA
+  int k = 0;
+  auto step = [&](const unsigned char* buf, unsigned char* nbuf, auto cbt) {
+    constexpr int cb = decltype(cbt)::value;
+    // gfx9 simm16: vm[3:0] exp[6:4] lgkm[11:8] vm[5:4]@[15:14]
+    if constexpr (cb == 0)
+      __builtin_amdgcn_s_waitcnt(((NST >> 4) << 14) | 0x0F70 | (NST & 15));
+    else
+      __builtin_amdgcn_s_waitcnt(0x0F70);
     __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
-    if (nk < nmine) {
-      if (ncb_next == 0) set_dma_tile(tile_of(nk));   // first block of the next tile
-      issue(nbuf, ncb_next);
-      if (++ncb_next == ncb) { ncb_next = 0; ++nk; }
+    if constexpr (cb + 1 < NCB) {
+      issue(nbuf, cb + 1);
+    } else if (k + 1 < nmine) {
+      set_dma_tile(tile_of(k + 1));
+      issue(nbuf, 0);
     }
     const unsigned char* wb = RESW ? wres + cb * WBLK_B : buf + HALO_B;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      asm volatile("" ::: "memory");
+    // fragments of tap t + 1 are read while tap t's 16 MFMAs run (two register sets): the wave never
+    // waits for its own LDS reads except at the first tap of a stage
+    bf16x8 wf[2][4], pf[2][4];
+    auto load_frags = [&](int tap, bf16x8 (&w)[4], bf16x8 (&p)[4]) {
       const int dy = tap / 3, dx = tap - dy * 3;
-      bf16x8 wf[4], pf[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = j * 16 + lr;
-        wf[j] = *reinterpret_cast<const bf16x8*>(wb + (tap * 64 + n) * 64 + ((lq ^ hswz(n)) * 16));
+        w[j] = *reinterpret_cast<const bf16x8*>(wb + (tap * 64 + n) * 64 + ((lq ^ hswz(n)) * 16));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int P = (wid * RPW + (i * 16) / TW + dy) * HWW + (i * 16) % TW + lr + dx;
-        pf[i] = *reinterpret_cast<const bf16x8*>(buf + P * 64 + ((lq ^ hswz(P)) * 16));
+        p[i] = *reinterpret_cast<const bf16x8*>(buf + P * 64 + ((lq ^ hswz(P)) * 16));
       }
+    };
+    if constexpr ((DBG & 8) == 0 && (DBG & 32) == 0) {
+      load_frags(0, wf[0], pf[0]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int tap = 0; tap < 9; ++tap) {
+        asm volatile("" ::: "memory");
+        if (tap + 1 < 9) load_frags(tap + 1, wf[(tap + 1) & 1], pf[(tap + 1) & 1]);
+        if constexpr ((DBG & 64) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], pf[i], acc[j][i], 0, 0, 0);
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tap & 1][j], pf[tap & 1][i], acc[j][i], 0, 0, 0);
+        if constexpr ((DBG & 64) != 0) __builtin_amdgcn_s_setprio(0);
+      }
+    } else if constexpr ((DBG & 8) == 0) {   // experiment: one register set, read then compute
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        asm volatile("" ::: "memory");
+        load_frags(tap, wf[0], pf[0]);
+        if constexpr ((DBG & 64) != 0) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0][j], pf[0][i], acc[j][i], 0, 0, 0);
+        if constexpr ((DBG & 64) != 0) __builtin_amdgcn_s_setprio(0);
+      }
     }
-    if (cb + 1 < ncb) {
-      ++cb;
-      return;
-    }
+    if constexpr (cb + 1 < NCB) return;
     // epilogue: exactly 16 vector stores per wave (N % 64 == 0, full tiles) + 1 with STATS, the
-    // youngest VM ops when the next tile's first stage waits
+    // youngest VM ops when the next tile's first stage waits.  The residual tile is loaded as one
+    // batch first: a load between two stores would wait for the older store (in-order vmcnt)
+    uint2 rraw[4][4];
+    if (a.res) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int oy = cur.y0 + wid * RPW + (i * 16) / TW, ox = cur.x0 + (i * 16) % TW + lr;
+        const long pix = cur.base + (long)oy * a.W + ox;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          rraw[i][j] = *reinterpret_cast<const uint2*>(a.res + pix * a.ldres + cur.n0 + j * 16 + lq * 4);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int oy = cur.y0 + wid * RPW + (i * 16) / TW, ox = cur.x0 + (i * 16) % TW + lr;
@@ -386,8 +427,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
         const int n = cur.n0 + j * 16 + lq * 4;
         float rv[4] = {0.f, 0.f, 0.f, 0.f};
         if (a.res) {
-          const uint2 raw = *reinterpret_cast<const uint2*>(a.res + pix * a.ldres + n);
-          const bf16* e = reinterpret_cast<const bf16*>(&raw);
+          const bf16* e = reinterpret_cast<const bf16*>(&rraw[i][j]);
 #pragma unroll
           for (int r = 0; r < 4; ++r) rv[r] = (float)e[r];
         }
@@ -402,7 +442,8 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
           oe[r] = (bf16)v;
           acc[j][i][r] = STATS ? (float)oe[r] : 0.f;   // the stored (rounded) value, for the statistics
         }
-        *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+        if constexpr (!(DBG & 16)) *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+        else if ((o.x ^ o.y) == 0x7fc00001u) *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
       }
     }
     if constexpr (STATS) {
@@ -477,13 +518,23 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
       float* dst = a.in_part + ((((b * a.tiles_x * a.tiles_y) + tile) * 8 + wid) * (long)a.N + c) * 2;
       *reinterpret_cast<float2*>(dst) = make_float2(S1, S2);
     }
-    cb = 0;
-    if (++k < nmine) cur = tile_of(k);
   };
-  const int nst = nmine * ncb;               // even
-  for (int st = 0; st < nst; st += 2) {
-    step(lds0, lds1);
-    step(lds1, lds0);
+  for (; k < nmine; ++k) {
+    step(lds0, lds1, std::integral_constant<int, 0>{});
+    step(lds1, lds0, std::integral_constant<int, 1>{});
+    if constexpr (NCB > 2) {
+      step(lds0, lds1, std::integral_constant<int, 2>{});
+      step(lds1, lds0, std::integral_constant<int, 3>{});
+    }
+    if constexpr (NCB > 4) {
+      step(lds0, lds1, std::integral_constant<int, 4>{});
+      step(lds1, lds0, std::integral_constant<int, 5>{});
+    }
+    if constexpr (NCB > 6) {
+      step(lds0, lds1, std::integral_constant<int, 6>{});
+      step(lds1, lds0, std::integral_constant<int, 7>{});
+    }
+    if (k + 1 < nmine) cur = tile_of(k + 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -737,14 +788,36 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   const int g = a.ntiles < num_cus() ? a.ntiles : num_cus();
   a.in_part = d.in_part;
   const bool resw = d.Cin <= 64 && d.N == 64;
-  if (resw && a.in_part)
-    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<true, true>), dim3((unsigned)g), dim3(512), 0, s, a);
-  else if (resw)
-    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<true, false>), dim3((unsigned)g), dim3(512), 0, s, a);
-  else if (a.in_part)
-    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<false, true>), dim3((unsigned)g), dim3(512), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<false, false>), dim3((unsigned)g), dim3(512), 0, s, a);
+  const int ncb = d.Cin / 32;
+  if (dbg && !a.in_part) {   // experiment variants
+#define GHOST_PP_DBG(R, NB, V)                                                                              \
+  if (resw == R && ncb == NB && dbg == V) {                                                                \
+    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<R, false, NB, V>), dim3((unsigned)g), dim3(512), 0, s, a); \
+    return (int)hipGetLastError();                                                                         \
+  }
+    GHOST_PP_DBG(true, 2, 18) GHOST_PP_DBG(true, 2, 32) GHOST_PP_DBG(true, 2, 50) GHOST_PP_DBG(true, 2, 64)
+    GHOST_PP_DBG(true, 2, 82) GHOST_PP_DBG(true, 2, 96) GHOST_PP_DBG(true, 2, 114)
+    GHOST_PP_DBG(false, 4, 22) GHOST_PP_DBG(false, 4, 32) GHOST_PP_DBG(false, 4, 54) GHOST_PP_DBG(false, 4, 64)
+    GHOST_PP_DBG(false, 4, 86) GHOST_PP_DBG(false, 4, 96) GHOST_PP_DBG(false, 4, 118)
+    GHOST_PP_DBG(false, 8, 22) GHOST_PP_DBG(false, 8, 32) GHOST_PP_DBG(false, 8, 54) GHOST_PP_DBG(false, 8, 64)
+    GHOST_PP_DBG(false, 8, 86) GHOST_PP_DBG(false, 8, 96) GHOST_PP_DBG(false, 8, 118)
+#undef GHOST_PP_DBG
+  }
+#define GHOST_PP(R, ST, NB) \
+  hipLaunchKernelGGL((conv3x3_halo_pp_kernel<R, ST, NB>), dim3((unsigned)g), dim3(512), 0, s, a)
+  const bool st = a.in_part != nullptr;
+  if (resw) {
+    if (st) GHOST_PP(true, true, 2); else GHOST_PP(true, false, 2);
+  } else {
+    switch (ncb) {
+      case 2: if (st) GHOST_PP(false, true, 2); else GHOST_PP(false, false, 2); break;
+      case 4: if (st) GHOST_PP(false, true, 4); else GHOST_PP(false, false, 4); break;
+      case 6: if (st) GHOST_PP(false, true, 6); else GHOST_PP(false, false, 6); break;
+      case 8: if (st) GHOST_PP(false, true, 8); else GHOST_PP(false, false, 8); break;
+      default: return -1;
+    }
+  }
+#undef GHOST_PP
   return (int)hipGetLastError();
 }
 

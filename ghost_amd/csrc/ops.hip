@@ -74,6 +74,126 @@ in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chu
   }
 }
 
+// Statistics of upsample2x(x) without visiting the upsampled pixels.  The x2 bilinear upsample is
+// linear and separable, u(oy, ox) = sum_{s,t} a(oy, s) a(ox, t) x(s, t), with each output touching two
+// adjacent source rows / columns, so with v = x - K (K = x(0, 0) = u(0, 0), the shift in_stats_final
+// adds back):
+//   sum_o u - K = sum_{s,t} wy(s) wx(t) v(s,t)                                   w(s)  = sum_o a(o,s)
+//   sum_o (u - K)^2 = sum_{s,t} [ G0y G0x v^2 + 2 G0y G1x v v(s,t+1)              G0(s) = sum_o a(o,s)^2
+//                     + 2 G1y G0x v v(s+1,t) + 2 G1y G1x (v v(s+1,t+1) + v(s,t+1) v(s+1,t)) ]
+//                                                                                G1(s) = sum_o a(o,s) a(o,s+1)
+// with the tap weights a of the upsample kernel (same fp32 source coordinates).  These are the
+// statistics of the fp32 upsample the reference normalises (AEI_Net.py:137 -> AADLayer.py:16); the
+// materialised bf16 upsample differs from it by storage rounding only.  One pass over the source,
+// ~10 VALU per source pixel and channel instead of ~44 for the four outputs it feeds.
+//
+// up2x_weights_kernel: the six tables (rows then columns) into wt[6][ld], ld >= max(H, W).
+__global__ void up2x_weights_kernel(const Up2xSrc u, float* __restrict__ wt, int ld) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int dim = 0; dim < 2; ++dim) {
+    const int n = dim ? u.W : u.H;
+    const float sc = dim ? u.sw : u.sh;
+    if (s >= n) continue;
+    double w = 0.0, g0 = 0.0, g1 = 0.0;
+    for (int o = max(0, 2 * s - 4); o <= min(2 * n - 1, 2 * s + 4); ++o) {
+      float r = sc * (float)o;
+      asm volatile("" : "+v"(r));
+      const int i0 = (int)r;
+      const float l1 = r - (float)i0, l0 = 1.f - l1;
+      // a(o, i0) = l0, a(o, i0 + 1) = l1 (l1 = 0 at the last source index)
+      const double as = i0 == s ? (double)l0 : (i0 + 1 == s ? (double)l1 : 0.0);
+      const double an = i0 == s ? (double)l1 : 0.0;   // a(o, s + 1) beside a(o, s)
+      w += as;
+      g0 += as * as;
+      g1 += as * an;
+    }
+    float* t = wt + dim * 3 * ld;
+    t[s] = (float)w;
+    t[ld + s] = (float)g0;
+    t[2 * ld + s] = (float)g1;
+  }
+}
+
+// a workgroup: 4 source rows x 128 source columns of one sample, 64 channels; lane (cc, q): channel
+// chunk cc, source row r0 + q % 4, columns c0 + 16 (q / 4) .. +15 walked left to right, the next
+// four columns of both rows loaded as one batch (eight 16-byte loads in flight per lane)
+template <typename T>
+__global__ void __launch_bounds__(256)
+in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, float* __restrict__ part, const Up2xSrc u,
+                        const float* __restrict__ wt, int ld) {
+  __shared__ float red[2][32][65];
+  const int b = blockIdx.z, cg = blockIdx.y, ch = blockIdx.x;
+  const int t = threadIdx.x, cc = t & 7, q = t >> 3;
+  constexpr int VEC = Vec16<T>::N;
+  static_assert(VEC == 8, "bf16 source");
+  const int nxb = u.W / 128;
+  const int sy = (ch / nxb) * 4 + (q & 3), sx0 = (ch % nxb) * 128 + (q >> 2) * 16;
+  const T* xb = x + (long)b * u.H * u.W * ldx + cg * 64 + cc * 8;
+  float K[8];
+  load16_f(xb, K);
+  const float* wyt = wt;
+  const float* wxt = wt + 3 * ld;
+  const float wy = wyt[sy], g0y = wyt[ld + sy], g1y = wyt[2 * ld + sy];
+  const int sy1 = sy + 1 < u.H ? sy + 1 : sy;   // g1y = 0 on the last row
+  const T* r0 = xb + (long)sy * u.W * ldx;
+  const T* r1 = xb + (long)sy1 * u.W * ldx;
+  float v[8], vd[8], R1[8], RT0[8], RT1[8];
+  load16_f(r0 + (long)sx0 * ldx, v);
+  load16_f(r1 + (long)sx0 * ldx, vd);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    v[e] -= K[e];
+    vd[e] -= K[e];
+    R1[e] = 0.f;
+    RT0[e] = 0.f;
+    RT1[e] = 0.f;
+  }
+  for (int k0 = 0; k0 < 16; k0 += 4) {
+    u32x4 nr0[4], nr1[4];   // raw columns sx0 + k0 + 1 .. +4 of both rows
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int sxn = min(sx0 + k0 + 1 + j, u.W - 1);   // g1x = 0 on the last column
+      nr0[j] = *reinterpret_cast<const u32x4*>(r0 + (long)sxn * ldx);
+      nr1[j] = *reinterpret_cast<const u32x4*>(r1 + (long)sxn * ldx);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int sx = sx0 + k0 + j;
+      const float wx = wxt[sx], g0x = wxt[ld + sx], g1x = wxt[2 * ld + sx], g1x2 = 2.f * g1x;
+      const bf16* e0 = reinterpret_cast<const bf16*>(&nr0[j]);
+      const bf16* e1 = reinterpret_cast<const bf16*>(&nr1[j]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float vr = (float)e0[e] - K[e], vdr = (float)e1[e] - K[e];
+        R1[e] = fmaf(wx, v[e], R1[e]);
+        RT0[e] = fmaf(g0x * v[e], v[e], fmaf(g1x2 * v[e], vr, RT0[e]));
+        RT1[e] = fmaf(g0x * v[e], vd[e], fmaf(g1x, fmaf(v[e], vdr, vr * vd[e]), RT1[e]));
+        v[e] = vr;
+        vd[e] = vdr;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][q][cc * 8 + e] = wy * R1[e];
+    red[1][q][cc * 8 + e] = fmaf(g0y, RT0[e], 2.f * g1y * RT1[e]);
+  }
+  __syncthreads();
+  if (t < 64) {
+    const int c = cg * 64 + t;
+    float a = 0.f, s2 = 0.f;
+    for (int i = 0; i < 32; ++i) {
+      a += red[0][i][t];
+      s2 += red[1][i][t];
+    }
+    if (c < C) {
+      float* o = part + (((long)b * nchunk + ch) * C + c) * 2;
+      o[0] = a;
+      o[1] = s2;
+    }
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 in_stats_final_kernel(const T* __restrict__ x, int ldx, long bstride, int B, int HW, int C, int nchunk,
@@ -147,7 +267,9 @@ static void stats_geometry(int HW, int& chunk, int& nchunk) {
 size_t in_stats_workspace_bytes(int B, int HW, int C) {
   int chunk, nchunk;
   stats_geometry(HW, chunk, nchunk);
-  return (size_t)B * nchunk * C * 2 * sizeof(float);
+  const int nrec = nchunk > HW / 512 ? nchunk : HW / 512;   // >= in_stats_up_quad_kernel's records
+  // + the upsample weight tables of in_stats_up_quad_kernel (6 x max(H, W) <= 6 x 4096 floats)
+  return (size_t)B * nrec * C * 2 * sizeof(float) + 6 * 4096 * sizeof(float) + 256;
 }
 
 template <typename T>
@@ -158,6 +280,20 @@ static void in_stats_launch(const T* x, int ldx, int B, int HW, int C, float* st
   dim3 g1(nchunk, (C + 63) / 64, B);
   dim3 g2((B * C + 255) / 256);
   const Up2xSrc u = up ? *up : Up2xSrc{0, 0, 0.f, 0.f};
+  if constexpr (sizeof(T) == 2) {
+    if (up && u.H % 4 == 0 && u.W % 128 == 0 && u.H <= 4096 && u.W <= 4096 && C % 64 == 0 && ldx % 8 == 0) {
+      // closed form over the source: (H / 4) * (W / 128) records <= the HW / 512 reserved
+      const int nr = (u.H / 4) * (u.W / 128);
+      const int ld = u.H > u.W ? u.H : u.W;
+      float* wt = part + (size_t)B * nr * C * 2;   // 6 x ld floats after the records (workspace slack)
+      hipLaunchKernelGGL(up2x_weights_kernel, dim3((ld + 127) / 128), dim3(128), 0, s, u, wt, ld);
+      hipLaunchKernelGGL(in_stats_up_quad_kernel<T>, dim3(nr, C / 64, B), dim3(256), 0, s, x, ldx, C, nr, part, u, wt,
+                         ld);
+      hipLaunchKernelGGL(in_stats_final_kernel<T>, g2, dim3(256), 0, s, x, ldx, (long)u.H * u.W, B, HW, C, nr, part,
+                         stat);
+      return;
+    }
+  }
   if (up)
     hipLaunchKernelGGL((in_stats_partial_kernel<T, true>), g1, dim3(256), 0, s, x, ldx, HW, C, chunk, nchunk, part, u);
   else

@@ -4,7 +4,7 @@
 //
 // Same arithmetic as PyTorch's upsample_bilinear2d: src = dst * scale with the product
 // rounded to fp32 (the empty asm keeps hipcc from re-forming scale*dst - floor as one FMA),
-// lambda = src - floor(src), value = l0y*(l0x*v00 + l1x*v01) + l1y*(l0x*v10 + l1x*v11).
+// lambda = src - floor(src), value = l0y*(l0x*v00 + l1x*v01) + l1y*(l0x*v10 + l1x*v11) (up2x_mix).
 #pragma once
 #include "ghost_common.h"
 
@@ -46,6 +46,14 @@ GHOST_DEV Up2xTap up2x_tap(const Up2xSrc& u, int oy, int ox) {
   return t;
 }
 
+// the bilinear mix with its FMA contraction spelled out, so that every kernel that samples the
+// upsample (the upsample kernel, statistics, AAD reads) rounds to the same value
+GHOST_DEV float up2x_mix(float ly0, float ly1, float lx0, float lx1, float v00, float v01, float v10, float v11) {
+  const float top = fmaf(lx0, v00, lx1 * v01);
+  const float bot = fmaf(lx0, v10, lx1 * v11);
+  return fmaf(ly0, top, ly1 * bot);
+}
+
 // VEC (16-byte) channels at `xc` (sample base + channel offset) of output pixel t, in fp32
 template <typename T>
 GHOST_DEV void up2x_load16_f(const T* xc, int ld, const Up2xTap& t, float* o) {
@@ -57,7 +65,7 @@ GHOST_DEV void up2x_load16_f(const T* xc, int ld, const Up2xTap& t, float* o) {
   load16_f(xc + (long)t.o11 * ld, v11);
 #pragma unroll
   for (int e = 0; e < VEC; ++e)
-    o[e] = t.ly0 * (t.lx0 * v00[e] + t.lx1 * v01[e]) + t.ly1 * (t.lx0 * v10[e] + t.lx1 * v11[e]);
+    o[e] = up2x_mix(t.ly0, t.ly1, t.lx0, t.lx1, v00[e], v01[e], v10[e], v11[e]);
 }
 
 }  // namespace ghost

@@ -132,6 +132,11 @@ int ghost_linear_f32(const float* x, int B, int K, const float* w_packed, int N,
 /* InstanceNorm statistics: stat[b][c] = (mean, 1/sqrt(var+1e-5)) */
 int ghost_instnorm_stats_nhwc(int dtype, const void* x, int B, int HW, int C, int ldx, float* stat, void* ws,
                               int64_t ws_bytes, void* stream);
+/* the same statistics of upsample2x(x) (bilinear x2, align_corners, values rounded to dtype as the
+ * upsample kernel stores them) for an [B, H, W, C] source, without materialising the upsample
+ * (AEI_Net.py:137 feeding AADLayer.py:16's InstanceNorm) */
+int ghost_instnorm_stats_up2x_nhwc(int dtype, const void* x, int B, int H, int W, int C, int ldx, float* stat,
+                                   void* ws, int64_t ws_bytes, void* stream);
 /* AADLayer.forward: gbw_packed [Npad][Kpad] rows interleaved per 16 channels
  * (gamma c0..15, beta c0..15, gamma c16..31, ...), gbb the matching biases (fp32);
  * wh [C] / bh [1] the conv_h weights; idgb [B][id_ld] holds gamma_id at c and beta_id
@@ -144,6 +149,8 @@ int ghost_aad_layer_nhwc(int dtype, const void* h_in, int ldh, const void* z_att
  * w3/b3 per layer in the permuted layout of pack.py pack_aad_v3; InstanceNorm statistics of h_in
  * are computed into the workspace first.  up2x = 1: h_in is upsample2x of the [B, H/2, W/2, C]
  * tensor passed as h_in (F.interpolate of AEI_Net.py:135-137 fused into the AADLayer read; C in {64, 128}).
+ * up2x bit 2 (value 2): z_attr is upsample2x of the [B, H/2, W/2, Ca] tensor passed as z_attr (the unet
+ * z_attr8 = F.interpolate(z_attr7), AEI_Net.py:94; C = 64).
  * C in {256, 512, 1024} (L = 1, Ca <= 512) runs the per-channel-tile kernel of aad_wide.hip. */
 int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, const void* z_attr, int lda, int B, int H, int W,
                              int C, int Ca, int L, const void* const w3[], const float* const b3[],
@@ -161,6 +168,9 @@ int ghost_set_split_k(int n);
 /* testing knob: 1 (default) lets the generator sample the upsample of AADBlk7's output inside
  * AADBlk8's first AADLayer pair instead of materialising it; 0 materialises it */
 int ghost_set_fuse_upsample(int on);
+/* testing knob: 1 (default) lets swaps sample z_attr8 = upsample2x(z_attr7) inside AADBlk8's AADLayers
+ * instead of materialising it (unet / linknet, bf16, fuse_tail off); 0 materialises it */
+int ghost_set_fuse_zup(int on);
 /* testing knob: 1 (default) lets the persistent 3x3 conv emit the InstanceNorm partials of its
  * output (no separate statistics pass); 0 computes them by a separate pass */
 int ghost_set_fuse_stats(int on);

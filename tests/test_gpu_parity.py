@@ -291,6 +291,39 @@ def test_instnorm_stats(lib, dt, B, C, H):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C,H,W", [(2, 64, 128, 128), (2, 128, 16, 256), (3, 128, 64, 64), (2, 64, 32, 32),
+                                     (2, 32, 16, 16), (1, 64, 7, 5), (2, 1024, 2, 2)])
+def test_instnorm_stats_of_virtual_upsample(lib, dt, B, C, H, W):
+    """Statistics of upsample2x(x) without materialising it == those of the materialised upsample: the
+    per-pixel kernel samples the same bf16-rounded values; the closed form over the source (bf16,
+    W % 128 == 0) gives the statistics of the fp32 upsample, so there the storage rounding remains."""
+    from ghost_amd import _lib
+    g = torch.Generator().manual_seed(C + H + W)
+    x = (torch.randn(B, C, H, W, generator=g) * 0.3 + 2.0).to(dt)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=DEV)
+    xd = nhwc(x).to(DEV)
+    # the materialised path: our upsample kernel, then the statistics of its output
+    upd = torch.empty(B, 2 * H, 2 * W, C, dtype=dt, device=DEV)
+    _lib.check(lib.ghost_upsample2x_nhwc(_lib.gdtype(dt), xd.data_ptr(), C, upd.data_ptr(), C, B, H, W, C, stream(lib)))
+    st_m = torch.empty(B, C, 2, device=DEV)
+    _lib.check(lib.ghost_instnorm_stats_nhwc(_lib.gdtype(dt), upd.data_ptr(), B, 4 * H * W, C, C, st_m.data_ptr(),
+                                             ws.data_ptr(), ws.numel(), stream(lib)))
+    stat = torch.empty(B, C, 2, device=DEV)
+    _lib.check(lib.ghost_instnorm_stats_up2x_nhwc(_lib.gdtype(dt), xd.data_ptr(), B, H, W, C, C, stat.data_ptr(),
+                                                  ws.data_ptr(), ws.numel(), stream(lib)))
+    st, st_m = stat.cpu().double(), st_m.cpu().double()
+    quad = dt == torch.bfloat16 and W % 128 == 0 and H % 4 == 0 and C % 64 == 0
+    torch.testing.assert_close(st[..., 0], st_m[..., 0], atol=1e-4 if quad else 1e-5, rtol=1e-5)   # fp32 sum order
+    torch.testing.assert_close(st[..., 1], st_m[..., 1], atol=0, rtol=1e-3 if quad else 1e-5)
+    # and against float64 statistics of the (unrounded) PyTorch upsample: bf16 storage rounding only
+    up = F.interpolate(x.double(), scale_factor=2, mode="bilinear", align_corners=True)
+    var, mean = torch.var_mean(up, dim=(2, 3), unbiased=False)
+    tol = 1e-5 if dt == torch.float32 else 8e-3   # bf16 half-ulp at |x| < 4 (a 4x4 output averages few)
+    torch.testing.assert_close(st[..., 0], mean, atol=tol, rtol=0)
+    torch.testing.assert_close(st[..., 1], 1.0 / torch.sqrt(var + 1e-5), atol=0, rtol=10 * tol)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("C,H", [(64, 128), (1024, 2), (32, 64), (128, 7)])
 def test_upsample2x(lib, dt, C, H):
     from ghost_amd import _lib
@@ -410,6 +443,23 @@ def test_bf16_through_upsample_aad_matches_materialised(lib, backbone, nb):
     Y1, _ = G(xt.to(DEV), z.to(DEV))
     d = (Y1.float().cpu() - Y0).abs()
     assert float(d.mean()) <= 1e-3 and float(d.max()) <= 0.1, (float(d.mean()), float(d.max()))
+
+
+@pytest.mark.parametrize("backbone,nb,B", [("unet", 2, 4), ("linknet", 3, 2)])
+def test_bf16_swap_virtual_zattr8_matches_materialised(lib, backbone, nb, B):
+    """Swaps sample z_attr8 = upsample2x(z_attr7) inside AADBlk8's AADLayers (same interpolation and
+    bf16 rounding as the upsample kernel they replace): the uint8 frames equal the materialised path."""
+    G = model(backbone, nb, compute_dtype=torch.bfloat16)
+    _, z = aei_ref.make_inputs(B, 17)
+    crops = torch.from_numpy(aei_ref.make_u8_crops(B, 4)).to(DEV)
+    try:
+        _lib_mod().check(lib.ghost_set_fuse_zup(0))
+        U0 = G.swap_u8(crops, z[:1].to(DEV)).cpu().numpy()
+    finally:
+        lib.ghost_set_fuse_zup(1)
+    U1 = G.swap_u8(crops, z[:1].to(DEV)).cpu().numpy()
+    du = np.abs(U1.astype(np.int16) - U0.astype(np.int16))
+    assert du.max() <= 1 and (du > 0).mean() <= 1e-3, (du.max(), (du > 0).mean())
 
 
 @pytest.mark.parametrize("backbone,nb", [("unet", 2), ("linknet", 3)])
@@ -569,25 +619,32 @@ def test_conv3x3_narrow_op(lib, dt, cin, cout, H, W, use_res):
                                               (64, 32, 128, 4, 2, 0), (128, 64, 64, 8, 1, 0), (128, 32, 64, 8, 1, 0),
                                               (64, 64, 256, 2, 2, 1), (64, 32, 128, 4, 2, 1), (64, 64, 64, 8, 1, 1),
                                               (128, 64, 128, 2, 1, 1), (128, 32, 64, 8, 1, 1),
+                                              # z_attr through the upsample too (2) / alone (2 = bit 1)
+                                              (64, 64, 256, 2, 2, 3), (64, 64, 256, 2, 1, 2), (64, 32, 128, 4, 2, 3),
+                                              (64, 32, 64, 8, 1, 2), (64, 64, 128, 4, 2, 2),
                                               # aad_wide: one 64-channel tile per workgroup
                                               (256, 128, 64, 8, 1, 0), (512, 256, 32, 8, 1, 0),
                                               (1024, 256, 16, 16, 1, 0), (512, 64, 32, 4, 1, 0),
                                               (1024, 512, 16, 8, 1, 0)])
 def test_aad_layers_v3_vs_oracle(lib, c_x, c_a, n, B, L, up):
     """Register-epilogue AAD kernel (1 or 2 layers sharing h_in / z_attr) against the oracle AADLayer;
-    up = 1: h_in is read through the bilinear x2 upsample of an n/2 source (AEI_Net.py:137)."""
+    up bit 1: h_in is read through the bilinear x2 upsample of an n/2 source (AEI_Net.py:137); bit 2:
+    z_attr likewise (z_attr8 = F.interpolate(z_attr7), AEI_Net.py:94)."""
     import ctypes as C
     from ghost_amd import _lib
     from ghost_amd.network.pack import pack_aad_v3
     dt = torch.bfloat16
     g = torch.Generator().manual_seed(c_x * 3 + n + L)
-    hn = n // 2 if up else n
+    hn = n // 2 if up & 1 else n
     hs = (torch.randn(B, c_x, hn, hn, generator=g) * 1.5 + 0.7).to(dt).float()
     # the materialised path stores the upsample in bf16: the reference sees those values
-    h = F.interpolate(hs, scale_factor=2, mode="bilinear", align_corners=True).to(dt).float() if up else hs
-    za = torch.randn(B, c_a, n, n, generator=g).to(dt).float()
+    up2 = lambda t: F.interpolate(t, scale_factor=2, mode="bilinear", align_corners=True).to(dt).float()  # noqa: E731
+    h = up2(hs) if up & 1 else hs
+    zn = n // 2 if up & 2 else n
+    zs = torch.randn(B, c_a, zn, zn, generator=g).to(dt).float()
+    za = up2(zs) if up & 2 else zs
     zi = torch.randn(B, 512, generator=g)
-    hd, zad = nhwc(hs).to(dt).to(DEV), nhwc(za).to(dt).to(DEV)
+    hd, zad = nhwc(hs).to(dt).to(DEV), nhwc(zs).to(dt).to(DEV)
     keep, w3s, b3s, whs, bhs, ids, outs, refs = [], [], [], [], [], [], [], []
     for l in range(L):
         specs = [(f"v3_{l}.{k}", shp, kind) for k, shp, kind in [

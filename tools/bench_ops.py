@@ -35,7 +35,7 @@ def timeit(fn, iters):
     return s.elapsed_time(e) / iters * 1e3   # us
 
 
-def conv_cases(lib, iters, dt=torch.bfloat16):
+def conv_cases(lib, iters, dt=torch.bfloat16, only_pp=False):
     B = 64
     ws = torch.empty(512 << 20, dtype=torch.uint8, device=DEV)
     st = torch.cuda.current_stream().cuda_stream
@@ -46,6 +46,8 @@ def conv_cases(lib, iters, dt=torch.bfloat16):
              ("gen32 512->512", 32, 512, 512, 3, 1, 1), ("gen16 1024->1024", 16, 1024, 1024, 3, 1, 1),
              ("gen8 1024->1024", 8, 1024, 1024, 3, 1, 1), ("gen4 1024->1024", 4, 1024, 1024, 3, 1, 1),
              ("enc conv2 32->64", 128, 32, 64, 4, 2, 1), ("enc conv1 3->32", 256, 3, 32, 4, 2, 1)]
+    if only_pp:   # the persistent halo conv's shapes
+        cases = [c for c in cases if c[1] >= 64 and c[4] == 3 and c[3] >= 64 and c[2] <= 256]
     for name, H, ci, co, k, s, p in cases:
         x = torch.randn(B, H, H, ci, device=DEV).to(dt)
         w = pack_conv(torch.randn(co, ci, k, k, device=DEV) * 0.05, dt)
@@ -160,11 +162,14 @@ def aad_v3_cases(lib, iters):
     B, dt = 64, torch.bfloat16
     st = torch.cuda.current_stream().cuda_stream
     ws = torch.empty(512 << 20, dtype=torch.uint8, device=DEV)
-    for c, ca, n, L, up in [(64, 64, 256, 2, 1), (64, 64, 256, 2, 0), (64, 64, 256, 1, 0), (128, 64, 128, 1, 0),
+    # up: bit 1 h_in through the x2 upsample, bit 2 z_attr through it
+    for c, ca, n, L, up in [(64, 64, 256, 2, 1), (64, 64, 256, 2, 3), (64, 64, 256, 2, 0), (64, 64, 256, 1, 0),
+                            (64, 64, 256, 1, 2), (128, 64, 128, 1, 0),
                             (256, 128, 64, 1, 0), (512, 256, 32, 1, 0), (1024, 512 // 2, 16, 1, 0)]:
-        hn = n // 2 if up else n
+        hn = n // 2 if up & 1 else n
+        zn = n // 2 if up & 2 else n
         h = torch.randn(B, hn, hn, c, device=DEV).to(dt)
-        za = torch.randn(B, n, n, ca, device=DEV).to(dt)
+        za = torch.randn(B, zn, zn, ca, device=DEV).to(dt)
         keep, w3, b3, wh, bh, ids, outs = [], [], [], [], [], [], []
         for _ in range(L):
             t = [torch.randn(c // 64 * 128, ca, device=DEV).to(dt) * 0.05, torch.zeros(c // 64 * 128, device=DEV),
@@ -209,6 +214,14 @@ def stats_cases(lib, iters, dt=torch.bfloat16):
                                                                      stat.data_ptr(), ws.data_ptr(), ws.numel(), st)),
                     iters)
         print(f"stats C={C} n={n} {us:9.1f} us  {x.numel() * x.element_size() / us / 1e3:7.1f} GB/s", flush=True)
+    for C, n in [(64, 128), (128, 64)]:   # statistics of the x2 upsample of an n x n source
+        x = torch.randn(B, n, n, C, device=DEV).to(dt)
+        stat = torch.empty(B, C, 2, device=DEV)
+        us = timeit(lambda: _lib.check(lib.ghost_instnorm_stats_up2x_nhwc(_lib.gdtype(dt), x.data_ptr(), B, n, n, C, C,
+                                                                          stat.data_ptr(), ws.data_ptr(), ws.numel(),
+                                                                          st)), iters)
+        print(f"stats_up2x C={C} {n}->{2 * n} {us:9.1f} us  {x.numel() * x.element_size() / us / 1e3:7.1f} GB/s(src)",
+              flush=True)
 
 
 def ceiling_cases(iters, dt=torch.bfloat16):
@@ -249,8 +262,8 @@ def main():
     print("env:", {k: v for k, v in os.environ.items() if k.startswith("GHOST_")})
     if a.only == "ceil":
         ceiling_cases(a.iters)
-    if a.only in ("", "conv"):
-        conv_cases(lib, a.iters)
+    if a.only in ("", "conv", "pp"):
+        conv_cases(lib, a.iters, only_pp=a.only == "pp")
     if a.only in ("", "arc"):
         arc_cases(lib, a.iters)
     if a.only in ("", "enc"):
