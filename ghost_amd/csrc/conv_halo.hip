@@ -14,6 +14,7 @@
 // which overlap one workgroup's DMA with the other's MFMAs.
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "conv_halo.h"
 #include "ghost_common.h"
@@ -212,9 +213,15 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
 // (cdna_hip_programming.md, glds notes).  Scale/shift live in LDS so the epilogue issues no
 // ordinary global load while a DMA is outstanding (hipcc would wait vmcnt(0) for its result).
 // ---------------------------------------------------------------------------
+// f(integral_constant<int, P>) for P in the sequence, in order (compile-time unrolling)
+template <int... P, class F>
+GHOST_DEV void pp_unroll(std::integer_sequence<int, P...>, F&& f) {
+  (f(std::integral_constant<int, P>{}), ...);
+}
+
 template <bool RESW, bool STATS, int NCB, int DBG = 0>
 __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) {
-  static_assert(NCB % 2 == 0 && NCB <= 8 && (!RESW || NCB == 2), "channel blocks per tile");
+  static_assert(NCB % 2 == 0 && NCB <= 32 && (!RESW || NCB == 2), "channel blocks per tile");
   // DBG (experiments only, GHOST_HALO_DBG): 2 no halo DMA, 4 no weight DMA, 8 no LDS reads/MFMA,
   // 16 no output stores
   // RESW: Cin <= 64 and N == 64 — the whole weight tensor (<= 2 blocks x 36 KB) stays resident in
@@ -376,31 +383,18 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
         p[i] = *reinterpret_cast<const bf16x8*>(buf + P * 64 + ((lq ^ hswz(P)) * 16));
       }
     };
-    if constexpr ((DBG & 8) == 0 && (DBG & 32) == 0) {
+    // (measured: the same time as one register set read then used, and with s_setprio around the MFMAs)
+    if constexpr ((DBG & 8) == 0) {
       load_frags(0, wf[0], pf[0]);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         asm volatile("" ::: "memory");
         if (tap + 1 < 9) load_frags(tap + 1, wf[(tap + 1) & 1], pf[(tap + 1) & 1]);
-        if constexpr ((DBG & 64) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tap & 1][j], pf[tap & 1][i], acc[j][i], 0, 0, 0);
-        if constexpr ((DBG & 64) != 0) __builtin_amdgcn_s_setprio(0);
-      }
-    } else if constexpr ((DBG & 8) == 0) {   // experiment: one register set, read then compute
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        asm volatile("" ::: "memory");
-        load_frags(tap, wf[0], pf[0]);
-        if constexpr ((DBG & 64) != 0) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0][j], pf[0][i], acc[j][i], 0, 0, 0);
-        if constexpr ((DBG & 64) != 0) __builtin_amdgcn_s_setprio(0);
       }
     }
     if constexpr (cb + 1 < NCB) return;
@@ -520,20 +514,12 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
     }
   };
   for (; k < nmine; ++k) {
-    step(lds0, lds1, std::integral_constant<int, 0>{});
-    step(lds1, lds0, std::integral_constant<int, 1>{});
-    if constexpr (NCB > 2) {
-      step(lds0, lds1, std::integral_constant<int, 2>{});
-      step(lds1, lds0, std::integral_constant<int, 3>{});
-    }
-    if constexpr (NCB > 4) {
-      step(lds0, lds1, std::integral_constant<int, 4>{});
-      step(lds1, lds0, std::integral_constant<int, 5>{});
-    }
-    if constexpr (NCB > 6) {
-      step(lds0, lds1, std::integral_constant<int, 6>{});
-      step(lds1, lds0, std::integral_constant<int, 7>{});
-    }
+    // the tile's NCB stages unrolled: even ones read lds0, odd ones lds1
+    pp_unroll(std::make_integer_sequence<int, NCB / 2>{}, [&](auto pt) {
+      constexpr int P = decltype(pt)::value;
+      step(lds0, lds1, std::integral_constant<int, 2 * P>{});
+      step(lds1, lds0, std::integral_constant<int, 2 * P + 1>{});
+    });
     if (k + 1 < nmine) cur = tile_of(k + 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -795,12 +781,8 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
     hipLaunchKernelGGL((conv3x3_halo_pp_kernel<R, false, NB, V>), dim3((unsigned)g), dim3(512), 0, s, a); \
     return (int)hipGetLastError();                                                                         \
   }
-    GHOST_PP_DBG(true, 2, 18) GHOST_PP_DBG(true, 2, 32) GHOST_PP_DBG(true, 2, 50) GHOST_PP_DBG(true, 2, 64)
-    GHOST_PP_DBG(true, 2, 82) GHOST_PP_DBG(true, 2, 96) GHOST_PP_DBG(true, 2, 114)
-    GHOST_PP_DBG(false, 4, 22) GHOST_PP_DBG(false, 4, 32) GHOST_PP_DBG(false, 4, 54) GHOST_PP_DBG(false, 4, 64)
-    GHOST_PP_DBG(false, 4, 86) GHOST_PP_DBG(false, 4, 96) GHOST_PP_DBG(false, 4, 118)
-    GHOST_PP_DBG(false, 8, 22) GHOST_PP_DBG(false, 8, 32) GHOST_PP_DBG(false, 8, 54) GHOST_PP_DBG(false, 8, 64)
-    GHOST_PP_DBG(false, 8, 86) GHOST_PP_DBG(false, 8, 96) GHOST_PP_DBG(false, 8, 118)
+    GHOST_PP_DBG(true, 2, 2) GHOST_PP_DBG(true, 2, 8) GHOST_PP_DBG(true, 2, 16) GHOST_PP_DBG(true, 2, 18)
+    GHOST_PP_DBG(false, 4, 6) GHOST_PP_DBG(false, 4, 8) GHOST_PP_DBG(false, 4, 16) GHOST_PP_DBG(false, 4, 22)
 #undef GHOST_PP_DBG
   }
 #define GHOST_PP(R, ST, NB) \
@@ -814,6 +796,8 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
       case 4: if (st) GHOST_PP(false, true, 4); else GHOST_PP(false, false, 4); break;
       case 6: if (st) GHOST_PP(false, true, 6); else GHOST_PP(false, false, 6); break;
       case 8: if (st) GHOST_PP(false, true, 8); else GHOST_PP(false, false, 8); break;
+      case 16: if (st) GHOST_PP(false, true, 16); else GHOST_PP(false, false, 16); break;
+      case 32: if (st) GHOST_PP(false, true, 32); else GHOST_PP(false, false, 32); break;
       default: return -1;
     }
   }
@@ -828,9 +812,15 @@ bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
   }();
   if (!conv3x3_halo_supported(d)) return false;
   const bool wide = d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0;
-  // measured A/B (B = 64): the persistent form wins up to Cin = 256 (256x256: -23 %, 128x128: -7 %,
-  // 64x64 256->256: -9 %); at Cin >= 512 the per-stage barrier costs more than the prefetch saves
-  const bool ok = wide && pp && d.N <= 512 && d.Cin % 64 == 0 && d.Cin <= 256 && !d.tanh_out;
+  static const int max_cin = [] {
+    const char* e = getenv("GHOST_HALO_PP_MAXCIN");
+    return e ? atoi(e) : 1024;
+  }();
+  // measured A/B (B = 64): the persistent form wins at every generator shape with W % 32 == 0 (256x256:
+  // -23 %, 128x128: -7 %, 64x64 256->256: -9 %; with the counted first-stage wait also 64x64 512->128
+  // -11 %, 32x32 512->512 -6 %, 32x32 1024->256 -8 %: +3 % frames/s end to end)
+  const bool cin_ok = d.Cin == 64 || d.Cin == 128 || d.Cin == 192 || d.Cin == 256 || d.Cin == 512 || d.Cin == 1024;
+  const bool ok = wide && pp && d.N <= 1024 && d.N % 64 == 0 && cin_ok && d.Cin <= max_cin && !d.tanh_out;
   if (ok && nrec) *nrec = (d.Hi / HaloWide::TH) * (d.Wi / HaloWide::TW) * 8;
   return ok;
 }

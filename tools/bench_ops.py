@@ -43,7 +43,8 @@ def conv_cases(lib, iters, dt=torch.bfloat16, only_pp=False):
     cases = [("gen256 64->64", 256, 64, 64, 3, 1, 1), ("gen256 cat128->3", 256, 128, 3, 3, 1, 1),
              ("gen128 128->128", 128, 128, 128, 3, 1, 1), ("gen128 cat256->64", 128, 256, 64, 3, 1, 1),
              ("gen64 256->256", 64, 256, 256, 3, 1, 1), ("gen64 cat512->128", 64, 512, 128, 3, 1, 1),
-             ("gen32 512->512", 32, 512, 512, 3, 1, 1), ("gen16 1024->1024", 16, 1024, 1024, 3, 1, 1),
+             ("gen32 512->512", 32, 512, 512, 3, 1, 1), ("gen32 cat1024->256", 32, 1024, 256, 3, 1, 1),
+             ("gen16 1024->1024", 16, 1024, 1024, 3, 1, 1),
              ("gen8 1024->1024", 8, 1024, 1024, 3, 1, 1), ("gen4 1024->1024", 4, 1024, 1024, 3, 1, 1),
              ("enc conv2 32->64", 128, 32, 64, 4, 2, 1), ("enc conv1 3->32", 256, 3, 32, 4, 2, 1)]
     if only_pp:   # the persistent halo conv's shapes
