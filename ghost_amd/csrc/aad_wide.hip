@@ -142,6 +142,8 @@ GHOST_DEV void aad_wide_body(const AadWideArgs& a) {
 
 // Ca <= 256: 4 waves per SIMD (<= 128 VGPRs), two workgroups per CU.  Ca = 512: the 133 KB of
 // weight rows allow one workgroup per CU, so the z_attr row (64 VGPRs) may use the registers.
+// (Measured alternative, not kept: each wave on four 16-pixel tiles per weight fragment — 4x less
+// LDS traffic per MFMA, 300-390 registers, one wave per SIMD — ran 10-17 % slower at 16x16-64x64.)
 template <int C, int CA>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_wide_kernel(const AadWideArgs a) {
   aad_wide_body<C, CA>(a);
