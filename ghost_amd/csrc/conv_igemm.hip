@@ -574,7 +574,8 @@ Plan make_plan(const ConvDesc& d) {
   p.fast = (d.Cin % 32 == 0) && (d.ldx % vec == 0) && ((uintptr_t)d.x % 16 == 0);
   // BK = 64 pays only on deep reductions (measured: 256x64 tiles lose 2x at BK 64 from LDS occupancy)
   const bool bk64_ok = bf && p.fast && d.Cin % 64 == 0 && d.Kpad % 64 == 0;
-  p.BK = (bk64_ok && d.Kpad >= 4608) ? 64 : 32;
+  // (Kpad 4096: the encoder's 16x16 conv and 8x8 deconv, measured -10..-19 % with BK 64)
+  p.BK = (bk64_ok && d.Kpad >= 4096) ? 64 : 32;
   if (force_bk == 32 || (force_bk == 64 && bk64_ok)) p.BK = force_bk;
   if (!p.fast) {
     p.BN = d.N <= 32 ? 32 : 64;
@@ -587,7 +588,9 @@ Plan make_plan(const ConvDesc& d) {
   } else if (d.N <= 32) {
     p.BN = 32; p.BM = 256;
   } else if (d.N <= 64) {
-    p.BN = 64; p.BM = 256;
+    // the encoder's 4x4/s2 convs gather 64-byte tap rows: 128-row tiles take the LDS-DMA ring
+    // (measured 128x128 32->64: 56 vs 72 us at 256 rows)
+    p.BN = 64; p.BM = (bf && d.kh == 4 && d.stride == 2 && d.kind == CONV_FWD) ? 128 : 256;
   } else {
     p.BN = 128;
     p.BM = ((p.M + 127) / 128) * ((d.N + 127) / 128) * p.npar >= 512 ? 128 : 64;
@@ -606,7 +609,10 @@ Plan make_plan(const ConvDesc& d) {
   int s = 1;
   if (d.force_split > 0) {
     s = d.force_split;
-  } else if (tiles < (d.min_wgs > 0 ? d.min_wgs : 256) && nk >= 16) {
+  } else if ((tiles < (d.min_wgs > 0 ? d.min_wgs : 256) && nk >= 16) ||
+             (d.min_wgs <= 0 && tiles == 256 && nk >= 64)) {
+    // one round of 256 tiles with a deep reduction splits in two as well (measured: the 4x4 deconv
+    // 2048->512 -26 %, the 16x16 4x4/s2 conv 256->512 -19 %)
     const int target = 2 * (d.min_wgs > 0 ? d.min_wgs : 256);
     s = (target + tiles - 1) / tiles;       // aim for >= 2 workgroups per CU
     s = s < nk / 8 ? s : nk / 8;            // keep >= 8 K steps per split
