@@ -192,9 +192,13 @@ void run_conv(Ctx& c, ConvDesc& d, int cls_all, int cls_big, double flops) {
 }
 
 static int g_fuse_upsample = 1;   // ghost_set_fuse_upsample (testing knob)
-static int g_fuse_zup = [] {       // GHOST_FUSE_ZUP=0 / ghost_set_fuse_zup(0): materialise z_attr8 in swaps
+// GHOST_FUSE_ZUP=1 / ghost_set_fuse_zup(1): swaps sample z_attr8 = upsample2x(z_attr7) inside AADBlk8's
+// AADLayers instead of materialising it.  Off by default: measured B = 64, the AAD kernels that
+// interpolate z_attr as well as h_in are compute/latency-bound and take what the upsample kernel
+// saves (AAD + upsample 2.500 vs 2.499 ms per step)
+static int g_fuse_zup = [] {
   const char* e = getenv("GHOST_FUSE_ZUP");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 0;
 }();
 // GHOST_FUSE_TAIL=1: AADBlk8's tail as one kernel (aad_tail.hip).  Off by default: measured B = 64 it
 // saves 2 GB of HBM traffic but runs latency-bound at one 8-wave workgroup per CU (793 us against the
@@ -1103,6 +1107,7 @@ extern "C" int ghost_aad_layer_nhwc(int dtype, const void* h_in, int ldh, const 
   const size_t mask_b = ((size_t)B * HW * sizeof(float) + 255) & ~size_t(255);
   ConvDesc d;
   d.ti = d.to = dtype;
+  d.force_split = g_force_split;   // testing knob (ghost_set_split_k)
   d.x = z_attr; d.B = B; d.Hi = H; d.Wi = W; d.Cin = Ca; d.ldx = lda;
   d.w = gbw_packed; d.N = 2 * C; d.Npad = Npad; d.Kpad = Kpad;
   d.kind = CONV_FWD; d.kh = d.kw = 1;

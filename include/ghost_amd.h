@@ -168,8 +168,8 @@ int ghost_set_split_k(int n);
 /* testing knob: 1 (default) lets the generator sample the upsample of AADBlk7's output inside
  * AADBlk8's first AADLayer pair instead of materialising it; 0 materialises it */
 int ghost_set_fuse_upsample(int on);
-/* testing knob: 1 (default) lets swaps sample z_attr8 = upsample2x(z_attr7) inside AADBlk8's AADLayers
- * instead of materialising it (unet / linknet, bf16, fuse_tail off); 0 materialises it */
+/* experimental knob: 1 lets swaps sample z_attr8 = upsample2x(z_attr7) inside AADBlk8's AADLayers
+ * instead of materialising it (unet / linknet, bf16, fuse_tail off); 0 (default) materialises it */
 int ghost_set_fuse_zup(int on);
 /* testing knob: 1 (default) lets the persistent 3x3 conv emit the InstanceNorm partials of its
  * output (no separate statistics pass); 0 computes them by a separate pass */

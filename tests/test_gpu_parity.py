@@ -452,12 +452,13 @@ def test_bf16_swap_virtual_zattr8_matches_materialised(lib, backbone, nb, B):
     G = model(backbone, nb, compute_dtype=torch.bfloat16)
     _, z = aei_ref.make_inputs(B, 17)
     crops = torch.from_numpy(aei_ref.make_u8_crops(B, 4)).to(DEV)
+    _lib_mod().check(lib.ghost_set_fuse_zup(0))
+    U0 = G.swap_u8(crops, z[:1].to(DEV)).cpu().numpy()
     try:
-        _lib_mod().check(lib.ghost_set_fuse_zup(0))
-        U0 = G.swap_u8(crops, z[:1].to(DEV)).cpu().numpy()
+        _lib_mod().check(lib.ghost_set_fuse_zup(1))
+        U1 = G.swap_u8(crops, z[:1].to(DEV)).cpu().numpy()
     finally:
-        lib.ghost_set_fuse_zup(1)
-    U1 = G.swap_u8(crops, z[:1].to(DEV)).cpu().numpy()
+        lib.ghost_set_fuse_zup(0)   # the default
     du = np.abs(U1.astype(np.int16) - U0.astype(np.int16))
     assert du.max() <= 1 and (du > 0).mean() <= 1e-3, (du.max(), (du > 0).mean())
 
