@@ -596,6 +596,7 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
   }
   int id_off = 0;
   bool m_virtual = false;   // m is not materialised: h_in = upsample2x(m) at n x n (m is n/2 x n/2)
+  const void* m_src = nullptr;   // m = upsample2x(m_src) materialised: its statistics come from the source
   for (int k = 1; k <= 8; ++k) {
     const int cin = h->gen()[k - 1][0], cout = h->gen()[k - 1][1];
     int Ca, n;
@@ -610,6 +611,8 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     float* stat_m = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
     if (m_virtual)
       run_stats_up(c, m, cin, B, n / 2, n / 2, cin, stat_m);
+    else if (m_src && in_stats_up2x_closed_form(h->dt, n / 2, n / 2, cin, cin))
+      run_stats_up(c, m_src, cin, B, n / 2, n / 2, cin, stat_m);   // one pass over the 4x smaller source
     else
       run_stats(c, m, cin, B, n * n, cin, stat_m);
     void* y = last_k ? y_out : c.alloc(P * cout * es);
@@ -688,11 +691,13 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
                         aad_v3_supported(h->dt, B, n_n * n_n, cout, Ca_n, Ca_n, cout, 8);
       if (fuse) {
         m = y;
+        m_src = nullptr;
         m_virtual = true;
       } else {
         void* mn = c.alloc((size_t)B * 4 * n * n * cout * es);
         run_up(c, y, cout, mn, cout, B, n, n, cout);
         m = mn;
+        m_src = y;
         m_virtual = false;
       }
     }

@@ -14,6 +14,8 @@ int in_stats(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, 
              hipStream_t s);
 // the same statistics of upsample2x(x) ([B, 2H, 2W, C], values rounded to dt) without materialising
 // it: x is the [B, H, W, C] source; workspace = in_stats_workspace_bytes(B, 4HW, C)
+// true when in_stats_up2x takes the closed form over the source (cheaper than reading the upsample)
+bool in_stats_up2x_closed_form(int dt, int H, int W, int C, int ldx);
 int in_stats_up2x(int dt, const void* x, int ldx, int B, int H, int W, int C, float* stat, void* ws, size_t ws_bytes,
                   hipStream_t s);
 

@@ -114,9 +114,10 @@ __global__ void up2x_weights_kernel(const Up2xSrc u, float* __restrict__ wt, int
   }
 }
 
-// a workgroup: 4 source rows x 128 source columns of one sample, 64 channels; lane (cc, q): channel
-// chunk cc, source row r0 + q % 4, columns c0 + 16 (q / 4) .. +15 walked left to right, the next
-// four columns of both rows loaded as one batch (eight 16-byte loads in flight per lane)
+// a workgroup: RB source rows x CPB = 512 / RB source columns of one sample (CPB = min(W, 128)),
+// 64 channels; lane (cc, q): channel chunk cc, source row r0 + q % RB, columns c0 + 16 (q / RB) ..
+// +15 walked left to right, the next four columns of both rows loaded as one batch (eight 16-byte
+// loads in flight per lane)
 template <typename T>
 __global__ void __launch_bounds__(256)
 in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, float* __restrict__ part, const Up2xSrc u,
@@ -126,8 +127,8 @@ in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, flo
   const int t = threadIdx.x, cc = t & 7, q = t >> 3;
   constexpr int VEC = Vec16<T>::N;
   static_assert(VEC == 8, "bf16 source");
-  const int nxb = u.W / 128;
-  const int sy = (ch / nxb) * 4 + (q & 3), sx0 = (ch % nxb) * 128 + (q >> 2) * 16;
+  const int CPB = u.W < 128 ? u.W : 128, RB = 512 / CPB, nxb = u.W / CPB;
+  const int sy = (ch / nxb) * RB + q % RB, sx0 = (ch % nxb) * CPB + (q / RB) * 16;
   const T* xb = x + (long)b * u.H * u.W * ldx + cg * 64 + cc * 8;
   float K[8];
   load16_f(xb, K);
@@ -272,6 +273,12 @@ size_t in_stats_workspace_bytes(int B, int HW, int C) {
   return (size_t)B * nrec * C * 2 * sizeof(float) + 6 * 4096 * sizeof(float) + 256;
 }
 
+bool in_stats_up2x_closed_form(int dt, int H, int W, int C, int ldx) {
+  if (dt != GHOST_BF16 || W % 16 || C % 64 || ldx % 8 || H > 4096 || W > 4096) return false;
+  const int cpb = W < 128 ? W : 128;   // source columns per workgroup; 512 / cpb rows
+  return W % cpb == 0 && H % (512 / cpb) == 0;
+}
+
 template <typename T>
 static void in_stats_launch(const T* x, int ldx, int B, int HW, int C, float* stat, float* part, const Up2xSrc* up,
                             hipStream_t s) {
@@ -281,9 +288,9 @@ static void in_stats_launch(const T* x, int ldx, int B, int HW, int C, float* st
   dim3 g2((B * C + 255) / 256);
   const Up2xSrc u = up ? *up : Up2xSrc{0, 0, 0.f, 0.f};
   if constexpr (sizeof(T) == 2) {
-    if (up && u.H % 4 == 0 && u.W % 128 == 0 && u.H <= 4096 && u.W <= 4096 && C % 64 == 0 && ldx % 8 == 0) {
+    if (up && in_stats_up2x_closed_form(GHOST_BF16, u.H, u.W, C, ldx)) {
       // closed form over the source: (H / 4) * (W / 128) records <= the HW / 512 reserved
-      const int nr = (u.H / 4) * (u.W / 128);
+      const int nr = u.H * u.W / 512;   // workgroups of 512 source pixels
       const int ld = u.H > u.W ? u.H : u.W;
       float* wt = part + (size_t)B * nr * C * 2;   // 6 x ld floats after the records (workspace slack)
       hipLaunchKernelGGL(up2x_weights_kernel, dim3((ld + 127) / 128), dim3(128), 0, s, u, wt, ld);
