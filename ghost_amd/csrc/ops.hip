@@ -2,6 +2,7 @@
 // and the layout/precision conversions at the AEI_Net boundary.  All NHWC, 16-byte
 // vector accesses along channels, fp32 arithmetic.
 #include <algorithm>
+#include <cstdlib>
 
 #include "ghost_common.h"
 #include "ops.h"
@@ -397,6 +398,75 @@ aad_mask_kernel(const T* __restrict__ h, int ldh, int HW, int C, int G, int ppb,
   }
 }
 
+// bf16 form with the per-channel tables in registers: lane gl of a G-lane pixel group always owns
+// channels 8 (gl + G j), j < NCH, so its (wh * rstd) factors stay in VGPRs and the logit is one FMA
+// per channel: sum_c (wh_c rstd_c) h_c - K with K = sum_c wh_c rstd_c mu_c per sample (as aad_v3).
+// Measured against the LDS-table kernel above: the per-element LDS reads made it VALU/LDS-bound
+// at 2-2.6 TB/s of h_in.
+template <int L, int NCH>
+__global__ void __launch_bounds__(256)
+aad_mask_reg_kernel(const bf16* __restrict__ h, int ldh, int HW, int C, int G, int ppb, const float* __restrict__ stat,
+                    const float* __restrict__ wh0, const float* __restrict__ bh0, float* __restrict__ mask0,
+                    const float* __restrict__ wh1, const float* __restrict__ bh1, float* __restrict__ mask1) {
+  const int t = threadIdx.x, b = blockIdx.y;
+  const int per = 256 / G, gl = t % G;
+  const float* st = stat + (long)b * C * 2;
+  float tab[L][NCH][8];
+  float k[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) k[l] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = (gl + G * j) * 8 + e;
+      const float mu = st[2 * c], rs = st[2 * c + 1];
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        tab[l][j][e] = (l ? wh1 : wh0)[c] * rs;
+        k[l] = fmaf(tab[l][j][e], mu, k[l]);
+      }
+    }
+  float bias[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) bias[l] = (l ? bh1 : bh0)[0] - group_sum(k[l], G);
+  const long base = (long)b * HW;
+  const int pend = min(HW, (blockIdx.x + 1) * ppb);
+  constexpr int U = 4;
+  for (int q0 = blockIdx.x * ppb + t / G; q0 < pend; q0 += U * per) {
+    u32x4 raw[U][NCH];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + u * per;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+        raw[u][j] = q < pend ? *reinterpret_cast<const u32x4*>(h + (base + q) * ldh + (gl + G * j) * 8)
+                             : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float sl[L];
+#pragma unroll
+      for (int l = 0; l < L; ++l) sl[l] = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        const bf16* e8 = reinterpret_cast<const bf16*>(&raw[u][j]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+#pragma unroll
+          for (int l = 0; l < L; ++l) sl[l] = fmaf(tab[l][j][e], (float)e8[e], sl[l]);
+      }
+      const int q = q0 + u * per;
+#pragma unroll
+      for (int l = 0; l < L; ++l) sl[l] = group_sum(sl[l], G);
+      if (gl == 0 && q < pend) {
+        mask0[base + q] = sigmoidf_ref(sl[0] + bias[0]);
+        if (L == 2) mask1[base + q] = sigmoidf_ref(sl[L - 1] + bias[L - 1]);
+      }
+    }
+  }
+}
+
 int aad_mask2(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh0,
               const float* bh0, float* mask0, const float* wh1, const float* bh1, float* mask1, hipStream_t s) {
   const int vec = dt == GHOST_F32 ? 4 : 8;
@@ -409,6 +479,20 @@ int aad_mask2(int dt, const void* h, int ldh, int B, int HW, int C, const float*
   if (ppb > HW) ppb = HW;
   dim3 grid((unsigned)((HW + ppb - 1) / ppb), (unsigned)B);
   const int L = wh1 ? 2 : 1;
+  static const int use_reg = [] {
+    const char* e = getenv("GHOST_MASK_REG");
+    return e ? atoi(e) : 1;
+  }();
+  if (use_reg && dt == GHOST_BF16 && (C == 8 * G || C == 16 * G)) {
+    const int nch = C / (8 * G);
+#define GHOST_MR(l, n)                                                                                              \
+  hipLaunchKernelGGL((aad_mask_reg_kernel<l, n>), grid, dim3(256), 0, s, (const bf16*)h, ldh, HW, C, G, ppb, stat, \
+                     wh0, bh0, mask0, wh1, bh1, mask1)
+    if (L == 2) { if (nch == 1) GHOST_MR(2, 1); else GHOST_MR(2, 2); }
+    else { if (nch == 1) GHOST_MR(1, 1); else GHOST_MR(1, 2); }
+#undef GHOST_MR
+    return (int)hipGetLastError();
+  }
   const size_t lds = (size_t)(L + 1) * C * sizeof(float);
 #define GHOST_M(T, l)                                                                                            \
   hipLaunchKernelGGL((aad_mask_kernel<T, l>), grid, dim3(256), lds, s, (const T*)h, ldh, HW, C, G, ppb, stat, wh0, \
