@@ -494,7 +494,13 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     }
     return;
   }
-  const size_t lmax = C == 64 ? 2 : 1;
+  // AADBlk7's block-input pair (C = 128, Ca = 64, materialised h_in) in one kernel: measured B = 64,
+  // 258 vs 2 x 141 us (GHOST_AAD_PAIR128=0: one layer per kernel)
+  static const int pair128 = [] {
+    const char* e = getenv("GHOST_AAD_PAIR128");
+    return e ? atoi(e) : 1;
+  }();
+  const size_t lmax = (C == 64 || (pair128 && C == 128 && Ca == 64 && !up_src)) ? 2 : 1;
   for (size_t i0 = 0; i0 < ls.size(); i0 += lmax) {
     AadV3Desc d;
     d.za = za; d.lda = lda; d.Ca = Ca; d.hin = hin; d.ldh = ldh; d.stat = stat;

@@ -626,7 +626,7 @@ def test_conv3x3_narrow_op(lib, dt, cin, cout, H, W, use_res):
 @pytest.mark.parametrize("c_x,c_a,n,B,L,up", [(64, 64, 256, 2, 2, 0), (64, 64, 256, 2, 1, 0), (128, 128, 128, 2, 1, 0),
                                               (64, 32, 128, 4, 2, 0), (128, 64, 64, 8, 1, 0), (128, 32, 64, 8, 1, 0),
                                               (64, 64, 256, 2, 2, 1), (64, 32, 128, 4, 2, 1), (64, 64, 64, 8, 1, 1),
-                                              (128, 64, 128, 2, 1, 1), (128, 32, 64, 8, 1, 1),
+                                              (128, 64, 128, 2, 1, 1), (128, 32, 64, 8, 1, 1), (128, 64, 128, 2, 2, 0),
                                               # z_attr through the upsample too (2) / alone (2 = bit 1)
                                               (64, 64, 256, 2, 2, 3), (64, 64, 256, 2, 1, 2), (64, 32, 128, 4, 2, 3),
                                               (64, 32, 64, 8, 1, 2), (64, 64, 128, 4, 2, 2),

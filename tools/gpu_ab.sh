@@ -1,7 +1,10 @@
+# same-box A/B of one environment knob: bash tools/gpu_ab.sh VAR "v1 v2 ..." [bench_ops --only arg]
 set -e
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "aad_layers_v3 or unet or linknet or resnet" > gpurun_out/t_mask.log 2>&1
-timeout -k 10 200 python tools/bench_ops.py --only aadv3 > gpurun_out/aad_m1.log 2>&1
-GHOST_MASK_REG=0 timeout -k 10 200 python tools/bench_ops.py --only aadv3 > gpurun_out/aad_m0.log 2>&1
-GHOST_MASK_REG=0 timeout -k 10 300 python bench.py > gpurun_out/bench_m0.log 2>&1
-timeout -k 10 300 python bench.py > gpurun_out/bench_m1.log 2>&1
+var=$1; vals=$2; only=${3:-aadv3}
+for v in $vals; do
+  env $var=$v timeout -k 10 200 python tools/bench_ops.py --only $only > gpurun_out/ab_ops_$v.log 2>&1
+done
+for v in $vals; do
+  env $var=$v timeout -k 10 300 python bench.py > gpurun_out/ab_bench_$v.log 2>&1
+done
