@@ -51,6 +51,13 @@ struct HaloArgs {
   int tiles_x, tiles_y, nNt, ntiles;
   int dbg;   // experiment mask (GHOST_HALO_DBG): 2 no halo DMA, 4 no weight DMA, 8 no MFMA
   float* in_part;   // pp kernel: InstanceNorm partials [B][tiles/sample][8 waves][N][2] or null
+  // epilogue variants of the non-persistent kernel (IBasicBlock convs, arc_runtime.hip): per-channel
+  // PReLU slope, residual before the activation, second output y2 = v*scale2 + shift2 (next BN)
+  const float* prelu;
+  bf16* y2;
+  const float* scale2;
+  const float* shift2;
+  int ldy2, res_first;
 };
 
 __device__ __attribute__((aligned(16))) unsigned int g_halo_zero[64] = {0};
@@ -160,10 +167,12 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
   }
 
   // epilogue: lane holds channels n0 + 64wn + 16j + 4lq + r of pixel (row RPW*wm + 16i/TW,
-  // column 16i % TW + lr)
+  // column 16i % TW + lr).  Tiles may overhang the image (H or W not a multiple of the tile: the
+  // halo DMA zero-fills outside it); those pixels are computed and dropped here.
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int oy = y0 + wm * RPW + (i * 16) / TW, ox = x0 + (i * 16) % TW + lr;
+    if (oy >= a.H || ox >= a.W) continue;
     const long pix = img + (long)oy * a.W + ox;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -179,11 +188,14 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        // same order as conv_igemm.hip epi_std
         float s = acc[j][i][r];
         if (a.scale) s *= a.scale[n + r];
         if (a.shift) s += a.shift[n + r];
-        s = s > 0.f ? s : s * a.slope;
-        s += rv[r];
+        if (a.res_first) s += rv[r];
+        const float sl = a.prelu ? a.prelu[n + r] : a.slope;
+        s = s > 0.f ? s : s * sl;
+        if (!a.res_first) s += rv[r];
         if (a.tanh_out) s = tanhf(s);
         v[r] = s;
       }
@@ -192,6 +204,11 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int r = 0; r < 4; ++r) oe[r] = (bf16)v[r];
       *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+      if (a.y2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) oe[r] = (bf16)(v[r] * a.scale2[n + r] + a.shift2[n + r]);
+        *reinterpret_cast<uint2*>(a.y2 + pix * a.ldy2 + n) = o;
+      }
     }
   }
 }
@@ -219,15 +236,19 @@ GHOST_DEV void pp_unroll(std::integer_sequence<int, P...>, F&& f) {
   (f(std::integral_constant<int, P>{}), ...);
 }
 
-template <bool RESW, bool STATS, int NCB, int DBG = 0>
-__global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) {
+// G = HaloWide (exact 16 x 32 tiles, the generator) or HaloSmall: 16 x 16 tiles that may overhang
+// the image (ArcFace 112 .. 14), 4 waves, with the IBasicBlock epilogue (per-channel PReLU, residual
+// before or after it, second output y2 = v*scale2 + shift2 = the next block's BatchNorm).
+template <class G, bool RESW, bool STATS, int NCB, int DBG = 0>
+__global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloArgs a) {
   static_assert(NCB % 2 == 0 && NCB <= 32 && (!RESW || NCB == 2), "channel blocks per tile");
+  constexpr bool EPX = G::TW == 16;   // small tiles: overhang masking + the extended epilogue
+  static_assert(!(EPX && STATS), "IN partials only from the exact 16 x 32 tiles");
   // DBG (experiments only, GHOST_HALO_DBG): 2 no halo DMA, 4 no weight DMA, 8 no LDS reads/MFMA,
   // 16 no output stores
   // RESW: Cin <= 64 and N == 64 — the whole weight tensor (<= 2 blocks x 36 KB) stays resident in
   // LDS for the kernel and only the halo (39 KB) streams per stage; otherwise every stage carries
   // its channel block's 9 x 64 weight rows too (75 KB).
-  using G = HaloWide;
   constexpr int TW = G::TW, HWW = G::HWW, HP = G::HP, HPIECES = G::HPIECES, WPIECES = G::WPIECES;
   constexpr int HALO_B = G::HALO_B, NW = G::NW, HPW = G::HPW, WPW = G::WPW, RPW = 64 / TW;
   constexpr int WBLK_B = 9 * 64 * 64;                           // one channel block of weights
@@ -239,12 +260,18 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
   __shared__ __attribute__((aligned(1024))) unsigned char lds1[STAGE_B];
   __shared__ __attribute__((aligned(1024))) unsigned char ldsw[RESW ? 2 * WBLK_B : 16];
   __shared__ float s_sc[512], s_sh[512];
+  __shared__ float s_ex[EPX ? 3 * 512 : 1];   // PReLU slope, scale2, shift2 (EPX)
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
   const int prow = lane >> 2, slot = lane & 3;
 
-  for (int n = tid; n < a.N; n += 512) {
+  for (int n = tid; n < a.N; n += NW * 64) {
     s_sc[n] = a.scale ? a.scale[n] : 1.f;
     s_sh[n] = a.shift ? a.shift[n] : 0.f;
+    if constexpr (EPX) {
+      s_ex[n] = a.prelu ? a.prelu[n] : a.slope;
+      s_ex[512 + n] = a.y2 ? a.scale2[n] : 0.f;
+      s_ex[1024 + n] = a.y2 ? a.shift2[n] : 0.f;
+    }
   }
   constexpr int ncb = NCB;
   // per-lane weight source offsets within a channel block (tap, row) — independent of the tile
@@ -344,7 +371,8 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
   // static.  The first stage of a tile waits vmcnt(NST): the previous tile's NST epilogue stores are
   // the wave's youngest VM ops (VM ops retire in issue order), so the wait covers this stage's DMA
   // without waiting for the stores to reach memory; the later stages wait vmcnt(0).
-  constexpr int NST = (DBG & 16) ? 0 : 16 + (STATS ? 1 : 0);
+  // (EPX: overhang-masked stores may be skipped by a whole wave, so the count is not static: wait for 0)
+  constexpr int NST = ((DBG & 16) || EPX) ? 0 : 16 + (STATS ? 1 : 0);
   if (nmine == 0) return;
   Tile cur = tile_of(0);
   set_dma_tile(cur);
@@ -407,15 +435,24 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
       for (int i = 0; i < 4; ++i) {
         const int oy = cur.y0 + wid * RPW + (i * 16) / TW, ox = cur.x0 + (i * 16) % TW + lr;
         const long pix = cur.base + (long)oy * a.W + ox;
+        const bool in = !EPX || (oy < a.H && ox < a.W);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          rraw[i][j] = *reinterpret_cast<const uint2*>(a.res + pix * a.ldres + cur.n0 + j * 16 + lq * 4);
+          rraw[i][j] = in ? *reinterpret_cast<const uint2*>(a.res + pix * a.ldres + cur.n0 + j * 16 + lq * 4)
+                          : make_uint2(0u, 0u);
       }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int oy = cur.y0 + wid * RPW + (i * 16) / TW, ox = cur.x0 + (i * 16) % TW + lr;
       const long pix = cur.base + (long)oy * a.W + ox;
+      if constexpr (EPX) {
+        if (oy >= a.H || ox >= a.W) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = cur.n0 + j * 16 + lq * 4;
@@ -427,6 +464,27 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
         }
         uint2 o;
         bf16* oe = reinterpret_cast<bf16*>(&o);
+        if constexpr (EPX) {
+          // same order as conv_igemm.hip epi_std
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float t = fmaf(acc[j][i][r], s_sc[n + r], s_sh[n + r]);
+            if (a.res_first) t += rv[r];
+            t = t > 0.f ? t : t * s_ex[n + r];
+            if (!a.res_first) t += rv[r];
+            if (a.tanh_out) t = tanhf(t);
+            v[r] = t;
+            oe[r] = (bf16)t;
+            acc[j][i][r] = 0.f;
+          }
+          *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+          if (a.y2) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) oe[r] = (bf16)(v[r] * s_ex[512 + n + r] + s_ex[1024 + n + r]);
+            *reinterpret_cast<uint2*>(a.y2 + pix * a.ldy2 + n) = o;
+          }
+        } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = fmaf(acc[j][i][r], s_sc[n + r], s_sh[n + r]);
@@ -438,6 +496,7 @@ __global__ void __launch_bounds__(512) conv3x3_halo_pp_kernel(const HaloArgs a) 
         }
         if constexpr (!(DBG & 16)) *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
         else if ((o.x ^ o.y) == 0x7fc00001u) *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+        }
       }
     }
     if constexpr (STATS) {
@@ -711,6 +770,16 @@ int convT_halo(const ConvDesc& d, hipStream_t s) {
   return d.N == 32 ? haloT_launch<32>(d, s) : haloT_launch<64>(d, s);
 }
 
+// which tile the non-persistent kernel uses: 16 x 32 when the image is a multiple of it (every
+// generator stage from 32x32 up), else 16 x 16 tiles allowed to overhang the image by up to a
+// quarter of the work (ArcFace 112 / 56 / 28 / 14: 100 / 77 / 77 / 77 % of the tile pixels used;
+// 7x7 and the generator's 8x8 and below stay on the implicit GEMM)
+static bool halo_exact_wide(const ConvDesc& d) { return d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0; }
+static bool halo_small_ok(const ConvDesc& d) {
+  const long tx = (d.Wi + HaloSmall::TW - 1) / HaloSmall::TW, ty = (d.Hi + HaloSmall::TH - 1) / HaloSmall::TH;
+  return 4L * d.Hi * d.Wi >= 3L * tx * ty * HaloSmall::TW * HaloSmall::TH;
+}
+
 bool conv3x3_halo_supported(const ConvDesc& d) {
   static const int enabled = [] {
     const char* e = getenv("GHOST_CONV_HALO");
@@ -718,11 +787,9 @@ bool conv3x3_halo_supported(const ConvDesc& d) {
   }();
   if (!enabled || d.kind != CONV_FWD || d.kh != 3 || d.kw != 3 || d.stride != 1 || d.pad != 1) return false;
   if (d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD || d.u8 || d.force_split) return false;
-  if (d.res_first || d.prelu || d.y2) return false;   // epilogue variants only the implicit GEMM has
   if (d.Cin % 32 || d.ldx % 8 || d.N % 64 || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
-  const bool wide = d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0;
-  const bool small = d.Wi == HaloSmall::TW && d.Hi % HaloSmall::TH == 0;
-  if ((!wide && !small) || d.Kpad < 9 * d.Cin || d.Npad < d.N) return false;
+  if (d.y2 && (d.ldy2 % 4 || (uintptr_t)d.y2 % 8 || !d.scale2 || !d.shift2)) return false;
+  if ((!halo_exact_wide(d) && !halo_small_ok(d)) || d.Kpad < 9 * d.Cin || d.Npad < d.N) return false;
   if ((uintptr_t)d.x % 16 || (uintptr_t)d.w % 16 || (uintptr_t)d.y % 8 || (d.res && (uintptr_t)d.res % 8)) return false;
   if ((long)d.Hi * d.Wi * d.ldx >= (1L << 31) || (long)d.Npad * d.Kpad >= (1L << 31)) return false;   // 32-bit offsets
   // measured (tools/bench_ops.py, B = 64): faster than the implicit GEMM at every generator stage
@@ -741,7 +808,10 @@ static int halo_launch(const ConvDesc& d, hipStream_t s) {
   a.scale = d.scale; a.shift = d.shift; a.res = (const bf16*)d.res;
   a.H = d.Hi; a.W = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx; a.N = d.N; a.Kpad = d.Kpad;
   a.ldy = d.ldy; a.ldres = d.ldres; a.tanh_out = d.tanh_out; a.slope = d.slope;
-  a.tiles_x = d.Wi / G::TW; a.tiles_y = d.Hi / G::TH; a.nNt = (d.N + G::BN - 1) / G::BN;
+  a.prelu = d.prelu; a.y2 = (bf16*)d.y2; a.scale2 = d.scale2; a.shift2 = d.shift2; a.ldy2 = d.ldy2;
+  a.res_first = d.res_first;
+  a.tiles_x = (d.Wi + G::TW - 1) / G::TW; a.tiles_y = (d.Hi + G::TH - 1) / G::TH;
+  a.nNt = (d.N + G::BN - 1) / G::BN;
   a.ntiles = d.B * a.tiles_x * a.tiles_y * a.nNt;
   hipLaunchKernelGGL(conv3x3_halo_kernel<G>, dim3((unsigned)a.ntiles), dim3(G::NW * 64), 0, s, a);
   return (int)hipGetLastError();
@@ -758,13 +828,28 @@ static int num_cus() {
   return n;
 }
 
+// the persistent kernel takes 16 x 16 tiles (HaloSmall) for images that are not a multiple of 16 x 32
+// (ArcFace 112 .. 14, overhanging tiles) — or, with GHOST_HALO_PP_SMALL=1, also the generator's
+// 16 x 16 stage (A/B knob)
+static bool pp_small(const ConvDesc& d) {
+  static const int force = [] {
+    const char* e = getenv("GHOST_HALO_PP_SMALL");
+    return e ? atoi(e) : 0;
+  }();
+  return !halo_exact_wide(d) && halo_small_ok(d) &&
+         (force || d.Wi % HaloSmall::TW || d.Hi % HaloSmall::TH || d.prelu || d.y2 || d.res_first);
+}
+
+template <class G>
 static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   HaloArgs a{};
   a.x = (const bf16*)d.x; a.w = (const bf16*)d.w; a.y = (bf16*)d.y;
   a.scale = d.scale; a.shift = d.shift; a.res = (const bf16*)d.res;
   a.H = d.Hi; a.W = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx; a.N = d.N; a.Kpad = d.Kpad;
   a.ldy = d.ldy; a.ldres = d.ldres; a.tanh_out = d.tanh_out; a.slope = d.slope;
-  a.tiles_x = d.Wi / HaloWide::TW; a.tiles_y = d.Hi / HaloWide::TH; a.nNt = d.N / 64;
+  a.prelu = d.prelu; a.y2 = (bf16*)d.y2; a.scale2 = d.scale2; a.shift2 = d.shift2; a.ldy2 = d.ldy2;
+  a.res_first = d.res_first;
+  a.tiles_x = (d.Wi + G::TW - 1) / G::TW; a.tiles_y = (d.Hi + G::TH - 1) / G::TH; a.nNt = d.N / 64;
   a.ntiles = d.B * a.tiles_x * a.tiles_y * a.nNt;
   static const int dbg = [] {
     const char* e = getenv("GHOST_HALO_DBG");
@@ -775,32 +860,43 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   a.in_part = d.in_part;
   const bool resw = d.Cin <= 64 && d.N == 64;
   const int ncb = d.Cin / 32;
-  if (dbg && !a.in_part) {   // experiment variants
-#define GHOST_PP_DBG(R, NB, V)                                                                              \
-  if (resw == R && ncb == NB && dbg == V) {                                                                \
-    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<R, false, NB, V>), dim3((unsigned)g), dim3(512), 0, s, a); \
-    return (int)hipGetLastError();                                                                         \
+  constexpr int NT = G::NW * 64;
+  if constexpr (G::TW == 32) {
+    if (dbg && !a.in_part) {   // experiment variants
+#define GHOST_PP_DBG(R, NB, V)                                                                               \
+  if (resw == R && ncb == NB && dbg == V) {                                                                 \
+    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<G, R, false, NB, V>), dim3((unsigned)g), dim3(NT), 0, s, a); \
+    return (int)hipGetLastError();                                                                          \
   }
-    GHOST_PP_DBG(true, 2, 2) GHOST_PP_DBG(true, 2, 8) GHOST_PP_DBG(true, 2, 16) GHOST_PP_DBG(true, 2, 18)
-    GHOST_PP_DBG(false, 4, 6) GHOST_PP_DBG(false, 4, 8) GHOST_PP_DBG(false, 4, 16) GHOST_PP_DBG(false, 4, 22)
+      GHOST_PP_DBG(true, 2, 2) GHOST_PP_DBG(true, 2, 8) GHOST_PP_DBG(true, 2, 16) GHOST_PP_DBG(true, 2, 18)
+      GHOST_PP_DBG(false, 4, 6) GHOST_PP_DBG(false, 4, 8) GHOST_PP_DBG(false, 4, 16) GHOST_PP_DBG(false, 4, 22)
 #undef GHOST_PP_DBG
+    }
   }
+  constexpr bool CAN_ST = G::TW == 32;
 #define GHOST_PP(R, ST, NB) \
-  hipLaunchKernelGGL((conv3x3_halo_pp_kernel<R, ST, NB>), dim3((unsigned)g), dim3(512), 0, s, a)
-  const bool st = a.in_part != nullptr;
+  hipLaunchKernelGGL((conv3x3_halo_pp_kernel<G, R, ST, NB>), dim3((unsigned)g), dim3(NT), 0, s, a)
+#define GHOST_PP2(R, NB)                                  \
+  if constexpr (CAN_ST) {                                  \
+    if (a.in_part) GHOST_PP(R, CAN_ST, NB); else GHOST_PP(R, false, NB); \
+  } else {                                                 \
+    if (a.in_part) return -1;                              \
+    GHOST_PP(R, false, NB);                                \
+  }
   if (resw) {
-    if (st) GHOST_PP(true, true, 2); else GHOST_PP(true, false, 2);
+    GHOST_PP2(true, 2)
   } else {
     switch (ncb) {
-      case 2: if (st) GHOST_PP(false, true, 2); else GHOST_PP(false, false, 2); break;
-      case 4: if (st) GHOST_PP(false, true, 4); else GHOST_PP(false, false, 4); break;
-      case 6: if (st) GHOST_PP(false, true, 6); else GHOST_PP(false, false, 6); break;
-      case 8: if (st) GHOST_PP(false, true, 8); else GHOST_PP(false, false, 8); break;
-      case 16: if (st) GHOST_PP(false, true, 16); else GHOST_PP(false, false, 16); break;
-      case 32: if (st) GHOST_PP(false, true, 32); else GHOST_PP(false, false, 32); break;
+      case 2: GHOST_PP2(false, 2) break;
+      case 4: GHOST_PP2(false, 4) break;
+      case 6: GHOST_PP2(false, 6) break;
+      case 8: GHOST_PP2(false, 8) break;
+      case 16: GHOST_PP2(false, 16) break;
+      case 32: GHOST_PP2(false, 32) break;
       default: return -1;
     }
   }
+#undef GHOST_PP2
 #undef GHOST_PP
   return (int)hipGetLastError();
 }
@@ -811,7 +907,8 @@ bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
     return e ? atoi(e) : 1;
   }();
   if (!conv3x3_halo_supported(d)) return false;
-  const bool wide = d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0;
+  if (d.prelu || d.y2 || d.res_first) return false;   // epilogue variants of the non-persistent kernel only
+  const bool wide = halo_exact_wide(d);
   static const int max_cin = [] {
     const char* e = getenv("GHOST_HALO_PP_MAXCIN");
     return e ? atoi(e) : 1024;
@@ -827,10 +924,17 @@ bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
 
 int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
   if (!conv3x3_halo_supported(d)) return -1;
-  const bool wide = d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0;
-  if (conv3x3_pp_takes(d, nullptr)) return halo_pp_launch(d, s);
-  if (d.in_part) return -1;   // only the persistent kernel writes InstanceNorm partials
-  if (wide) return halo_launch<HaloWide>(d, s);
+  if (conv3x3_pp_takes(d, nullptr)) return halo_pp_launch<HaloWide>(d, s);
+  if (d.in_part) return -1;   // only the persistent 16 x 32 kernel writes InstanceNorm partials
+  static const int pp = [] {
+    const char* e = getenv("GHOST_HALO_PP");
+    return e ? atoi(e) : 1;
+  }();
+  const int ncb = d.Cin / 32;
+  if (pp && pp_small(d) && d.N <= 512 && d.Cin % 64 == 0 &&
+      (ncb == 2 || ncb == 4 || ncb == 6 || ncb == 8 || ncb == 16 || ncb == 32))
+    return halo_pp_launch<HaloSmall>(d, s);
+  if (halo_exact_wide(d)) return halo_launch<HaloWide>(d, s);
   return halo_launch<HaloSmall>(d, s);
 }
 

@@ -112,6 +112,14 @@ def test_conv2d_op(lib, dt, cin, cout, k, s, p, H):
     (32, 32, 128, 1, 1, 0, 16, "res_relu"),   # Bottleneck tail relu(bn3(conv3) + residual)
     (64, 64, 64, 3, 1, 1, 28, "prelu_y2"),    # IBasicBlock conv + BN + PReLU, with a BN'd second output
     (64, 64, 128, 3, 2, 1, 28, "res_y2"),     # IBasicBlock conv2/s2 + BN + residual, second output = next BN
+    # 3x3/s1 shapes the halo kernel takes in bf16 with overhanging 16x16 tiles (ArcFace stages)
+    (64, 64, 64, 3, 1, 1, 112, "prelu_y2"),   # layer1 block-0 conv1 at 112x112 (7 x 7 exact tiles)
+    (64, 64, 128, 3, 1, 1, 56, "prelu_y2"),   # layer2 block-0 conv1 at 56x56
+    (128, 128, 128, 3, 1, 1, 28, "res_y2"),   # layer2 conv2 + residual + next BN
+    (256, 256, 256, 3, 1, 1, 14, "prelu_y2"), # layer3 conv1
+    (256, 256, 256, 3, 1, 1, 14, "res_y2"),   # layer3 conv2
+    (64, 64, 64, 3, 1, 1, 48, "res_relu"),    # residual before the activation on the halo path
+    (512, 512, 512, 3, 1, 1, 7, "res_y2"),    # 7x7 stays on the implicit GEMM
 ])
 def test_conv2d_ex_epilogues(lib, dt, cin, ldx, cout, k, s, p, H, mode):
     """ghost_conv2d_ex_nhwc: residual-before-activation, per-channel PReLU and the dual output."""
