@@ -218,37 +218,44 @@ in_stats_final_kernel(const T* __restrict__ x, int ldx, long bstride, int B, int
   stat[(long)i * 2 + 1] = (float)(1.0 / sqrt(var + (double)kInEps));
 }
 
-// records [B][nrec][C][2] = (mean, centred sum of squares) over 64 pixels each.  Grid (C/16, B), 256
-// threads = 16 channels x 16 record lanes; fp64 sums, reduced across the record lanes in LDS.
-__global__ void __launch_bounds__(256)
+// records [B][nrec][C][2] = (mean, centred sum of squares) over 64 pixels each.  Grid (C/16, B),
+// 16 channels x RL record lanes; fp64 sums, reduced across the record lanes in LDS.  (RL = 64 for
+// the 256x256 stage's 1024 records per channel: 256 threads took 42 us there, latency-bound on
+// 64 serial loads per thread.)
+template <int RL>
+__global__ void __launch_bounds__(16 * RL)
 in_stats_tiles_final_kernel(const float* __restrict__ part, int nrec, int C, float* __restrict__ stat) {
-  __shared__ double r1[16][17], r2[16][17];
+  __shared__ double r1[RL][17], r2[RL][17];
   const int b = blockIdx.y, cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   // pass 1: mean of the record means (equal counts); pass 2: Chan's M2 = sum M2_r + 64 (m_r - mean)^2
   const float* base = part + ((long)b * nrec * C + c) * 2;
   double s1 = 0.0;
-  if (c < C)
-    for (int k = rl; k < nrec; k += 16) s1 += (double)base[(long)k * C * 2];
+  if (c < C) {
+#pragma unroll 4
+    for (int k = rl; k < nrec; k += RL) s1 += (double)base[(long)k * C * 2];
+  }
   r1[rl][cl] = s1;
   __syncthreads();
   double mean = 0.0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) mean += r1[k][cl];
+  for (int k = 0; k < RL; ++k) mean += r1[k][cl];
   mean /= nrec;
   double m2 = 0.0;
-  if (c < C)
-    for (int k = rl; k < nrec; k += 16) {
+  if (c < C) {
+#pragma unroll 4
+    for (int k = rl; k < nrec; k += RL) {
       const float2 v = *reinterpret_cast<const float2*>(base + (long)k * C * 2);
       const double d = (double)v.x - mean;
       m2 += (double)v.y + 64.0 * d * d;
     }
+  }
   r2[rl][cl] = m2;
   __syncthreads();
   if (rl == 0 && c < C) {
     double t2 = 0.0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) t2 += r2[k][cl];
+    for (int k = 0; k < RL; ++k) t2 += r2[k][cl];
     const double var = t2 / (64.0 * nrec);
     stat[((long)b * C + c) * 2 + 0] = (float)mean;
     stat[((long)b * C + c) * 2 + 1] = (float)(1.0 / sqrt(var + (double)kInEps));
@@ -257,7 +264,10 @@ in_stats_tiles_final_kernel(const float* __restrict__ part, int nrec, int C, flo
 
 int in_stats_from_tiles(const float* part, int B, int nrec, int C, float* stat, hipStream_t s) {
   if (!part || !stat || B <= 0 || nrec <= 0 || C <= 0 || B > 65535) return -1;
-  hipLaunchKernelGGL(in_stats_tiles_final_kernel, dim3((C + 15) / 16, B), dim3(256), 0, s, part, nrec, C, stat);
+  if (nrec >= 512)
+    hipLaunchKernelGGL(in_stats_tiles_final_kernel<64>, dim3((C + 15) / 16, B), dim3(1024), 0, s, part, nrec, C, stat);
+  else
+    hipLaunchKernelGGL(in_stats_tiles_final_kernel<16>, dim3((C + 15) / 16, B), dim3(256), 0, s, part, nrec, C, stat);
   return (int)hipGetLastError();
 }
 
