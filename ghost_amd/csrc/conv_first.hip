@@ -86,14 +86,15 @@ struct FirstMfmaArgs {
   long M;
 };
 
+// each wave walks kFirstChunks runs of 64 output pixels: the weight fragments (32 gathered bf16 per
+// lane) and the BN scale/shift are set up once per wave, not once per 64 pixels (measured 81 us at
+// 256x256, B = 64, with one run per wave: 1.2 TB/s for a 100 MB HBM kernel)
+constexpr int kFirstChunks = 4;
+
 __global__ void __launch_bounds__(256) conv_first_mfma_kernel(const FirstMfmaArgs a) {
   const int lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
-  const long m0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;   // 64 pixels of one output row
-  if (m0 >= a.M) return;
-  const int hw = a.Ho * a.Wo;
-  const int b = (int)(m0 / hw);
-  const int r0 = (int)(m0 - (long)b * hw);
-  const int oy = r0 / a.Wo, ox0 = r0 - oy * a.Wo;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wave * kFirstChunks * 64 >= a.M) return;
   // A fragments: channel rows n = 16j + lr, K = 32s + 8lq + e -> (ky, kx, c4) = (K/16, K/4 % 4, K % 4)
   bf16x8 wf[2][2];
 #pragma unroll
@@ -108,6 +109,22 @@ __global__ void __launch_bounds__(256) conv_first_mfma_kernel(const FirstMfmaArg
       }
       __builtin_memcpy(&wf[j][s], e8, 16);
     }
+  float sc[2][4], sh[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = j * 16 + lq * 4 + r;
+      sc[j][r] = a.scale ? a.scale[n] : 1.f;
+      sh[j][r] = a.shift ? a.shift[n] : 0.f;
+    }
+  const int hw = a.Ho * a.Wo;
+  for (int ch = 0; ch < kFirstChunks; ++ch) {
+  const long m0 = (wave * kFirstChunks + ch) * 64;   // 64 pixels of one output row
+  if (m0 >= a.M) break;
+  const int b = (int)(m0 / hw);
+  const int r0 = (int)(m0 - (long)b * hw);
+  const int oy = r0 / a.Wo, ox0 = r0 - oy * a.Wo;
   const bf16* xb = a.x + (long)b * a.Hi * a.Wi * 4;
   f32x4 acc[2][4];
 #pragma unroll
@@ -142,13 +159,12 @@ __global__ void __launch_bounds__(256) conv_first_mfma_kernel(const FirstMfmaArg
       bf16* oe = reinterpret_cast<bf16*>(&o);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = acc[j][i][r];
-        if (a.scale) v *= a.scale[n + r];
-        if (a.shift) v += a.shift[n + r];
+        const float v = fmaf(acc[j][i][r], sc[j][r], sh[j][r]);
         oe[r] = (bf16)(v > 0.f ? v : v * a.slope);
       }
       *reinterpret_cast<uint2*>(a.y + m * a.ldy + n) = o;
     }
+  }
   }
 }
 
@@ -175,7 +191,7 @@ int conv_first(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t s) {
     m.x = (const bf16*)d.x; m.w = (const bf16*)d.w; m.y = (bf16*)d.y; m.scale = d.scale; m.shift = d.shift;
     m.Hi = d.Hi; m.Wi = d.Wi; m.Ho = Ho; m.Wo = Wo; m.Kpad = d.Kpad; m.ldy = d.ldy; m.slope = d.slope;
     m.M = (long)d.B * Ho * Wo;
-    hipLaunchKernelGGL(conv_first_mfma_kernel, dim3((unsigned)((m.M / 64 + 3) / 4)), dim3(256), 0, s, m);
+    hipLaunchKernelGGL(conv_first_mfma_kernel, dim3((unsigned)(((m.M / 64 + kFirstChunks - 1) / kFirstChunks + 3) / 4)), dim3(256), 0, s, m);
     return (int)hipGetLastError();
   }
   if (!ws || ws_bytes < conv_first_workspace_bytes() || (uintptr_t)ws % 16) return -1;
