@@ -162,16 +162,20 @@ def main():
     rng = np.random.Generator(np.random.PCG64(1000 + rank))
     crops = torch.from_numpy(rng.integers(0, 256, size=(B, 256, 256, 3), dtype=np.uint8)).to(dev)
     z = torch.from_numpy(np.random.Generator(np.random.PCG64(1)).normal(size=(1, 512)).astype(np.float32)).to(dev)
-    out = torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev)
-    gathered = torch.empty(world * B, 256, 256, 3, dtype=torch.uint8, device=dev) if world > 1 else None
+    # swap -> all-gather of the uint8 swaps to every rank; the gather of step k overlaps step k + 1
+    # (dp.GatherPipeline; GHOST_DP_OVERLAP=0 gathers synchronously after each step)
+    from ghost_amd.inference.dp import GatherPipeline
+    pipe = GatherPipeline(lambda c, o: G.swap_u8(c, z, out=o), (B, 256, 256, 3), dev,
+                          depth=2 if os.environ.get("GHOST_DP_OVERLAP", "1") != "0" else 1)
 
     def step():
-        G.swap_u8(crops, z, out=out)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+        slot = pipe.submit(crops)
+        if pipe.depth == 1:
+            pipe.result(slot)
 
     for _ in range(a.warmup):
         step()
+    pipe.drain()
     torch.cuda.synchronize()
     prof = not a.no_profile
     names = ["aad_all", "aad_dual_256", "conv3x3_all", "conv3x3_256", "in_stats_mask", "encoder", "upsample",
@@ -187,6 +191,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    pipe.drain()                  # every step's all-gather is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   __shared__ __attribute__((aligned(1024))) unsigned char lds0[STAGE_B];
   __shared__ __attribute__((aligned(1024))) unsigned char lds1[STAGE_B];
   __shared__ __attribute__((aligned(1024))) unsigned char ldsw[RESW ? 2 * WBLK_B : 16];
-  __shared__ float s_sc[512], s_sh[512];
+  __shared__ float s_sc[512], s_sh[512];   // N <= 512 (conv3x3_pp_takes / conv3x3_halo)
   __shared__ float s_ex[EPX ? 3 * 512 : 1];   // PReLU slope, scale2, shift2 (EPX)
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
   const int prow = lane >> 2, slot = lane & 3;
@@ -917,7 +917,7 @@ bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
   // -23 %, 128x128: -7 %, 64x64 256->256: -9 %; with the counted first-stage wait also 64x64 512->128
   // -11 %, 32x32 512->512 -6 %, 32x32 1024->256 -8 %: +3 % frames/s end to end)
   const bool cin_ok = d.Cin == 64 || d.Cin == 128 || d.Cin == 192 || d.Cin == 256 || d.Cin == 512 || d.Cin == 1024;
-  const bool ok = wide && pp && d.N <= 1024 && d.N % 64 == 0 && cin_ok && d.Cin <= max_cin && !d.tanh_out;
+  const bool ok = wide && pp && d.N <= 512 && d.N % 64 == 0 && cin_ok && d.Cin <= max_cin && !d.tanh_out;
   if (ok && nrec) *nrec = (d.Hi / HaloWide::TH) * (d.Wi / HaloWide::TW) * 8;
   return ok;
 }

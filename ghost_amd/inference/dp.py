@@ -77,3 +77,54 @@ def swap_mixed_identities(crops: torch.Tensor, identity_index: torch.Tensor, sou
     (fc1/fc2 per sample, AADLayer.py:28-29) handles the mix in one launch sequence."""
     z = source_embeds.reshape(source_embeds.shape[0], -1).index_select(0, identity_index.to(source_embeds.device))
     return G.swap_u8(crops, z, out=out)
+
+
+class GatherPipeline:
+    """A stream of per-rank batches, each swapped on this GPU and then all-gathered to every rank,
+    with the all-gather of batch k in flight (RCCL's own stream, over xGMI) while batch k+1 is
+    swapped.  ``depth`` output/gather buffer pairs rotate; a slot's previous all-gather is waited on
+    (stream-ordered for RCCL: ``Work.wait()`` makes the compute stream wait, the host does not block)
+    before the swap overwrites it, so no batch's bytes change while a collective reads them.
+
+    ``swap(crops, out)`` writes the uint8 swaps of ``crops`` into ``out`` (``AEI_Net.swap_u8``).
+    ``submit`` returns the slot whose ``result`` is the gathered [world * B, ...] batch in rank order.
+    """
+
+    def __init__(self, swap: Callable, batch_shape, device, dtype=torch.uint8, group=None, depth: int = 2):
+        self.swap, self.group, self.depth = swap, group, max(1, depth)
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.nccl = self.world > 1 and dist.get_backend(group) == "nccl"
+        shape = tuple(batch_shape)
+        self.outs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(self.depth)]
+        self.gath = ([torch.empty((self.world * shape[0],) + shape[1:], dtype=dtype, device=device)
+                      for _ in range(self.depth)] if self.world > 1 else self.outs)
+        self.pending: List[Optional[object]] = [None] * self.depth
+        self.k = 0
+
+    def _wait(self, slot: int):
+        w = self.pending[slot]
+        if w is not None:
+            w.wait()
+            self.pending[slot] = None
+
+    def submit(self, crops: torch.Tensor) -> int:
+        slot = self.k % self.depth
+        self._wait(slot)                      # the collective still reading this slot's buffer
+        self.swap(crops, self.outs[slot])
+        if self.world > 1:
+            if self.nccl:
+                self.pending[slot] = dist.all_gather_into_tensor(self.gath[slot], self.outs[slot], group=self.group,
+                                                                 async_op=True)
+            else:
+                self.pending[slot] = dist.all_gather(list(self.gath[slot].chunk(self.world)), self.outs[slot],
+                                                     group=self.group, async_op=True)
+        self.k += 1
+        return slot
+
+    def result(self, slot: int) -> torch.Tensor:
+        self._wait(slot)
+        return self.gath[slot]
+
+    def drain(self):
+        for s in range(self.depth):
+            self._wait(s)

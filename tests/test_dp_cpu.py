@@ -59,6 +59,54 @@ def test_swap_frames_dp_gloo_order(world, n, bs):
         assert np.array_equal(results[r], expect), r
 
 
+def _pipe_worker(rank, world, port, depth, q):
+    from ghost_amd.inference.dp import GatherPipeline
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B = 3
+        pipe = GatherPipeline(lambda c, o: o.copy_(fake_swap(c)), (B, 4, 4, 3), torch.device("cpu"), depth=depth)
+        batches = [torch.full((B, 4, 4, 3), 10 * k + rank, dtype=torch.uint8) + torch.arange(B, dtype=torch.uint8)
+                   .view(B, 1, 1, 1) for k in range(5)]
+        got, prev = [], None
+        for k, bt in enumerate(batches):
+            slot = pipe.submit(bt)
+            if prev is not None:      # batch k-1's gather, read while batch k's is in flight
+                got.append(pipe.result(prev).clone())
+            prev = slot
+        got.append(pipe.result(prev).clone())
+        pipe.drain()
+        q.put((rank, [g.numpy() for g in got]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_gather_pipeline_gloo(depth):
+    """dp.GatherPipeline (bench.py's swap -> all-gather stream): batch k's gathered swaps, in rank
+    order, on every rank, with batch k+1 submitted before batch k is read."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, depth, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    B = 3
+    for k in range(5):
+        expect = torch.cat([fake_swap(torch.full((B, 4, 4, 3), 10 * k + r, dtype=torch.uint8)
+                                      + torch.arange(B, dtype=torch.uint8).view(B, 1, 1, 1)) for r in range(world)])
+        for r in range(world):
+            if depth == 1 and k < 4:
+                continue      # depth 1 reuses the slot: only the last batch is still readable
+            assert np.array_equal(results[r][k], expect.numpy()), (r, k)
+
+
 def test_shard_bounds_partition():
     for n in range(0, 40):
         for world in (1, 2, 3, 8):
