@@ -215,4 +215,159 @@ int conv_first(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// ArcFace stem: Conv2d(3, 64, 3, s1, p1) + BN + PReLU (+ the next block's BN as a second output),
+// on the same 4-channel (RGB + zero) input layout (arc_runtime.hip: stem).  K = 9 taps x 4 channels
+// = 36, two MFMA k-steps (taps 8s + 2lq, +1 per lane; taps >= 9 are zero): a lane's 8 K values are
+// two taps of one output pixel, gathered as two 8-byte pixel loads.  The implicit GEMM takes this
+// shape on its scalar-gather path (Cin = 3): 127 us at B = 64 for 12 MB read + 206 MB written.
+// ---------------------------------------------------------------------------
+struct StemArgs {
+  const bf16* x;      // [B][H][W][4]
+  const bf16* w;      // packed [Npad][Kpad], K = (ky*3 + kx)*3 + c
+  bf16* y;
+  bf16* y2;
+  const float* scale;
+  const float* shift;
+  const float* prelu;
+  const float* scale2;
+  const float* shift2;
+  int H, W, Kpad, ldy, ldy2;
+  float slope;
+  int M;
+};
+
+constexpr int kStemChunks = 4;
+
+__global__ void __launch_bounds__(256) conv_stem3x3_kernel(const StemArgs a) {
+  const int lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // the 64 x 27 weights and the five per-channel tables, staged once per workgroup (the per-lane
+  // gathers of the fragments below then hit LDS, not 64 scattered global loads per lane)
+  __shared__ bf16 s_w[64 * 28];
+  __shared__ float s_t[5][64];
+  for (int i = threadIdx.x; i < 64 * 28; i += 256) {
+    const int n = i / 28, k = i - n * 28;
+    s_w[i] = k < 27 ? a.w[(long)n * a.Kpad + k] : (bf16)0.f;
+  }
+  if (threadIdx.x < 64) {
+    const int n = threadIdx.x;
+    s_t[0][n] = a.scale ? a.scale[n] : 1.f;
+    s_t[1][n] = a.shift ? a.shift[n] : 0.f;
+    s_t[2][n] = a.prelu ? a.prelu[n] : a.slope;
+    s_t[3][n] = a.y2 ? a.scale2[n] : 0.f;
+    s_t[4][n] = a.y2 ? a.shift2[n] : 0.f;
+  }
+  __syncthreads();
+  if (wave * kStemChunks * 64 >= a.M) return;
+  // A fragments: rows n = 16j + lr; K = 32s + 8lq + e -> tap = 8s + 2lq + (e >> 2), c = e & 3
+  bf16x8 wf[4][2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16 e8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int tap = 8 * s + 2 * lq + (e >> 2), c = e & 3;
+        e8[e] = (tap < 9 && c < 3) ? s_w[(j * 16 + lr) * 28 + tap * 3 + c] : (bf16)0.f;
+      }
+      __builtin_memcpy(&wf[j][s], e8, 16);
+    }
+  // this lane's 4 channels of each j: n = 16j + 4lq + r
+  float sc[4][4], sh[4][4], pr[4][4], sc2[4][4], sh2[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = j * 16 + lq * 4 + r;
+      sc[j][r] = s_t[0][n];
+      sh[j][r] = s_t[1][n];
+      pr[j][r] = s_t[2][n];
+      sc2[j][r] = s_t[3][n];
+      sh2[j][r] = s_t[4][n];
+    }
+  // 32-bit pixel indices (M < 2^31, checked on the host): a 64-bit division per lane and fragment
+  // cost more than the MFMAs
+  const int hw = a.H * a.W;
+  for (int ch = 0; ch < kStemChunks; ++ch) {
+    const int m0 = (int)((wave * kStemChunks + ch) * 64);
+    if (m0 >= a.M) break;
+    const int b0 = m0 / hw, rb = m0 - b0 * hw;       // a 64-pixel chunk spans at most two samples
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + i * 16 + lr;                // this lane's B-fragment pixel
+      const bool mok = m < a.M;
+      int r0 = rb + i * 16 + lr, b = b0;
+      if (r0 >= hw) { r0 -= hw; ++b; }
+      const int oy = r0 / a.W, ox = r0 - oy * a.W;
+      const bf16* xb = a.x + (long)b * hw * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        uint2 p[2] = {{0u, 0u}, {0u, 0u}};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int tap = 8 * s + 2 * lq + h;
+          const int iy = oy + tap / 3 - 1, ix = ox + tap % 3 - 1;
+          if (mok && tap < 9 && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+            p[h] = *reinterpret_cast<const uint2*>(xb + ((long)iy * a.W + ix) * 4);
+        }
+        const u32x4 raw = {p[0].x, p[0].y, p[1].x, p[1].y};
+        bf16x8 bfrag;
+        __builtin_memcpy(&bfrag, &raw, 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], bfrag, acc[j][i], 0, 0, 0);
+      }
+    }
+    // epilogue (conv_igemm.hip epi_std / store_std order): v = acc*scale + shift, PReLU, y = v,
+    // y2 = v*scale2 + shift2; lane holds channels 16j + 4lq + r of pixel m0 + 16i + lr
+    // (measured: staging the tile through LDS for whole-row stores is slower, 95 vs 88 us)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + i * 16 + lr;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = j * 16 + lq * 4;
+        uint2 o, o2;
+        bf16* oe = reinterpret_cast<bf16*>(&o);
+        bf16* oe2 = reinterpret_cast<bf16*>(&o2);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = fmaf(acc[j][i][r], sc[j][r], sh[j][r]);
+          v = v > 0.f ? v : v * pr[j][r];
+          oe[r] = (bf16)v;
+          oe2[r] = (bf16)(v * sc2[j][r] + sh2[j][r]);
+        }
+        *reinterpret_cast<uint2*>(a.y + (long)m * a.ldy + n) = o;
+        if (a.y2) *reinterpret_cast<uint2*>(a.y2 + (long)m * a.ldy2 + n) = o2;
+      }
+    }
+  }
+}
+
+bool conv_stem3x3_supported(const ConvDesc& d) {
+  return d.kind == CONV_FWD && d.kh == 3 && d.kw == 3 && d.stride == 1 && d.pad == 1 && d.Cin == 3 && d.ldx == 4 &&
+         d.N == 64 && d.ti == GHOST_BF16 && d.to == GHOST_BF16 && d.epi == EPI_STD && !d.res && !d.res_first &&
+         !d.tanh_out && !d.u8 && !d.force_split && d.Kpad >= 27 && d.Npad >= 64 && d.ldy % 4 == 0 &&
+         (uintptr_t)d.x % 8 == 0 && (uintptr_t)d.y % 8 == 0 && (long)d.B * d.Hi * d.Wi < (1L << 30) &&
+         (!d.y2 || (d.scale2 && d.shift2 && d.ldy2 % 4 == 0 && (uintptr_t)d.y2 % 8 == 0));
+}
+
+int conv_stem3x3(const ConvDesc& d, hipStream_t s) {
+  if (!conv_stem3x3_supported(d)) return -1;
+  StemArgs a{};
+  a.x = (const bf16*)d.x; a.w = (const bf16*)d.w; a.y = (bf16*)d.y; a.y2 = (bf16*)d.y2;
+  a.scale = d.scale; a.shift = d.shift; a.prelu = d.prelu; a.scale2 = d.scale2; a.shift2 = d.shift2;
+  a.H = d.Hi; a.W = d.Wi; a.Kpad = d.Kpad; a.ldy = d.ldy; a.ldy2 = d.ldy2; a.slope = d.slope;
+  a.M = d.B * d.Hi * d.Wi;
+  const long waves = ((long)(a.M + 63) / 64 + kStemChunks - 1) / kStemChunks;
+  hipLaunchKernelGGL(conv_stem3x3_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
 }  // namespace ghost

@@ -760,7 +760,7 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
 }  // namespace
 
 size_t conv_workspace_bytes(const ConvDesc& d) {
-  if (conv3x3_halo_supported(d) || convT_halo_supported(d)) return 0;
+  if (conv3x3_halo_supported(d) || convT_halo_supported(d) || conv_stem3x3_supported(d)) return 0;
   if (conv_first_supported(d)) return conv_first_workspace_bytes();
   Plan p = make_plan(d);
   if (!p.partial) return 0;
@@ -776,6 +776,7 @@ int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream
     return -1;
   if (conv3x3_halo_supported(d)) return conv3x3_halo(d, stream);
   if (conv_first_supported(d)) return conv_first(d, ws, ws_bytes, stream);
+  if (conv_stem3x3_supported(d)) return conv_stem3x3(d, stream);
   if (convT_halo_supported(d)) return convT_halo(d, stream);
   Plan p = make_plan(d);
   if (p.NT > d.Npad) return -1;  // weight rows read by the last tile must exist

@@ -120,6 +120,8 @@ def test_conv2d_op(lib, dt, cin, cout, k, s, p, H):
     (256, 256, 256, 3, 1, 1, 14, "res_y2"),   # layer3 conv2
     (64, 64, 64, 3, 1, 1, 48, "res_relu"),    # residual before the activation on the halo path
     (512, 512, 512, 3, 1, 1, 7, "res_y2"),    # 7x7 stays on the implicit GEMM
+    (3, 4, 64, 3, 1, 1, 112, "prelu_y2"),     # ArcFace stem (bf16: the 4-channel MFMA stem kernel)
+    (3, 4, 64, 3, 1, 1, 9, "prelu_y2"),       # stem with a partial last 64-pixel chunk (B*81 = 162)
 ])
 def test_conv2d_ex_epilogues(lib, dt, cin, ldx, cout, k, s, p, H, mode):
     """ghost_conv2d_ex_nhwc: residual-before-activation, per-channel PReLU and the dual output."""
