@@ -7,10 +7,13 @@
 namespace ghost {
 
 // true when conv3x3_halo takes this descriptor (3x3/s1/p1, bf16, standard epilogue without the
-// uint8 copy, H % 16 == 0, W % 32 == 0, K ordered (channel block, tap, channel) as pack.py packs it)
+// uint8 copy — PReLU / residual-first / second BN'd output allowed —, K ordered (channel block, tap,
+// channel) as pack.py packs it, and either exact 16 x 32 tiles or 16 x 16 tiles that overhang the
+// image by at most a quarter of their pixels)
 bool conv3x3_halo_supported(const ConvDesc& d);
-// true when conv3x3_halo runs the persistent kernel for d, which can also emit InstanceNorm
+// true when conv3x3_halo runs the persistent 16 x 32 kernel for d, which can also emit InstanceNorm
 // partials of its output (d.in_part): count of partial records per (sample, channel) in *nrec
+// (the persistent 16 x 16 form for overhanging tiles / the IBasicBlock epilogue writes no partials)
 bool conv3x3_pp_takes(const ConvDesc& d, int* nrec);
 int conv3x3_halo(const ConvDesc& d, hipStream_t s);
 

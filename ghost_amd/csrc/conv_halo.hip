@@ -12,6 +12,10 @@
 // channels of one pixel and the epilogue stores 8 bytes per lane.
 // 8 waves, each 2 output rows (64 pixels) x 64 channels; 75 KB LDS -> two workgroups per CU,
 // which overlap one workgroup's DMA with the other's MFMAs.
+// The same plan serves ArcFace's IResNet (arc_runtime.hip) with 16 x 16 tiles (4 waves of 4 rows)
+// that may overhang 112/56/28/14-pixel images: the halo DMA zero-fills outside the image and the
+// epilogue drops those pixels; it also applies the IBasicBlock epilogue (PReLU, residual, the next
+// block's BatchNorm as a second output).
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
