@@ -873,6 +873,7 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
     return (int)hipGetLastError();                                                                          \
   }
       GHOST_PP_DBG(true, 2, 2) GHOST_PP_DBG(true, 2, 8) GHOST_PP_DBG(true, 2, 16) GHOST_PP_DBG(true, 2, 18)
+      GHOST_PP_DBG(true, 2, 26) GHOST_PP_DBG(true, 2, 24)
       GHOST_PP_DBG(false, 4, 6) GHOST_PP_DBG(false, 4, 8) GHOST_PP_DBG(false, 4, 16) GHOST_PP_DBG(false, 4, 22)
 #undef GHOST_PP_DBG
     }
