@@ -263,8 +263,8 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   __shared__ __attribute__((aligned(1024))) unsigned char lds0[STAGE_B];
   __shared__ __attribute__((aligned(1024))) unsigned char lds1[STAGE_B];
   __shared__ __attribute__((aligned(1024))) unsigned char ldsw[RESW ? 2 * WBLK_B : 16];
-  __shared__ float s_sc[512], s_sh[512];   // N <= 512 (conv3x3_pp_takes / conv3x3_halo)
-  __shared__ float s_ex[EPX ? 3 * 512 : 1];   // PReLU slope, scale2, shift2 (EPX)
+  __shared__ __attribute__((aligned(16))) float s_sc[512], s_sh[512];   // N <= 512 (conv3x3_pp_takes / conv3x3_halo)
+  __shared__ __attribute__((aligned(16))) float s_ex[EPX ? 3 * 512 : 4];   // PReLU slope, scale2, shift2 (EPX)
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
   const int prow = lane >> 2, slot = lane & 3;
 
@@ -468,14 +468,18 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
         }
         uint2 o;
         bf16* oe = reinterpret_cast<bf16*>(&o);
+        // the lane's 4 channels' tables as one 16-byte LDS read each (n % 4 == 0), not 4 scalar reads
+        const f32x4 tsc = *reinterpret_cast<const f32x4*>(s_sc + n);
+        const f32x4 tsh = *reinterpret_cast<const f32x4*>(s_sh + n);
         if constexpr (EPX) {
           // same order as conv_igemm.hip epi_std
+          const f32x4 tpr = *reinterpret_cast<const f32x4*>(s_ex + n);
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float t = fmaf(acc[j][i][r], s_sc[n + r], s_sh[n + r]);
+            float t = fmaf(acc[j][i][r], tsc[r], tsh[r]);
             if (a.res_first) t += rv[r];
-            t = t > 0.f ? t : t * s_ex[n + r];
+            t = t > 0.f ? t : t * tpr[r];
             if (!a.res_first) t += rv[r];
             if (a.tanh_out) t = tanhf(t);
             v[r] = t;
@@ -484,14 +488,16 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
           }
           *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
           if (a.y2) {
+            const f32x4 tsc2 = *reinterpret_cast<const f32x4*>(s_ex + 512 + n);
+            const f32x4 tsh2 = *reinterpret_cast<const f32x4*>(s_ex + 1024 + n);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) oe[r] = (bf16)(v[r] * s_ex[512 + n + r] + s_ex[1024 + n + r]);
+            for (int r = 0; r < 4; ++r) oe[r] = (bf16)(v[r] * tsc2[r] + tsh2[r]);
             *reinterpret_cast<uint2*>(a.y2 + pix * a.ldy2 + n) = o;
           }
         } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = fmaf(acc[j][i][r], s_sc[n + r], s_sh[n + r]);
+          float v = fmaf(acc[j][i][r], tsc[r], tsh[r]);
           v = v > 0.f ? v : v * a.slope;
           v += rv[r];
           if (a.tanh_out) v = tanhf(v);
