@@ -66,12 +66,9 @@ _SIGS = {
     "ghost_upsample2x_nhwc": (i32, [i32, vp, i32, vp, i32, i32, i32, i32, i32, vp]),
     "ghost_nhwc_to_nchw": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp]),
     "ghost_crops_to_input_nhwc": (i32, [vp, i64, i32, i32, i32, i32, vp, vp]),
-    "ghost_set_split_k": (i32, [i32]),
-    "ghost_set_fuse_upsample": (i32, [i32]),
-    "ghost_set_fuse_zup": (i32, [i32]),
-
-    "ghost_set_fuse_stats": (i32, [i32]),
-    "ghost_set_fuse_tail": (i32, [i32]),
+    "ghost_aei_set_option": (i32, [vp, i32, i32]),
+    "ghost_aei_get_option": (i32, [vp, i32, C.POINTER(i32)]),
+    "ghost_aei_set_taps": (i32, [vp, C.POINTER(vp)]),
     "ghost_aad_layers_v3_nhwc": (i32, [vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp), C.POINTER(vp),
                                        C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), i32, f32, C.POINTER(vp),
                                        C.POINTER(i32), vp, i64, vp]),
@@ -83,7 +80,7 @@ _SIGS = {
 class ConvEpi(C.Structure):
     """struct ghost_conv_epi (include/ghost_amd.h)."""
     _fields_ = [("scale", vp), ("shift", vp), ("slope", f32), ("prelu", vp), ("res", vp), ("ldres", i32),
-                ("res_first", i32), ("tanh_out", i32), ("y2", vp), ("ldy2", i32), ("scale2", vp), ("shift2", vp)]
+                ("res_first", i32), ("tanh_out", i32), ("y2", vp), ("ldy2", i32), ("scale2", vp), ("shift2", vp), ("split_k", i32)]
 
 
 def header_symbols():
@@ -140,3 +137,10 @@ def require_gpu(t: torch.Tensor, what: str) -> None:
     if not t.is_cuda:
         raise RuntimeError(f"ghost_amd: {what} runs only on a ROCm GPU (MI355X); got a {t.device} tensor. "
                            "The CPU path of the reference is not shipped by this package.")
+
+
+def require_same_device(t: torch.Tensor, dev: torch.device, what: str) -> None:
+    """The reference raises torch's device-mismatch error for a host embedding next to device crops;
+    the native path would read a host pointer on the GPU, so refuse it here."""
+    if t.device != dev:
+        raise RuntimeError(f"ghost_amd: {what} must be on {dev}, got a {t.device} tensor")

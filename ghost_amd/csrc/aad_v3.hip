@@ -511,10 +511,7 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   }
   dim3 grid((unsigned)((long)d.B * d.HW / a.PPW));
   if (upz) {
-    static const int z4 = [] {   // 1: the 4-wave form for every shape, 0: the 8-wave form, 2: by shape
-      const char* e = getenv("GHOST_AAD_Z4");
-      return e ? atoi(e) : 2;
-    }();
+    static const int z4 = GHOST_KNOB("GHOST_AAD_Z4", 2);
     // by shape: 4 waves where the 128-VGPR cap spills (h_in through the upsample as well)
     const bool four = z4 == 1 || (z4 == 2 && up);
 #define GHOST_V3Z(ca, l, u)                                                                          \
@@ -530,16 +527,10 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
 #undef GHOST_V3Z
     return -1;
   }
-  static const int use_v4 = [] {
-    const char* e = getenv("GHOST_AAD_V4");
-    return e ? atoi(e) : 1;
-  }();
+  static const int use_v4 = GHOST_KNOB("GHOST_AAD_V4", 1);
   // v4 (prefetching) only for the through-upsample form: measured B = 64, 256x256 L = 2: 724 vs 734 us
   // with the upsample, 604 vs 550 us without it (there v3's register loads win)
-  static const unsigned dyn_lds = [] {   // experiment: extra dynamic LDS to force the occupancy down
-    const char* e = getenv("GHOST_AAD_DYNLDS");
-    return e ? (unsigned)atoi(e) : 0u;
-  }();
+  static const unsigned dyn_lds = GHOST_KNOB("GHOST_AAD_DYNLDS", 0u);
   if (use_v4 && up && d.C == 64 && a.PPW % 256 == 0 && d.ldh % 8 == 0) {
 #define GHOST_V4(ca, l, u)                                                                       \
     if (d.Ca == ca && d.L == l && up == u) {                                                     \

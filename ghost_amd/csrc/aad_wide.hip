@@ -159,10 +159,7 @@ int wide_ppw(int B, int HW, int C, int Ca) {
   // 133 KB Ca = 512 rows): the weight rows staged per workgroup are then amortised over as
   // many 16-pixel tiles as possible
   const long minwg = Ca > 256 ? 256 : 512;
-  static const int force = [] {
-    const char* e = getenv("GHOST_AAD_WIDE_PPW");
-    return e ? atoi(e) : 0;
-  }();
+  static const int force = GHOST_KNOB("GHOST_AAD_WIDE_PPW", 0);
   if (force > 0 && HW % force == 0 && force % 16 == 0) return force;
   int best = 0;
   for (int ppw = 16; ppw <= HW && ppw <= 4096; ppw *= 2)

@@ -17,7 +17,6 @@
 #include "../../include/ghost_amd.h"
 #include "aad_fused.h"
 #include "aad_v3.h"
-#include "aad_tail.h"
 #include "conv_halo.h"
 #include "aad_wide.h"
 #include "conv_igemm.h"
@@ -69,6 +68,9 @@ struct ghost_aei {
   int nb = 2, c_id = 512, dt = GHOST_F32, esz = 4;
   std::map<std::string, const void*> slots;   // name -> device pointer (nullptr = unbound)
   int id_total = 0;                            // sum over AAD layers of 2*c_x
+  // per-handle plan options (ghost_aei_set_option); defaults are the measured choices
+  int opt[GHOST_AEI_NOPT] = {1, 1, 0};
+  void* taps[8] = {nullptr};                   // ghost_aei_set_taps: AADBlk1..7 outputs copied here
   // profiling
   int prof_mask = 0;
   std::vector<hipEvent_t> ev;
@@ -161,10 +163,7 @@ struct Ctx {
 };
 
 // one conv launch (or its workspace accounting in the dry run)
-static const bool g_trace = [] {   // GHOST_PLAN_TRACE=1: one stderr line per conv / AAD launch (profiling aid)
-  const char* e = getenv("GHOST_PLAN_TRACE");
-  return e && atoi(e) != 0;
-}();
+static const bool g_trace = GHOST_KNOB("GHOST_PLAN_TRACE", 0) != 0;   // one stderr line per launch (tuning builds)
 
 void run_conv(Ctx& c, ConvDesc& d, int cls_all, int cls_big, double flops) {
   if (!c.ok()) return;
@@ -190,27 +189,6 @@ void run_conv(Ctx& c, ConvDesc& d, int cls_all, int cls_big, double flops) {
   if (e_big >= 0) c.prof_end(cls_big, e_big, bytes, flops);
   if (e_all >= 0) c.prof_end(cls_all, e_all, bytes, flops);
 }
-
-static int g_fuse_upsample = 1;   // ghost_set_fuse_upsample (testing knob)
-// GHOST_FUSE_ZUP=1 / ghost_set_fuse_zup(1): swaps sample z_attr8 = upsample2x(z_attr7) inside AADBlk8's
-// AADLayers instead of materialising it.  Off by default: measured B = 64, the AAD kernels that
-// interpolate z_attr as well as h_in are compute/latency-bound and take what the upsample kernel
-// saves (AAD + upsample 2.500 vs 2.499 ms per step)
-static int g_fuse_zup = [] {
-  const char* e = getenv("GHOST_FUSE_ZUP");
-  return e ? atoi(e) : 0;
-}();
-// GHOST_FUSE_TAIL=1: AADBlk8's tail as one kernel (aad_tail.hip).  Off by default: measured B = 64 it
-// saves 2 GB of HBM traffic but runs latency-bound at one 8-wave workgroup per CU (793 us against the
-// 586 us of the dual-layer AAD's second layer + separate AAD + narrow conv it replaces): +0.6 % only
-static int g_fuse_tail = [] {
-  const char* e = getenv("GHOST_FUSE_TAIL");
-  return e ? atoi(e) : 0;
-}();
-static int g_fuse_stats = [] {     // GHOST_FUSE_STATS=0: statistics by a separate pass (A/B, tests)
-  const char* e = getenv("GHOST_FUSE_STATS");
-  return e ? atoi(e) : 1;
-}();
 
 void run_stats(Ctx& c, const void* x, int ldx, int B, int HW, int C, float* stat) {
   if (!c.ok()) return;
@@ -496,10 +474,7 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
   }
   // AADBlk7's block-input pair (C = 128, Ca = 64, materialised h_in) in one kernel: measured B = 64,
   // 258 vs 2 x 141 us (GHOST_AAD_PAIR128=0: one layer per kernel)
-  static const int pair128 = [] {
-    const char* e = getenv("GHOST_AAD_PAIR128");
-    return e ? atoi(e) : 1;
-  }();
+  static const int pair128 = GHOST_KNOB("GHOST_AAD_PAIR128", 1);
   const size_t lmax = (C == 64 || (pair128 && C == 128 && Ca == 64 && !up_src)) ? 2 : 1;
   for (size_t i0 = 0; i0 < ls.size(); i0 += lmax) {
     AadV3Desc d;
@@ -560,7 +535,7 @@ bool conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, 
   d.res = res; d.ldres = ldres;
   d.tanh_out = tanh_out; d.u8 = u8;
   int nrec = 0;
-  const bool fused = stat && g_fuse_stats && conv3x3_pp_takes(d, &nrec);
+  const bool fused = stat && c.h->opt[GHOST_AEI_OPT_FUSE_STATS] && conv3x3_pp_takes(d, &nrec);
   if (fused) d.in_part = (float*)c.alloc((size_t)B * nrec * Cout * 2 * sizeof(float));
   run_conv(c, d, 2, 3, flops);
   if (fused && c.ok() && !c.dry) {
@@ -622,51 +597,18 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     else
       run_stats(c, m, cin, B, n * n, cin, stat_m);
     void* y = last_k ? y_out : c.alloc(P * cout * es);
-    // AADBlk8 (-> RGB): its last add_blocks AADLayer, the last_add_block AADLayer and the fused
-    // 128 -> 3 output conv run as one kernel (aad_tail.hip): the two 64-channel AADLayer outputs
-    // never reach HBM
-    const bool tail = last_k && split && !zv && g_fuse_tail && h->dt == GHOST_BF16 && cin == 64 && cout <= 3 &&
-                      aad_tail_supported(h->dt, n, n, Ca, Ca, cin, cin);
     // x-branch and h'-branch share the output conv: conv(cat(a_x, a_h), [W_x | W_h]) = x + h'
-    void* cat = (split && !tail) ? c.alloc(P * 2 * cin * es) : nullptr;
+    void* cat = split ? c.alloc(P * 2 * cin * es) : nullptr;
     const void* x = m;
     const float* stat_x = stat_m;
     for (int i = 0; i < nb; ++i) {
       const bool last = i == nb - 1;
       const std::string cn = blk + ".conv" + std::to_string(i) + ".w";
-      if (last && tail) {
-        AadTailDesc d;
-        d.za = za; d.lda = Ca; d.Ca = Ca;
-        const std::string ln[2] = {blk + ".aad" + std::to_string(i), blk + ".aadlast"};
-        const int off[2] = {base + 2 * cin * i, base + 2 * cin * nb};
-        const void* hin[2] = {x, m};
-        const float* st[2] = {stat_x, stat_m};
-        const bool up[2] = {i == 0 && m_virtual, m_virtual};
-        for (int l = 0; l < 2; ++l) {
-          d.hin[l] = hin[l]; d.ldh[l] = cin; d.stat[l] = st[l];
-          if (up[l]) { d.up_H[l] = n / 2; d.up_W[l] = n / 2; }
-          d.w3[l] = c.W(ln[l] + ".w3");
-          d.b3[l] = (const float*)c.W(ln[l] + ".b3");
-          d.wh[l] = (const float*)c.W(ln[l] + ".wh");
-          d.bh[l] = (const float*)c.W(ln[l] + ".bh");
-          d.idgb[l] = idgb ? idgb + off[l] : nullptr;
-        }
-        d.id_ld = h->id_total;
-        d.wn = c.W(cn + "n");
-        d.y = y; d.u8 = u8; d.B = B; d.H = n; d.W = n; d.tanh_out = 1;
-        if (c.ok() && !c.dry) {
-          const double Pn = (double)B * n * n;
-          int e_all = c.prof_begin(0);
-          c.check(aad_tail(d, c.s), "aad_tail");
-          if (e_all >= 0) c.prof_end(0, e_all, Pn * 2.0 * (2.0 * cin + Ca) * es, 2.0 * Pn * 2.0 * 2.0 * cin * Ca);
-        }
-        break;
-      }
       std::vector<AadOut> group;
       void* a = (last && split) ? cat : c.alloc(P * cin * es);
       const int lda_out = (last && split) ? 2 * cin : cin;
       group.push_back({blk + ".aad" + std::to_string(i), base + 2 * cin * i, a, lda_out});
-      if (i == 0 && split && !tail)   // last_add_block's AADLayer reads the block input m as well
+      if (i == 0 && split)   // last_add_block's AADLayer reads the block input m as well
         group.push_back({blk + ".aadlast", base + 2 * cin * nb, (char*)cat + (size_t)cin * es, 2 * cin});
       aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb, i == 0 && m_virtual, zv);
       if (!last) {
@@ -685,6 +627,8 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
       }
     }
     id_off = base + 2 * cin * nb + (split ? 2 * cin : 0);
+    if (!last_k && h->taps[k - 1] && c.ok() && !c.dry)   // diagnostic copy of the block output (parity bisection)
+      c.check((int)hipMemcpyAsync(h->taps[k - 1], y, P * cout * es, hipMemcpyDeviceToDevice, c.s), "tap copy");
     if (!last_k) {
       // AADBlk(k+1) reads its input m only through the first AADLayer pair and the statistics
       // when cin != cout: those sample the upsample on the fly and m is never written
@@ -693,7 +637,7 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
       const int cout_n = h->gen()[k][1];
       // C = 64 only: at C = 128 (AADBlk7) the two single-layer kernels re-reading the upsample
       // cost more (+110 us) than the materialised upsample they replace (-85 us), measured B = 64
-      const bool fuse = g_fuse_upsample && cout != cout_n && cout == 64 && Ca_n % 32 == 0 &&
+      const bool fuse = h->opt[GHOST_AEI_OPT_FUSE_UPSAMPLE] && cout != cout_n && cout == 64 && Ca_n % 32 == 0 &&
                         aad_v3_supported(h->dt, B, n_n * n_n, cout, Ca_n, Ca_n, cout, 8);
       if (fuse) {
         m = y;
@@ -791,7 +735,7 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
     h->attr_geom(7, C7, H7);
     h->attr_geom(8, C8, H8);
     const int cin8 = h->gen()[7][0];
-    z8v = mode == M_SWAP && g_fuse_zup && !h->resnet && !g_fuse_tail && C7 == C8 && H8 == 2 * H7 && cin8 == 64 &&
+    z8v = mode == M_SWAP && h->opt[GHOST_AEI_OPT_FUSE_ZUP] && !h->resnet && C7 == C8 && H8 == 2 * H7 && cin8 == 64 &&
           h->dt == GHOST_BF16 && aad_v3_supported(h->dt, B, H8 * H8, cin8, C8, C8, cin8, 8);
   }
   for (int k = 1; k <= 8; ++k) {
@@ -999,35 +943,28 @@ extern "C" int ghost_aei_profile_read(ghost_aei* h, int cls, double* ms, int64_t
 // ---------------------------------------------------------------------------
 // C ABI: single operators
 // ---------------------------------------------------------------------------
-extern "C" int ghost_set_fuse_tail(int on) {
-  g_fuse_tail = on ? 1 : 0;
+extern "C" int ghost_aei_set_option(ghost_aei* h, int option, int value) {
+  if (!h) return fail(GHOST_EINVAL, "null handle");
+  if (option < 0 || option >= GHOST_AEI_NOPT) return fail(GHOST_EINVAL, "unknown option");
+  if (value != 0 && value != 1) return fail(GHOST_EINVAL, "option value must be 0 or 1");
+  h->opt[option] = value;
   return 0;
 }
 
-extern "C" int ghost_set_fuse_stats(int on) {
-  g_fuse_stats = on ? 1 : 0;
+extern "C" int ghost_aei_get_option(ghost_aei* h, int option, int* value) {
+  if (!h || !value) return fail(GHOST_EINVAL, "null argument");
+  if (option < 0 || option >= GHOST_AEI_NOPT) return fail(GHOST_EINVAL, "unknown option");
+  *value = h->opt[option];
   return 0;
 }
 
-extern "C" int ghost_set_fuse_upsample(int on) {
-  g_fuse_upsample = on ? 1 : 0;
-  return 0;
-}
-
-extern "C" int ghost_set_fuse_zup(int on) {
-  g_fuse_zup = on ? 1 : 0;
-  return 0;
-}
-
-static int g_force_split = 0;
-extern "C" int ghost_set_split_k(int n) {
-  if (n < 0) return fail(GHOST_EINVAL, "split must be >= 0");
-  g_force_split = n;
+extern "C" int ghost_aei_set_taps(ghost_aei* h, void* const taps[8]) {
+  if (!h) return fail(GHOST_EINVAL, "null handle");
+  for (int k = 0; k < 8; ++k) h->taps[k] = taps ? taps[k] : nullptr;
   return 0;
 }
 
 static int conv_op(ConvDesc& d, void* ws, int64_t ws_bytes, void* stream, const char* what) {
-  d.force_split = g_force_split;
   const size_t need = conv_workspace_bytes(d);
   if (need > 0 && (!ws || (size_t)ws_bytes < need))
     return fail(GHOST_ENOWS, std::string(what) + ": workspace too small, need " + std::to_string(need));
@@ -1063,6 +1000,8 @@ extern "C" int ghost_conv2d_ex_nhwc(int dtype, const void* x, int B, int H, int 
   d.scale = epi->scale; d.shift = epi->shift; d.slope = epi->slope; d.prelu = epi->prelu;
   d.res = epi->res; d.ldres = epi->ldres; d.res_first = epi->res_first; d.tanh_out = epi->tanh_out;
   d.y2 = epi->y2; d.ldy2 = epi->ldy2; d.scale2 = epi->scale2; d.shift2 = epi->shift2;
+  if (epi->split_k < 0) return fail(GHOST_EINVAL, "ghost_conv2d_ex_nhwc: split_k must be >= 0");
+  d.force_split = epi->split_k;
   d.y = y; d.ldy = ldy;
   return conv_op(d, ws, ws_bytes, stream, "ghost_conv2d_ex_nhwc");
 }
@@ -1118,7 +1057,6 @@ extern "C" int ghost_aad_layer_nhwc(int dtype, const void* h_in, int ldh, const 
   const size_t mask_b = ((size_t)B * HW * sizeof(float) + 255) & ~size_t(255);
   ConvDesc d;
   d.ti = d.to = dtype;
-  d.force_split = g_force_split;   // testing knob (ghost_set_split_k)
   d.x = z_attr; d.B = B; d.Hi = H; d.Wi = W; d.Cin = Ca; d.ldx = lda;
   d.w = gbw_packed; d.N = 2 * C; d.Npad = Npad; d.Kpad = Kpad;
   d.kind = CONV_FWD; d.kh = d.kw = 1;

@@ -83,10 +83,7 @@ struct ArcCtx {
 };
 
 static int arc_min_wgs() {
-  static const int v = [] {
-    const char* e = getenv("GHOST_ARC_MINWG");
-    return e ? atoi(e) : 0;
-  }();
+  static const int v = GHOST_KNOB("GHOST_ARC_MINWG", 0);
   return v;
 }
 

@@ -748,10 +748,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 }
 
 bool convT_halo_supported(const ConvDesc& d) {
-  static const int enabled = [] {
-    const char* e = getenv("GHOST_CONVT_HALO");
-    return e ? atoi(e) : 1;
-  }();
+  static const int enabled = GHOST_KNOB("GHOST_CONVT_HALO", 1);
   if (!enabled || d.kind != CONV_T4S2 || d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD) return false;
   if (d.u8 || d.tanh_out || d.force_split || d.Cin % 32 || d.ldx % 8 || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
   if (d.res_first || d.prelu || d.y2) return false;   // epilogue variants only the implicit GEMM has
@@ -791,10 +788,7 @@ static bool halo_small_ok(const ConvDesc& d) {
 }
 
 bool conv3x3_halo_supported(const ConvDesc& d) {
-  static const int enabled = [] {
-    const char* e = getenv("GHOST_CONV_HALO");
-    return e ? atoi(e) : 1;
-  }();
+  static const int enabled = GHOST_KNOB("GHOST_CONV_HALO", 1);
   if (!enabled || d.kind != CONV_FWD || d.kh != 3 || d.kw != 3 || d.stride != 1 || d.pad != 1) return false;
   if (d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD || d.u8 || d.force_split) return false;
   if (d.Cin % 32 || d.ldx % 8 || d.N % 64 || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
@@ -804,10 +798,7 @@ bool conv3x3_halo_supported(const ConvDesc& d) {
   if ((long)d.Hi * d.Wi * d.ldx >= (1L << 31) || (long)d.Npad * d.Kpad >= (1L << 31)) return false;   // 32-bit offsets
   // measured (tools/bench_ops.py, B = 64): faster than the implicit GEMM at every generator stage
   // from 32x32 up (N = 64 .. 512); GHOST_CONV_HALO_MAXN caps N for A/B runs
-  static const int max_n = [] {
-    const char* e = getenv("GHOST_CONV_HALO_MAXN");
-    return e ? atoi(e) : 1 << 30;
-  }();
+  static const int max_n = GHOST_KNOB("GHOST_CONV_HALO_MAXN", 1 << 30);
   return d.N <= max_n;
 }
 
@@ -842,10 +833,7 @@ static int num_cus() {
 // (ArcFace 112 .. 14, overhanging tiles) — or, with GHOST_HALO_PP_SMALL=1, also the generator's
 // 16 x 16 stage (A/B knob)
 static bool pp_small(const ConvDesc& d) {
-  static const int force = [] {
-    const char* e = getenv("GHOST_HALO_PP_SMALL");
-    return e ? atoi(e) : 0;
-  }();
+  static const int force = GHOST_KNOB("GHOST_HALO_PP_SMALL", 0);
   return !halo_exact_wide(d) && halo_small_ok(d) &&
          (force || d.Wi % HaloSmall::TW || d.Hi % HaloSmall::TH || d.prelu || d.y2 || d.res_first);
 }
@@ -861,18 +849,16 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   a.res_first = d.res_first;
   a.tiles_x = (d.Wi + G::TW - 1) / G::TW; a.tiles_y = (d.Hi + G::TH - 1) / G::TH; a.nNt = d.N / 64;
   a.ntiles = d.B * a.tiles_x * a.tiles_y * a.nNt;
-  static const int dbg = [] {
-    const char* e = getenv("GHOST_HALO_DBG");
-    return e ? atoi(e) : 0;
-  }();
+  static const int dbg = GHOST_KNOB("GHOST_HALO_DBG", 0);
   a.dbg = dbg;
   const int g = a.ntiles < num_cus() ? a.ntiles : num_cus();
   a.in_part = d.in_part;
   const bool resw = d.Cin <= 64 && d.N == 64;
   const int ncb = d.Cin / 32;
   constexpr int NT = G::NW * 64;
+#ifdef GHOST_TUNING
   if constexpr (G::TW == 32) {
-    if (dbg && !a.in_part) {   // experiment variants
+    if (dbg && !a.in_part) {   // experiment variants (tuning builds only)
 #define GHOST_PP_DBG(R, NB, V)                                                                               \
   if (resw == R && ncb == NB && dbg == V) {                                                                 \
     hipLaunchKernelGGL((conv3x3_halo_pp_kernel<G, R, false, NB, V>), dim3((unsigned)g), dim3(NT), 0, s, a); \
@@ -884,6 +870,7 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
 #undef GHOST_PP_DBG
     }
   }
+#endif
   constexpr bool CAN_ST = G::TW == 32;
 #define GHOST_PP(R, ST, NB) \
   hipLaunchKernelGGL((conv3x3_halo_pp_kernel<G, R, ST, NB>), dim3((unsigned)g), dim3(NT), 0, s, a)
@@ -913,17 +900,11 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
 }
 
 bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
-  static const int pp = [] {
-    const char* e = getenv("GHOST_HALO_PP");
-    return e ? atoi(e) : 1;
-  }();
+  static const int pp = GHOST_KNOB("GHOST_HALO_PP", 1);
   if (!conv3x3_halo_supported(d)) return false;
   if (d.prelu || d.y2 || d.res_first) return false;   // epilogue variants of the non-persistent kernel only
   const bool wide = halo_exact_wide(d);
-  static const int max_cin = [] {
-    const char* e = getenv("GHOST_HALO_PP_MAXCIN");
-    return e ? atoi(e) : 1024;
-  }();
+  static const int max_cin = GHOST_KNOB("GHOST_HALO_PP_MAXCIN", 1024);
   // measured A/B (B = 64): the persistent form wins at every generator shape with W % 32 == 0 (256x256:
   // -23 %, 128x128: -7 %, 64x64 256->256: -9 %; with the counted first-stage wait also 64x64 512->128
   // -11 %, 32x32 512->512 -6 %, 32x32 1024->256 -8 %: +3 % frames/s end to end)
@@ -937,10 +918,7 @@ int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
   if (!conv3x3_halo_supported(d)) return -1;
   if (conv3x3_pp_takes(d, nullptr)) return halo_pp_launch<HaloWide>(d, s);
   if (d.in_part) return -1;   // only the persistent 16 x 32 kernel writes InstanceNorm partials
-  static const int pp = [] {
-    const char* e = getenv("GHOST_HALO_PP");
-    return e ? atoi(e) : 1;
-  }();
+  static const int pp = GHOST_KNOB("GHOST_HALO_PP", 1);
   const int ncb = d.Cin / 32;
   if (pp && pp_small(d) && d.N <= 512 && d.Cin % 64 == 0 &&
       (ncb == 2 || ncb == 4 || ncb == 6 || ncb == 8 || ncb == 16 || ncb == 32))

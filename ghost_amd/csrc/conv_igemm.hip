@@ -552,13 +552,9 @@ struct Plan {
   bool partial;   // GEMM writes fp32 partials, splitk_reduce_kernel applies the epilogue
 };
 
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
 
 Plan make_plan(const ConvDesc& d) {
-  static const int force_bk = env_int("GHOST_CONV_BK", 0);   // tuning knob (0 = heuristic)
+  static const int force_bk = GHOST_KNOB("GHOST_CONV_BK", 0);   // tuning knob (0 = heuristic)
   Plan p{};
   p.npar = d.kind == CONV_T4S2 ? 4 : 1;
   if (d.kind == CONV_T4S2) {
@@ -596,11 +592,13 @@ Plan make_plan(const ConvDesc& d) {
     p.BM = ((p.M + 127) / 128) * ((d.N + 127) / 128) * p.npar >= 512 ? 128 : 64;
   }
   if (!p.fast || p.BM >= 256) p.BK = force_bk == 64 && bk64_ok ? 64 : 32;
+#ifdef GHOST_TUNING
   static const char* force_tile = getenv("GHOST_CONV_TILE");   // tuning knob "BMxBN"
   if (force_tile && p.fast && d.epi != EPI_AAD) {
     int bm = 0, bn = 0;
     if (sscanf(force_tile, "%dx%d", &bm, &bn) == 2 && bn >= d.N / 2 && bm > 0) { p.BM = bm; p.BN = bn; }
   }
+#endif
   p.nNt = (d.N + p.BN - 1) / p.BN;
   p.nMt = (p.M + p.BM - 1) / p.BM;
   p.NT = p.nNt * p.BN;
@@ -695,7 +693,7 @@ int dispatch_tile(const ConvArgs& a, const Plan& p, hipStream_t s) {
 
 template <int EPI>
 bool launch_glds(const ConvArgs& a, const Plan& p, hipStream_t s) {
-  static const int stages = env_int("GHOST_CONV_STAGES", 3);
+  static const int stages = GHOST_KNOB("GHOST_CONV_STAGES", 3);
   dim3 grid(p.nMt * p.nNt, p.nsplit, p.npar);
 #define GHOST_G(bm, bn, st)                                                                      \
   if (p.BM == bm && p.BN == bn && stages == st) {                                                \
@@ -722,7 +720,7 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
     hipLaunchKernelGGL((splitk_reduce_kernel<float, KEPI_STD>), grid, dim3(256), 0, s, a);
     return 0;
   } else {
-  static const int use_v2 = env_int("GHOST_CONV_V2", 1);
+  static const int use_v2 = GHOST_KNOB("GHOST_CONV_V2", 1);
   if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
     // measured (tools/bench_ops.py): the DMA ring wins on the 128-row tiles, loses on 256x64
     if (use_v2 && p.fast && p.BK == 32 && d.epi != EPI_AAD && p.BM <= 128 && p.partial == (p.nsplit > 1)) {

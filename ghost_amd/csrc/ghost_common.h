@@ -10,6 +10,20 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+// A/B tuning knobs.  Only a tuning build (GHOST_TUNING=1 python -m ghost_amd.build, which adds
+// -DGHOST_TUNING) reads them from the environment; the shipping library compiles each knob to the
+// default that the measurements chose, so no process-global switch changes its behaviour.
+#ifdef GHOST_TUNING
+inline int ghost_env_knob(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+#define GHOST_KNOB(name, dflt) ghost_env_knob(name, dflt)
+#else
+#define GHOST_KNOB(name, dflt) (dflt)
+#endif
 
 #define GHOST_DEV __device__ __forceinline__
 

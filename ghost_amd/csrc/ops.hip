@@ -489,10 +489,7 @@ int aad_mask2(int dt, const void* h, int ldh, int B, int HW, int C, const float*
   if (ppb > HW) ppb = HW;
   dim3 grid((unsigned)((HW + ppb - 1) / ppb), (unsigned)B);
   const int L = wh1 ? 2 : 1;
-  static const int use_reg = [] {
-    const char* e = getenv("GHOST_MASK_REG");
-    return e ? atoi(e) : 1;
-  }();
+  static const int use_reg = GHOST_KNOB("GHOST_MASK_REG", 1);
   if (use_reg && dt == GHOST_BF16 && (C == 8 * G || C == 16 * G)) {
     const int nch = C / (8 * G);
 #define GHOST_MR(l, n)                                                                                              \
@@ -634,6 +631,9 @@ int crops_u8_to_input(const uint8_t* crops, int64_t batch_stride, int B, int H, 
     hipLaunchKernelGGL(crops_kernel<float>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (float*)y, ldy);
   else if (dt == GHOST_BF16)
     hipLaunchKernelGGL(crops_kernel<bf16>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (bf16*)y, ldy);
+  else if (dt == GHOST_F16)   // transform_target_to_torch(half=True) of the reference: float16
+    hipLaunchKernelGGL(crops_kernel<_Float16>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W,
+                       (_Float16*)y, ldy);
   else
     return -1;
   return (int)hipGetLastError();

@@ -17,14 +17,14 @@ from .. import _lib
 def transform_target_to_torch(resized_frs: np.ndarray, half: bool = True, device=None) -> torch.Tensor:
     """core.py:13-26: uint8 BGR NHWC crops -> RGB, /255, (x-0.5)/0.5, returned as an NCHW view.
 
-    Runs on the GPU kernel ``ghost_crops_to_input_nhwc``; ``half=True`` yields bfloat16
-    (the MI355X throughput dtype) instead of float16.
+    Runs on the GPU kernel ``ghost_crops_to_input_nhwc``; ``half=True`` yields float16 as in the
+    reference (core.py:20-21: fp32 /255, then fp16); ``half=False`` float32.
     """
     device = torch.device(device or "cuda")
     crops = torch.from_numpy(np.ascontiguousarray(resized_frs)).to(device)
     _lib.require_gpu(crops, "transform_target_to_torch")
     B, H, W, _ = crops.shape
-    dt = torch.bfloat16 if half else torch.float32
+    dt = torch.float16 if half else torch.float32
     y = torch.empty(B, H, W, 3, dtype=dt, device=device)
     lib = _lib.load()
     _lib.check(lib.ghost_crops_to_input_nhwc(crops.data_ptr(), crops.stride(0), B, H, W, _lib.gdtype(dt),

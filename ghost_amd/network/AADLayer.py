@@ -49,6 +49,8 @@ class AADLayer(nn.Module):
     @torch.no_grad()
     def forward(self, h_in, z_attr, z_id, relu: bool = False):
         _lib.require_gpu(h_in, "AADLayer.forward")
+        _lib.require_same_device(z_attr, h_in.device, "z_attr")
+        _lib.require_same_device(z_id, h_in.device, "z_id")
         lib = _lib.load()
         pdt = self.conv1.weight.dtype
         dt = torch.float32 if pdt == torch.float32 else torch.bfloat16
@@ -74,7 +76,8 @@ class AADLayer(nn.Module):
                                             p["gbb"].data_ptr(), p["wh"].data_ptr(), p["bh"].data_ptr(),
                                             idgb.data_ptr(), 2 * C, 0.0 if relu else 1.0, out.data_ptr(), C,
                                             ws.data_ptr(), ws.numel(), s), "AADLayer")
-        return out.permute(0, 3, 1, 2)
+        out = out.permute(0, 3, 1, 2)
+        return out.to(torch.float16) if pdt == torch.float16 else out   # .half(): the reference's dtype
 
 
 class _Container(nn.Sequential):

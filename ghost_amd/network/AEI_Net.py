@@ -14,9 +14,11 @@ the attr maps are returned as NCHW *views* (``channels_last`` strides) — same 
 values as the reference, no copy.
 
 Numerics: fp32 parameters run the fp32 path (exact-fp32 MFMA, |dY| <= 1e-3 vs the
-reference CPU forward); ``.half()`` / ``.bfloat16()`` parameters (or
-``compute_dtype=torch.bfloat16``) run the bf16 throughput path (bf16 storage, fp32
-accumulation) and return bf16 tensors.  There is no CPU path.
+reference CPU forward).  ``.bfloat16()`` parameters (or ``compute_dtype=torch.bfloat16``)
+run the bf16 throughput path (bf16 storage, fp32 accumulation) and return bf16 tensors.
+``.half()`` parameters (inference.py:30) run the same bf16 kernels and return float16
+tensors, as the reference's fp16 module does: the dtype callers see is the reference's,
+the storage precision is bf16 (DESIGN.md §2 quotes both errors).  There is no CPU path.
 """
 from __future__ import annotations
 
@@ -125,10 +127,14 @@ class AADGenerator(nn.Module):
         raise NotImplementedError("ghost_amd: AADGenerator runs inside AEI_Net.forward on the MI355X path")
 
 
+# per-handle plan options (include/ghost_amd.h GHOST_AEI_OPT_*)
+OPTIONS = {"fuse_upsample": 0, "fuse_stats": 1, "fuse_zup": 2}
+
+
 class _Runtime:
     """Native handle + packed weights for one (device, compute dtype)."""
 
-    def __init__(self, backbone, num_blocks, c_id, dtype, slots):
+    def __init__(self, backbone, num_blocks, c_id, dtype, slots, options=None):
         self.lib = _lib.load()
         self.dtype = dtype
         h = C.c_void_p()
@@ -140,6 +146,8 @@ class _Runtime:
             _lib.check(self.lib.ghost_aei_bind(h, name.encode(), t.data_ptr(), t.numel()), f"bind {name}")
         if self.lib.ghost_aei_missing(h) != 0:
             _lib.check(-2, "weights incomplete")
+        for name, v in (options or {}).items():
+            _lib.check(self.lib.ghost_aei_set_option(h, OPTIONS[name], int(v)), f"option {name}")
         self.geom = []
         for k in range(1, 9):
             c_, h_, w_ = C.c_int(), C.c_int(), C.c_int()
@@ -172,6 +180,7 @@ class AEI_Net(nn.Module):
         self.generator = AADGenerator(backbone, c_id, num_blocks)
         self._rt = None
         self._rt_sig = None
+        self._options = {}
         import weakref
         self.encoder._owner = weakref.ref(self)
 
@@ -180,6 +189,20 @@ class AEI_Net(nn.Module):
         if self.compute_dtype is not None:
             return self.compute_dtype
         return torch.float32 if self.generator.up1.weight.dtype == torch.float32 else torch.bfloat16
+
+    def _out_dtype(self, rt) -> torch.dtype:
+        """float16 for a .half() module (the reference's output dtype), else the compute dtype."""
+        if self.compute_dtype is None and self.generator.up1.weight.dtype == torch.float16:
+            return torch.float16
+        return rt.dtype
+
+    def set_option(self, name: str, value: int) -> None:
+        """Per-model plan option (include/ghost_amd.h): fuse_upsample, fuse_stats, fuse_zup (0 / 1)."""
+        if name not in OPTIONS:
+            raise ValueError(f"ghost_amd: unknown option {name!r} (known: {sorted(OPTIONS)})")
+        self._options[name] = int(value)
+        if self._rt is not None:
+            _lib.check(self._rt.lib.ghost_aei_set_option(self._rt.h, OPTIONS[name], int(value)), f"option {name}")
 
     def _runtime(self, device) -> _Runtime:
         dt = self._dtype()
@@ -191,7 +214,7 @@ class AEI_Net(nn.Module):
                     raise RuntimeError(f"ghost_amd: parameter {k} is on {v.device}, input on {device}")
             with torch.no_grad():
                 slots = pack_all(sd, self.backbone, self.num_blocks, self.c_id, dt)
-            self._rt = _Runtime(self.backbone, self.num_blocks, self.c_id, dt, slots)
+            self._rt = _Runtime(self.backbone, self.num_blocks, self.c_id, dt, slots, self._options)
             self._rt_sig = sig
         return self._rt
 
@@ -210,7 +233,18 @@ class AEI_Net(nn.Module):
 
     @torch.no_grad()
     def forward(self, Xt, z_id, *, out_u8: Optional[torch.Tensor] = None):
+        Y, attrs, _ = self._forward(Xt, z_id, out_u8, taps=False)
+        return Y, attrs
+
+    @torch.no_grad()
+    def forward_taps(self, Xt, z_id, *, out_u8: Optional[torch.Tensor] = None):
+        """forward + the stored outputs of AADBlk1..7 (NCHW views, before the x2 upsample): the
+        per-stage checkpoints the bf16 parity tests bisect against the storage-emulating oracle."""
+        return self._forward(Xt, z_id, out_u8, taps=True)
+
+    def _forward(self, Xt, z_id, out_u8, taps):
         rt, B, attrs, st = self._prep(Xt, "AEI_Net.forward")
+        _lib.require_same_device(z_id, Xt.device, "z_id")
         z = z_id.reshape(z_id.shape[0], -1)
         if z.shape[0] != B or z.shape[1] != self.c_id:
             raise RuntimeError(f"ghost_amd: z_id must hold {B} rows of {self.c_id}, got {tuple(z_id.shape)}")
@@ -227,22 +261,39 @@ class AEI_Net(nn.Module):
             _lib.check(int(nbytes), "workspace sizing")
         ws = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
         ap = (C.c_void_p * 8)(*[a.data_ptr() for a in attrs])
-        _lib.check(lib.ghost_aei_forward(rt.h, Xt.data_ptr(), _lib.gdtype(Xt.dtype), st, B, z.data_ptr(),
-                                         _lib.gdtype(z.dtype), z.stride(0), Y.data_ptr(),
-                                         out_u8.data_ptr() if out_u8 is not None else None, ap, ws.data_ptr(),
-                                         ws.numel(), _lib.stream_ptr(dev)), "AEI_Net.forward")
-        return Y.permute(0, 3, 1, 2), tuple(a.permute(0, 3, 1, 2) for a in attrs)
+        blocks = []
+        if taps:
+            cin_cout = [(1024, 1024), (1024, 1024), (1024, 1024), (1024, 512), (512, 256), (256, 128), (128, 64)]
+            blocks = [torch.empty(B, 2 ** k, 2 ** k, cin_cout[k - 1][1], dtype=rt.dtype, device=dev) for k in range(1, 8)]
+            _lib.check(lib.ghost_aei_set_taps(rt.h, (C.c_void_p * 8)(*[b.data_ptr() for b in blocks], None)), "taps")
+        try:
+            _lib.check(lib.ghost_aei_forward(rt.h, Xt.data_ptr(), _lib.gdtype(Xt.dtype), st, B, z.data_ptr(),
+                                             _lib.gdtype(z.dtype), z.stride(0), Y.data_ptr(),
+                                             out_u8.data_ptr() if out_u8 is not None else None, ap, ws.data_ptr(),
+                                             ws.numel(), _lib.stream_ptr(dev)), "AEI_Net.forward")
+        finally:
+            if taps:
+                lib.ghost_aei_set_taps(rt.h, None)
+        od = self._out_dtype(rt)
+        Y = Y.permute(0, 3, 1, 2)
+        attrs = tuple(a.permute(0, 3, 1, 2) for a in attrs)
+        if od != rt.dtype:
+            Y, attrs = Y.to(od), tuple(a.to(od) for a in attrs)
+        return Y, attrs, [b.permute(0, 3, 1, 2) for b in blocks]
 
     @torch.no_grad()
     def get_attr(self, X):
         rt, B, attrs, st = self._prep(X, "AEI_Net.get_attr")
         lib = rt.lib
         nbytes = lib.ghost_aei_workspace_bytes(rt.h, B)
+        if nbytes < 0:
+            _lib.check(int(nbytes), "workspace sizing")
         ws = torch.empty(int(nbytes), dtype=torch.uint8, device=X.device)
         ap = (C.c_void_p * 8)(*[a.data_ptr() for a in attrs])
         _lib.check(lib.ghost_aei_get_attr(rt.h, X.data_ptr(), _lib.gdtype(X.dtype), st, B, ap, ws.data_ptr(),
                                           ws.numel(), _lib.stream_ptr(X.device)), "AEI_Net.get_attr")
-        return tuple(a.permute(0, 3, 1, 2) for a in attrs)
+        od = self._out_dtype(rt)
+        return tuple(a.permute(0, 3, 1, 2).to(od) for a in attrs)
 
     @torch.no_grad()
     def swap_u8(self, crops_u8: torch.Tensor, z_id: torch.Tensor, out: Optional[torch.Tensor] = None):
@@ -253,6 +304,7 @@ class AEI_Net(nn.Module):
         if crops_u8[0].stride() != (768, 3, 1):
             crops_u8 = crops_u8.contiguous()
         dev = crops_u8.device
+        _lib.require_same_device(z_id, dev, "z_id")
         rt = self._runtime(dev)
         B = crops_u8.shape[0]
         z = z_id.reshape(z_id.shape[0], -1)
@@ -261,10 +313,18 @@ class AEI_Net(nn.Module):
         zrs = z.stride(0) if z.shape[0] == B else 0   # one identity row broadcast (faceshifter_run.py:15-16)
         if z.shape[0] not in (1, B):
             raise RuntimeError("ghost_amd: z_id must have 1 or B rows")
+        if z.shape[1] != self.c_id:
+            raise RuntimeError(f"ghost_amd: z_id rows must hold {self.c_id} values, got {tuple(z_id.shape)}")
         if out is None:
             out = torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev)
+        elif (tuple(out.shape) != (B, 256, 256, 3) or out.dtype != torch.uint8 or not out.is_contiguous()
+              or out.device != dev):
+            raise RuntimeError(f"ghost_amd: out must be a contiguous uint8 [{B},256,256,3] tensor on {dev}, got "
+                               f"{out.dtype} {tuple(out.shape)} on {out.device}")
         lib = rt.lib
         nbytes = lib.ghost_aei_swap_workspace_bytes(rt.h, B)
+        if nbytes < 0:
+            _lib.check(int(nbytes), "workspace sizing")
         ws = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
         _lib.check(lib.ghost_aei_swap_u8(rt.h, crops_u8.data_ptr(), crops_u8.stride(0), B, z.data_ptr(),
                                          _lib.gdtype(z.dtype), zrs, out.data_ptr(), ws.data_ptr(), ws.numel(),

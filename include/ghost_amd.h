@@ -77,6 +77,23 @@ int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_str
                       int zid_dtype, int64_t zid_row_stride, uint8_t* out_u8, void* ws, int64_t ws_bytes,
                       void* stream);
 
+/* Per-handle plan options (defaults are the measured choices; every forward of the handle uses them):
+ *   GHOST_AEI_OPT_FUSE_UPSAMPLE (1): AADBlk8's first AADLayer pair samples upsample2x(AADBlk7 output) on the fly
+ *                                    instead of reading a materialised upsample (0 materialises it)
+ *   GHOST_AEI_OPT_FUSE_STATS (1):    the persistent 3x3 conv emits the InstanceNorm partials of its output
+ *                                    (0: a separate statistics pass)
+ *   GHOST_AEI_OPT_FUSE_ZUP (0):      swaps sample z_attr8 = upsample2x(z_attr7) inside AADBlk8's AADLayers
+ *                                    instead of materialising it (unet / linknet, bf16)
+ * value is 0 or 1.  A handle is not shared across threads without external synchronisation. */
+enum { GHOST_AEI_OPT_FUSE_UPSAMPLE = 0, GHOST_AEI_OPT_FUSE_STATS = 1, GHOST_AEI_OPT_FUSE_ZUP = 2, GHOST_AEI_NOPT = 3 };
+int ghost_aei_set_option(ghost_aei* h, int option, int value);
+int ghost_aei_get_option(ghost_aei* h, int option, int* value);
+/* Diagnostic taps (parity bisection): while set, every forward / swap of the handle copies the stored
+ * output of AADBlk k (k = 1..7, NHWC [B, 2^k, 2^k, cout_k] in the handle dtype, before the x2 upsample)
+ * into taps[k-1] when that pointer is non-NULL (taps[7] is unused: AADBlk8's output is Y).
+ * NULL taps clears them. */
+int ghost_aei_set_taps(ghost_aei* h, void* const taps[8]);
+
 /* per-kernel-class device timing with HIP events (bench instrumentation).
  * class_mask bit i enables class i; classes: 0 AAD kernels (all stages), 1 the block-input AAD
  * kernel at 256x256 (through-upsample, aad_v4), 2 conv3x3 (all), 3 conv3x3 at 256x256, 4 IN stats + mask,
@@ -111,6 +128,7 @@ typedef struct ghost_conv_epi {
   int ldy2;
   const float* scale2;
   const float* shift2;
+  int split_k;   /* 0 = the planner's choice; n > 0 forces n K-splits (tests of the split-K reduction) */
 } ghost_conv_epi;
 int ghost_conv2d_ex_nhwc(int dtype, const void* x, int B, int H, int W, int Cin, int ldx, const void* w_packed,
                          int Cout, int Npad, int Kpad, int kh, int kw, int stride, int pad, const ghost_conv_epi* epi,
@@ -163,21 +181,6 @@ int ghost_nhwc_to_nchw(int dtype, const void* x, int ldx, int B, int H, int W, i
 /* transform_target_to_torch (core.py:13-26): uint8 BGR NHWC crops -> RGB NHWC in [-1,1] (dtype f32/bf16) */
 int ghost_crops_to_input_nhwc(const uint8_t* crops, int64_t crop_batch_stride, int B, int H, int W, int dtype, void* y,
                               void* stream);
-/* testing knob: force the split-K factor of subsequent single-operator convs (0 = heuristic) */
-int ghost_set_split_k(int n);
-/* testing knob: 1 (default) lets the generator sample the upsample of AADBlk7's output inside
- * AADBlk8's first AADLayer pair instead of materialising it; 0 materialises it */
-int ghost_set_fuse_upsample(int on);
-/* experimental knob: 1 lets swaps sample z_attr8 = upsample2x(z_attr7) inside AADBlk8's AADLayers
- * instead of materialising it (unet / linknet, bf16, fuse_tail off); 0 (default) materialises it */
-int ghost_set_fuse_zup(int on);
-/* testing knob: 1 (default) lets the persistent 3x3 conv emit the InstanceNorm partials of its
- * output (no separate statistics pass); 0 computes them by a separate pass */
-int ghost_set_fuse_stats(int on);
-/* experimental knob: 1 runs AADBlk8's last AADLayers + output conv as one kernel (aad_tail.hip);
- * 0 (default) runs them as separate kernels */
-int ghost_set_fuse_tail(int on);
-
 /* ---- ArcFace identity encoder (IResNet, the netArc GHOST loads) ------------------------
  * Replaces: inference.py:33-36 iresnet100(fp16=False) + load_state_dict + .cuda().eval();
  *   core.py:43-54 / video_processing.py:136-140 netArc(F.interpolate(normalize_and_torch_batch(crops),

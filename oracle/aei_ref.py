@@ -301,6 +301,184 @@ def aei_forward(p, xt, z_id, backbone="unet", num_blocks=2, dtype=torch.float32)
 
 
 # ----------------------------------------------------------------------------
+# bf16-storage emulation (the checker of the bf16 throughput path)
+# ----------------------------------------------------------------------------
+# The same reference algorithm as above, with every tensor the MI355X runtime *stores* in bf16
+# rounded to bf16 at that point, and every weight the packer stores in bf16 rounded likewise
+# (ghost_amd/network/pack.py).  Arithmetic between storage points stays fp32: the kernels
+# accumulate in fp32 and apply BatchNorm / bias / InstanceNorm / mask / blend / residual / tanh
+# in fp32 epilogues.  Differences left against the kernels are fp32 summation order only, which
+# can flip a bf16 rounding here and there; the GPU tests gate on that residual.
+#
+# Storage points (aei_runtime.hip plan):
+#   input x (crops_kernel / input_to_nhwc)            -> bf16
+#   every encoder conv / deconv output after BN + LReLU (+ linknet skip add) -> bf16
+#   z_attr8 = up2x(z_attr7)                           -> bf16
+#   m1 = up1(z_id) (fp32 weights, fp32 z_id)         -> bf16
+#   AADLayer output after its ReLU                    -> bf16   (gamma/beta from bf16 conv1/conv2,
+#                                                                fc1/fc2 and conv_h in fp32)
+#   3x3 conv outputs inside a block                   -> bf16
+#   block output: last conv + residual (x + h' in one GEMM over [a_x | a_h] when cin != cout) -> bf16
+#   m_{k+1} = up2x(y_k)                               -> bf16 (materialised or sampled in-kernel)
+#   Y = tanh(.)                                       -> bf16; the u8 frame comes from the fp32 tanh
+# InstanceNorm statistics are those of the stored bf16 tensor, except where the runtime takes the
+# statistics of an upsample in closed form over its source (source side >= 32, C % 64 == 0:
+# ops.hip in_stats_up2x_closed_form), which are the statistics of the fp32 upsample.
+_STORE = [torch.bfloat16]     # storage dtype of the emulation (float32: rounding off, for self-checks)
+
+
+def _q(t: torch.Tensor) -> torch.Tensor:
+    return t.to(_STORE[0]).float()
+
+
+def _wq(p, key):
+    return _q(p[key].float())
+
+
+def _conv4x4_block_q(x, p, i):
+    y = F.conv2d(x, _wq(p, f"encoder.conv{i}.0.weight"), None, stride=2, padding=1)
+    return _q(F.leaky_relu(_bn_eval(y, p, f"encoder.conv{i}.1"), LRELU))
+
+
+def _deconv4x4_block_q(x, skip, p, i, backbone):
+    y = F.conv_transpose2d(x, _wq(p, f"encoder.deconv{i}.deconv.weight"), None, stride=2, padding=1)
+    y = F.leaky_relu(_bn_eval(y, p, f"encoder.deconv{i}.bn"), LRELU)
+    return _q(y + skip) if backbone == "linknet" else torch.cat((_q(y), skip), dim=1)
+
+
+def _res_conv_q(x, p, wkey, bnkey, stride, pad, relu, res=None):
+    y = _bn_eval(F.conv2d(x, _wq(p, wkey), None, stride=stride, padding=pad), p, bnkey)
+    if res is not None:
+        y = y + res
+    return _q(F.relu(y) if relu else y)
+
+
+def _encoder_resnet_q(xt, p):
+    x0 = _res_conv_q(xt, p, "encoder.conv0.weight", "encoder.bn0", 1, 3, True)
+    x = _res_conv_q(x0, p, "encoder.conv1.weight", "encoder.bn1", 2, 3, True)
+    feats = [x0, x]
+    for li, _cin, _planes, stride, blk in resnet_blocks():
+        pre = f"encoder.layer{li}.{blk}"
+        t = _res_conv_q(x, p, f"{pre}.conv1.weight", f"{pre}.bn1", stride, 0, True)
+        t = _res_conv_q(t, p, f"{pre}.conv2.weight", f"{pre}.bn2", 1, 1, True)
+        res = x
+        if blk == 0:
+            res = _res_conv_q(x, p, f"{pre}.downsample.0.weight", f"{pre}.downsample.1", stride, 0, False)
+        x = _res_conv_q(t, p, f"{pre}.conv3.weight", f"{pre}.bn3", 1, 0, True, res)
+        if blk == 1:
+            feats.append(x)
+    return tuple(reversed(feats))
+
+
+def encoder_bf16_storage(xt, p, backbone="unet"):
+    """MLAttrEncoder.forward (AEI_Net.py:72-95) with bf16 storage; xt already bf16-valued."""
+    if backbone == "resnet":
+        return _encoder_resnet_q(xt, p)
+    feats, x = [], xt
+    for i in range(1, 8):
+        x = _conv4x4_block_q(x, p, i)
+        feats.append(x)
+    z = [feats[6]]
+    for i in range(1, 7):
+        z.append(_deconv4x4_block_q(z[-1], feats[6 - i], p, i, backbone))
+    z.append(_q(up2x(z[-1])))
+    return tuple(z)
+
+
+def _in_stats(t):
+    var, mean = torch.var_mean(t, dim=(2, 3), unbiased=False, keepdim=True)
+    return mean, torch.rsqrt(var + IN_EPS)
+
+
+def aad_layer_bf16_storage(h_in, z_attr, z_id, p, prefix, stats=None):
+    """AADLayer.forward (AADLayer.py:20-38) + the ReLU after it, bf16 weights for conv1/conv2,
+    output stored in bf16.  `stats` = (mean, rstd) when the runtime takes them elsewhere."""
+    mean, rstd = stats if stats is not None else _in_stats(h_in)
+    h = (h_in - mean) * rstd
+    ga = F.conv2d(z_attr, _wq(p, f"{prefix}.conv1.weight"), p[f"{prefix}.conv1.bias"].float())
+    ba = F.conv2d(z_attr, _wq(p, f"{prefix}.conv2.weight"), p[f"{prefix}.conv2.bias"].float())
+    gi = F.linear(z_id, p[f"{prefix}.fc1.weight"].float(), p[f"{prefix}.fc1.bias"].float())
+    bi = F.linear(z_id, p[f"{prefix}.fc2.weight"].float(), p[f"{prefix}.fc2.bias"].float())
+    c_x = h.shape[1]
+    A = ga * h + ba
+    I = gi.reshape(h.shape[0], c_x, 1, 1) * h + bi.reshape(h.shape[0], c_x, 1, 1)
+    M = torch.sigmoid(F.conv2d(h, p[f"{prefix}.conv_h.weight"].float(), p[f"{prefix}.conv_h.bias"].float()))
+    return _q(F.relu((1 - M) * A + M * I))
+
+
+def up1_bf16_storage(z_id, p):
+    """m1 = up1(z_id) (AEI_Net.py:101,123): fp32 weights and z_id, stored in bf16."""
+    z_id = z_id.float().reshape(z_id.shape[0], -1)
+    return _q(F.conv_transpose2d(z_id.reshape(z_id.shape[0], -1, 1, 1), p["generator.up1.weight"].float(),
+                                 p["generator.up1.bias"].float()))
+
+
+def gen_block_bf16_storage(y_prev, za, z_id, p, backbone, num_blocks, k):
+    """AADBlk_k (AAD_ResBlk.forward, AADLayer.py:74-80) from the *stored* previous block output
+    (k = 1: m1 from up1_bf16_storage), including the x2 upsample in front of it (AEI_Net.py:125-137).
+    Returns the stored block output (bf16-valued; k = 8: the fp32 pre-tanh sum).  Taking the stored
+    input of one block isolates that block's arithmetic: the per-stage parity tests feed it the
+    GPU's own AADBlk_{k-1} output."""
+    cin, cout, _ca = GEN_BLOCKS[backbone][k - 1]
+    z_id = z_id.float().reshape(z_id.shape[0], -1)
+    if k == 1:
+        m, m_stats = y_prev, None
+    else:
+        u = up2x(y_prev)
+        m = _q(u)
+        m_stats = _in_stats(u) if (y_prev.shape[-1] >= 32 and cin % 64 == 0) else None
+    pre = f"generator.AADBlk{k}"
+    x, st = m, m_stats
+    for i in range(num_blocks):
+        a = aad_layer_bf16_storage(x, za, z_id, p, f"{pre}.add_blocks.{3 * i}", st)
+        x = F.conv2d(a, _wq(p, f"{pre}.add_blocks.{3 * i + 2}.weight"), None, padding=1)
+        st = None
+        if i < num_blocks - 1:
+            x = _q(x)
+    if cin != cout:
+        a = aad_layer_bf16_storage(m, za, z_id, p, f"{pre}.last_add_block.0", m_stats)
+        y = x + F.conv2d(a, _wq(p, f"{pre}.last_add_block.2.weight"), None, padding=1)
+    else:
+        y = x + m
+    return y if k == 8 else _q(y)
+
+
+def generator_bf16_storage(z_attr, z_id, p, backbone="unet", num_blocks=2):
+    """AADGenerator.forward (AEI_Net.py:122-139) with bf16 storage -> (tanh fp32, [y_1 .. y_8] block
+    outputs as stored, y_8 the pre-tanh sum)."""
+    y = up1_bf16_storage(z_id, p)
+    blocks = []
+    for k in range(1, 9):
+        y = gen_block_bf16_storage(y, z_attr[k - 1], z_id, p, backbone, num_blocks, k)
+        blocks.append(y)
+    return torch.tanh(blocks[-1]), blocks
+
+
+@torch.no_grad()
+def aei_forward_bf16_storage(p, xt, z_id, backbone="unet", num_blocks=2, store=torch.bfloat16):
+    """AEI_Net.forward (AEI_Net.py:153-156) as the bf16 runtime stores it -> (Y, attr, blocks, y_u8_src).
+
+    Y is the bf16-rounded tanh output, attr the stored encoder maps, blocks the stored AADBlk1..7
+    outputs (+ AADBlk8's pre-tanh sum), and y_u8_src the fp32 tanh the uint8 frame is made from."""
+    prev, _STORE[0] = _STORE[0], store
+    try:
+        xt = _q(xt.float())
+        attr = encoder_bf16_storage(xt, p, backbone)
+        t, blocks = generator_bf16_storage(attr, z_id, p, backbone, num_blocks)
+        return _q(t), attr, blocks, t
+    finally:
+        _STORE[0] = prev
+
+
+def fp16_reference_forward(p, xt, z_id, backbone="unet", num_blocks=2):
+    """The reference GPU precision (inference.py:30 G.half(), core.py:21,66 fp16 inputs): the same
+    restatement evaluated in float16 end to end (CPU fp16 ops), returned as fp32."""
+    p16 = {k: (v.half() if v.is_floating_point() else v) for k, v in p.items()}
+    y, _ = aei_forward(p16, xt.half(), z_id.half(), backbone, num_blocks, dtype=torch.float16)
+    return y.float()
+
+
+# ----------------------------------------------------------------------------
 # pipeline arithmetic on either side of the generator
 # ----------------------------------------------------------------------------
 def transform_target(crops_u8_bgr: np.ndarray) -> torch.Tensor:

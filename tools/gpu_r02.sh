@@ -1,0 +1,13 @@
+# round-2 GPU session helper: bash tools/gpu_r02.sh <what...>  (each step time-limited, stops at the first failure)
+set -e
+export PYTHONUNBUFFERED=1
+mkdir -p gpurun_out
+for w in "$@"; do
+  case $w in
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputests.log 2>&1 ;;
+    bisect) timeout -k 10 300 python tools/bf16_bisect.py --backbone unet --num-blocks 2 --fp16 --json gpurun_out/bisect_unet2.json > gpurun_out/bisect_unet2.log 2>&1
+            timeout -k 10 300 python tools/bf16_bisect.py --backbone linknet --num-blocks 3 --fp16 --json gpurun_out/bisect_linknet3.json > gpurun_out/bisect_linknet3.log 2>&1 ;;
+    bench) timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 ;;
+    *) echo "unknown step $w"; exit 2 ;;
+  esac
+done
