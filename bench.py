@@ -1,25 +1,33 @@
 """Benchmark: swapped 256x256 frames/s of GHOST's swap forward on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N --steps K --warmup W --batch 64 --backbone unet --num-blocks 2]
+    python bench.py [--gpus N --steps K --warmup W --batch 64 --backbone unet --num-blocks 2 --identities 1]
     torchrun --nproc-per-node N bench.py --gpus N ...     (driver's multi-GPU form)
 
-One step = one faceshifter_batch of B synthetic aligned-face crops per GPU, device-resident:
-uint8 BGR crops -> normalise -> AEI_Net (encoder + AAD generator, bf16) -> tanh -> uint8 BGR,
-then (N > 1) an RCCL all-gather of every rank's swapped crops (frame order = rank order).
-Weak scaling: B frames per GPU; value = N*B*K / max-over-ranks wall time of the K timed steps.
+Headline (BASELINE config 2 at N = 1, config 4 at N > 1): one step = one faceshifter_batch of B
+synthetic aligned-face crops per GPU, device-resident: uint8 BGR crops -> normalise -> AEI_Net
+(encoder + AAD generator, bf16) -> tanh -> uint8 BGR, then (N > 1) an RCCL all-gather of every
+rank's swapped crops (frame order = rank order).  Weak scaling: B frames per GPU;
+value = N*B*K / max-over-ranks wall time of the K timed steps.  ``--identities 4 --backbone linknet
+--num-blocks 3`` makes the headline BASELINE config 5 (mixed-identity batches, per-sample identity
+rows).
 
-Besides the JSON line's throughput, it reports
-* roofline: the dominant AAD kernel, aad_v4_kernel<64,2,true> (the two AADLayers of AADBlk8 that
-  read the same h_in / z_attr at 256x256, h_in sampled through the bilinear x2 upsample of AADBlk7's
-  128x128 output), HBM-bound: its algorithmic bytes per launch by SURVEY.md §8d's formula (fixed
-  regardless of fusion: sum over its two AADLayers of |h_in| + |z_attr| + |out|, 64 frames at
-  256x256x64 bf16 = 3.22 GB) / its average launch time, timed with HIP events recorded around each of its
-  launches on the launch stream inside the timed region; `traffic` = PMC-measured HBM bytes per
-  launch of the same kernel from profiles/traffic_latest.json;
+Besides the JSON line's throughput, rank 0 at N = 1 reports
+* roofline: the dominant AAD kernel, aad_v4_kernel<64,2,true> (the two AADLayers of AADBlk8 that read
+  the same h_in / z_attr at 256x256, h_in sampled through the bilinear x2 upsample of AADBlk7's
+  128x128 output), HBM-bound.  ``achieved`` = the bytes that fused kernel must move at minimum (the
+  128x128 source of h_in once, z_attr8 once, the two 256x256 outputs: 2.147 GB at B = 64) / its
+  average launch time, timed with HIP events recorded on the launch stream around each of its
+  launches inside the timed region; ``traffic`` = its PMC-measured HBM bytes per launch
+  (profiles/traffic_latest.json); ``formula_frac`` keeps SURVEY.md §8d's per-layer formula
+  (|h_in|+|z_attr|+|out| per AADLayer, 3.22 GB), which counts bytes the fused kernel never moves;
 * roofline_conv3x3 (MFMA-bound, all generator 3x3 convs) and aad_decoder_gbs (SURVEY.md §8d
-  definition: 135.58 MB/frame of AADLayer bytes / total AAD kernel time);
+  definition: AADLayer bytes / total AAD kernel time);
+* legs: the D2H-inclusive config 2 (pinned host output, copy overlapped with the next batch), config 5
+  (4 identities, linknet/3, mixed batches), config 3 (a 900-frame 1080p video: H2D of the crops,
+  BS-batched swaps with per-batch D2H, `present` re-insertion, H2D of the full frames, paste-back
+  blend, D2H of the blended frames), ArcFace embeddings/s;
 * cpu_baseline: the CPU restatement (oracle/aei_ref.py, fp32, same ATen op sequence as the
-  reference) on this host's cores over a bounded sample (rank 0, N=1 only).
+  reference) on this host's CPUs at B = 1 and B = 64, 1 warm-up + 3 timed iterations each.
 """
 from __future__ import annotations
 
@@ -39,7 +47,7 @@ sys.path.insert(0, REPO)
 try:
     BASELINE_METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 except (OSError, ValueError, KeyError):
-    BASELINE_METRIC = "swapped frames/sec at 256\u00d7256 bf16, 1/2/4/8 MI355X; AAD decoder HBM GB/s"
+    BASELINE_METRIC = "swapped frames/sec at 256×256 bf16, 1/2/4/8 MI355X; AAD decoder HBM GB/s"
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA spec
 AAD_BYTES_PER_FRAME = {"unet": 135.58e6, "linknet": 156.02e6, "resnet": 135.58e6}
@@ -53,11 +61,14 @@ def parse():
     ap.add_argument("--batch", type=int, default=64, help="frames per GPU per step")
     ap.add_argument("--backbone", default="unet")
     ap.add_argument("--num-blocks", type=int, default=2)
+    ap.add_argument("--identities", type=int, default=1, help="source identities mixed in every batch (config 5: 4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--legs", default="d2h,config5,video,arcface",
+                    help="side measurements at N=1 (comma list of d2h, config5, video, arcface; '' = none)")
+    ap.add_argument("--video", type=int, default=900, help="frames of the config-3 video leg")
+    ap.add_argument("--cpu-batches", default="1,64", help="CPU baseline batch sizes ('' = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
-    ap.add_argument("--arc-batch", type=int, default=64,
-                    help="faces per ArcFace (iresnet100) embedding batch in the side measurement (0 = skip)")
+    ap.add_argument("--arc-batch", type=int, default=64, help="faces per ArcFace embedding batch in its leg")
     return ap.parse_args()
 
 
@@ -91,9 +102,36 @@ def arcface_flops_per_face(layers=(3, 13, 30, 3)):
     return fl + 2.0 * 512 * 49 * 512
 
 
+def make_model(backbone, nb, dt, dev):
+    from ghost_amd.network import AEI_Net
+    from oracle.aei_ref import make_weights, param_specs   # deterministic synthetic weights (no checkpoint offline)
+    G = AEI_Net(backbone, num_blocks=nb, c_id=512, compute_dtype=dt).eval()
+    G.load_state_dict(make_weights(param_specs(backbone, nb)))
+    return G.to(dev)
+
+
+def identity_rows(n, dev):
+    return torch.from_numpy(np.random.Generator(np.random.PCG64(1)).normal(size=(n, 512)).astype(np.float32)).to(dev)
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+# ---------------------------------------------------------------------------------------------
+# side legs (rank 0, N = 1)
+# ---------------------------------------------------------------------------------------------
 def arcface_leg(dev, n, steps):
-    """Side measurement (not the headline): iresnet100 bf16 embeddings/s on device u8 224x224 crops
-    (normalise + 0.5x resize + network), the per-frame identity path of config 5."""
+    """iresnet100 bf16 embeddings/s on device u8 224x224 crops (normalise + 0.5x resize + network),
+    the per-frame identity path of config 5.  Parity of the network itself is unpinned (the IResNet
+    source and weights are not in the reference tree)."""
     from ghost_amd.arcface import iresnet100
     from oracle.arcface_ref import make_weights, param_specs
     net = iresnet100(fp16=False, compute_dtype=torch.bfloat16).eval()
@@ -101,42 +139,194 @@ def arcface_leg(dev, n, steps):
     net = net.to(dev)
     crops = torch.from_numpy(np.random.Generator(np.random.PCG64(5)).integers(0, 256, (n, 224, 224, 3),
                                                                            dtype=np.uint8)).to(dev)
-    for _ in range(2):
-        net.embed_u8(crops)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(steps):
-        net.embed_u8(crops)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / steps
+    el = timed(lambda: net.embed_u8(crops), steps, 2)
+    ms = el * 1e3 / steps
     fl = arcface_flops_per_face() * n
     return {"model": "iresnet100 bf16 (synthetic weights), u8 224x224 crops -> 512-d embeddings", "batch": n,
+            "parity": "unpinned (no IResNet source, weights or fixtures in the reference)",
             "ms_per_batch": round(ms, 3), "embeddings_per_s": round(n / (ms / 1e3), 1),
             "gflop_per_face": round(arcface_flops_per_face() / 1e9, 2),
             "mfma_tflops": round(fl / (ms / 1e3) / 1e12, 1),
             "mfma_frac": round(fl / (ms / 1e3) / 1e12 / BF16_PEAK_TFLOPS, 4)}
 
 
-def cpu_baseline(backbone, nb, seconds):
-    """Oracle (CPU fp32 restatement) frames/s on this host, bounded sample."""
+def d2h_leg(G, crops, z, steps):
+    """Config 2 including faceshifter_run.py:22's .cpu(): each batch's uint8 swaps are copied into a
+    pinned host buffer on a copy stream while the next batch is swapped (two device/host slots)."""
+    dev = crops.device
+    B = crops.shape[0]
+    outs = [torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+    hosts = [torch.empty(B, 256, 256, 3, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    copy = torch.cuda.Stream(dev)
+    cur = torch.cuda.current_stream(dev)
+    done = [torch.cuda.Event() for _ in range(2)]
+    copied = [None, None]
+    k = [0]
+
+    def step():
+        s = k[0] % 2
+        if copied[s] is not None:
+            cur.wait_event(copied[s])          # the copy still reading this slot
+        G.swap_u8(crops, z, out=outs[s])
+        done[s].record(cur)
+        with torch.cuda.stream(copy):
+            copy.wait_event(done[s])
+            hosts[s].copy_(outs[s], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(copy)
+            copied[s] = ev
+        k[0] += 1
+
+    def run():
+        step()
+
+    el = timed(run, steps, 3)
+    copy.synchronize()
+    return {"workload": f"config 2 + D2H: batch={B} unet/2 bf16 swaps copied to pinned host memory per batch "
+                        "(copy stream, overlapped with the next batch's swap)",
+            "frames_per_s": round(B * steps / el, 1), "ms_per_batch": round(el * 1e3 / steps, 3),
+            "d2h_bytes_per_batch": B * 196608}
+
+
+def config5_leg(dev, B, steps, warmup, n_ident=4):
+    """BASELINE config 5 on one GPU: linknet/3, every batch mixes 4 source identities (per-sample
+    identity rows into the AAD identity path, dp.swap_mixed_identities); per GPU of the 8-GPU config."""
+    from ghost_amd.inference.dp import swap_mixed_identities
+    G = make_model("linknet", 3, torch.bfloat16, dev)
+    crops = torch.from_numpy(np.random.Generator(np.random.PCG64(77)).integers(0, 256, size=(B, 256, 256, 3),
+                                                                            dtype=np.uint8)).to(dev)
+    zs = identity_rows(n_ident, dev)
+    idx = torch.arange(B, device=dev) % n_ident
+    out = torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev)
+    el = timed(lambda: swap_mixed_identities(crops, idx, zs, G, out=out), steps, warmup)
+    del G
+    torch.cuda.empty_cache()
+    return {"workload": f"config 5 per GPU: batch={B} crops mixing {n_ident} identities, AEI_Net linknet "
+                        "num_blocks=3 bf16, u8 in -> u8 out", "frames_per_s": round(B * steps / el, 1),
+            "ms_per_batch": round(el * 1e3 / steps, 3)}
+
+
+def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
+    """BASELINE config 3 on one GPU, after host detection/alignment (models absent here: synthetic
+    pre-aligned crops, affine transforms and masks).  Timed end to end:
+      1. swap_identity_frames (core.py:57-88): H2D of the identity's crops, BS-batched swaps with a
+         per-batch D2H of the uint8 result (overlapped), `present` re-insertion (5 % faceless frames);
+      2. paste-back (get_final_video, video_processing.py:207-241): the full 1080p frames H2D in chunks,
+         warp + mask composite on the device (blend.blend_swaps) from the device-resident swaps, D2H of
+         the blended frames; copies on their own streams overlap the previous chunk's blend.
+    The reference's cv2.resize 256 -> 224 of the swap is folded into the warp (transform scaled by
+    256/224, the mask made at 256); landmarks / mask construction / the video writer stay on the host."""
+    from ghost_amd.inference.blend import blend_swaps
+    from ghost_amd.inference.core import swap_identity_frames
+    rng = np.random.Generator(np.random.PCG64(9))
+    present = (rng.random(n_frames) > 0.05).astype(np.int64)
+    n_face = int(present.sum())
+    crops = rng.integers(0, 256, size=(n_face, 256, 256, 3), dtype=np.uint8)
+    tile = torch.from_numpy(rng.integers(0, 256, size=(16, H, W, 3), dtype=np.uint8))
+    frames_h = torch.empty(n_frames, H, W, 3, dtype=torch.uint8, pin_memory=True)
+    for i in range(0, n_frames, 16):
+        frames_h[i:i + 16] = tile[:min(16, n_frames - i)]
+    # crop <- frame affine maps (a face of ~300 px somewhere in the frame), scaled by 256/224
+    ang = rng.uniform(-0.3, 0.3, n_frames)
+    sc = rng.uniform(0.7, 0.9, n_frames)
+    tx, ty = rng.uniform(600, 1300, n_frames), rng.uniform(200, 700, n_frames)
+    mats = np.zeros((n_frames, 2, 3), np.float32)
+    mats[:, 0, 0], mats[:, 0, 1] = sc * np.cos(ang), -sc * np.sin(ang)
+    mats[:, 1, 0], mats[:, 1, 1] = sc * np.sin(ang), sc * np.cos(ang)
+    mats[:, 0, 2] = -(mats[:, 0, 0] * tx + mats[:, 0, 1] * ty)
+    mats[:, 1, 2] = -(mats[:, 1, 0] * tx + mats[:, 1, 1] * ty)
+    mats *= 256.0 / 224.0
+    yy, xx = np.mgrid[0:256, 0:256]
+    mask = np.clip(1.0 - (((yy - 128) / 110.0) ** 2 + ((xx - 128) / 95.0) ** 2), 0, 1).astype(np.float32)
+    masks_d = torch.from_numpy(np.broadcast_to(mask, (n_frames, 256, 256)).copy()).to(dev)
+    mats_d = torch.from_numpy(mats).to(dev)
+    valid_d = torch.from_numpy(present.astype(np.int32)).to(dev)
+    z = identity_rows(1, dev)
+    CH = 32
+    bufs = [torch.empty(CH, H, W, 3, dtype=torch.uint8, device=dev) for _ in range(2)]
+    s_in, s_out = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    cur = torch.cuda.current_stream(dev)
+
+    def run():
+        final, swaps_d = swap_identity_frames(crops, present, z, G, BS=BS, device=dev, return_device=True)
+        # frame-indexed device swaps (faceless frames: a zero row, masked off by valid)
+        idx = torch.from_numpy(np.maximum(np.cumsum(present) - 1, 0)).to(dev)
+        swaps_f = swaps_d.index_select(0, idx)
+        freed = [None, None]
+        for c, f0 in enumerate(range(0, n_frames, CH)):
+            f1 = min(n_frames, f0 + CH)
+            b = bufs[c % 2]
+            with torch.cuda.stream(s_in):
+                if freed[c % 2] is not None:
+                    s_in.wait_event(freed[c % 2])
+                b[:f1 - f0].copy_(frames_h[f0:f1], non_blocking=True)
+                loaded = torch.cuda.Event()
+                loaded.record(s_in)
+            cur.wait_event(loaded)
+            blend_swaps(b[:f1 - f0], swaps_f[f0:f1], masks_d[f0:f1], mats_d[f0:f1], valid_d[f0:f1])
+            blended = torch.cuda.Event()
+            blended.record(cur)
+            with torch.cuda.stream(s_out):
+                s_out.wait_event(blended)
+                frames_h[f0:f1].copy_(b[:f1 - f0], non_blocking=True)   # result_frames[i] = final
+                ev = torch.cuda.Event()
+                ev.record(s_out)
+                freed[c % 2] = ev
+        s_out.synchronize()
+        return final
+
+    run()                                   # warm-up (allocations, first launches)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    final = run()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    assert len(final) == n_frames and sum(1 for f in final if len(f)) == n_face
+    return {"workload": f"config 3: {n_frames}-frame {W}x{H} video, 1 identity, {n_face} frames with a face; "
+                        f"crops H2D -> swaps (BS={BS}, per-batch D2H) -> present re-insertion -> frames H2D -> "
+                        "device paste-back -> frames D2H (host detect/align/landmarks/mask/writer excluded)",
+            "frames_per_s": round(n_frames / el, 1), "seconds": round(el, 3),
+            "host_bytes_moved": int(n_face * 196608 * 2 + 2 * n_frames * H * W * 3)}
+
+
+def host_cpu_budget():
+    """CPUs this process may use: the cgroup quota when one is set (the GPU box gives a job a share
+    of a large host, whose os.cpu_count() is many times that share), else the affinity mask."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_baseline(backbone, nb, batches):
+    """Oracle (CPU fp32 restatement, same ATen op sequence as the reference) frames/s on this host:
+    BASELINE.md §4 — B in {1, 64}, 1 warm-up + 3 timed iterations each, time.perf_counter."""
     from oracle import aei_ref
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cpu_budget()
     torch.set_num_threads(threads)
     p = aei_ref.make_weights(aei_ref.param_specs(backbone, nb))
-    bs = 4
-    xt, z = aei_ref.make_inputs(bs, seed=3)
-    aei_ref.aei_forward(p, xt[:1], z[:1], backbone, nb)       # warm-up
-    frames, t0 = 0, time.perf_counter()
-    while True:
-        aei_ref.aei_forward(p, xt, z, backbone, nb)
-        frames += bs
+    per_b = {}
+    for bs in batches:
+        xt, z = aei_ref.make_inputs(bs, seed=3)
+        aei_ref.aei_forward(p, xt, z, backbone, nb)        # warm-up
+        t0 = time.perf_counter()
+        for _ in range(3):
+            aei_ref.aei_forward(p, xt, z, backbone, nb)
         el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": round(frames / el, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} frames of {backbone}/{nb} fp32 in batches of {bs} (oracle/aei_ref.py), {el:.1f}s"}
+        per_b[str(bs)] = {"frames_per_s": round(3 * bs / el, 3), "s_per_batch": round(el / 3, 3)}
+    best = max(batches)
+    return {"value": per_b[str(best)]["frames_per_s"], "unit": "frames/s", "cores": threads, "kind": "port",
+            "os_cpu_count": os.cpu_count(), "by_batch": per_b,
+            "sample": f"{backbone}/{nb} fp32 (oracle/aei_ref.py) at B in {list(batches)}: 1 warm-up + 3 timed "
+                      f"iterations each on {threads} threads (the process's CPU quota); value = B={best}"}
 
 
 def main():
@@ -150,18 +340,17 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
-    from ghost_amd.network import AEI_Net
-    from oracle.aei_ref import make_weights, param_specs   # deterministic synthetic weights (no checkpoint offline)
-
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
-    G = AEI_Net(a.backbone, num_blocks=a.num_blocks, c_id=512, compute_dtype=dt).eval()
-    G.load_state_dict(make_weights(param_specs(a.backbone, a.num_blocks)))
-    G = G.to(dev)
+    G = make_model(a.backbone, a.num_blocks, dt, dev)
 
     B = a.batch
     rng = np.random.Generator(np.random.PCG64(1000 + rank))
     crops = torch.from_numpy(rng.integers(0, 256, size=(B, 256, 256, 3), dtype=np.uint8)).to(dev)
-    z = torch.from_numpy(np.random.Generator(np.random.PCG64(1)).normal(size=(1, 512)).astype(np.float32)).to(dev)
+    zs = identity_rows(max(1, a.identities), dev)
+    if a.identities > 1:      # config 5: per-sample identity rows (dp.swap_mixed_identities)
+        z = zs.index_select(0, torch.arange(B, device=dev) % a.identities).contiguous()
+    else:
+        z = zs[:1]
     # swap -> all-gather of the uint8 swaps to every rank; the gather of step k overlaps step k + 1
     # (dp.GatherPipeline; GHOST_DP_OVERLAP=0 gathers synchronously after each step)
     from ghost_amd.inference.dp import GatherPipeline
@@ -215,38 +404,46 @@ def main():
     if rank == 0:
         frames = world * B * a.steps
         value = frames / el
+        cfg = "config 5 (mixed identities)" if a.identities > 1 else ("config 4" if world > 1 else "config 2")
         res = {
             "metric": BASELINE_METRIC,
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.dtype if a.dtype == "fp32" else "bf16", "data": "synthetic",
-            "config": {"workload": f"batch={B} synthetic 256x256 aligned faces per GPU, AEI_Net {a.backbone} "
-                                   f"num_blocks={a.num_blocks}, faceshifter_batch (u8 in -> u8 out)"
+            "config": {"workload": f"BASELINE {cfg}: batch={B} synthetic 256x256 aligned faces per GPU"
+                                   + (f" mixing {a.identities} identities" if a.identities > 1 else "")
+                                   + f", AEI_Net {a.backbone} num_blocks={a.num_blocks}, faceshifter_batch "
+                                     "(u8 in -> u8 out, device-resident; D2H in legs.d2h)"
                                    + (", RCCL all-gather of swapped crops" if world > 1 else ""),
                        "global_batch": world * B, "per_gpu_batch": B, "backbone": a.backbone,
-                       "num_blocks": a.num_blocks, "parallelism": f"dp{world}"},
+                       "num_blocks": a.num_blocks, "identities": max(1, a.identities),
+                       "parallelism": f"dp{world}"},
         }
         if prof and classes["aad_dual_256"]["launches"]:
             c = classes["aad_dual_256"]
-            per_launch_bytes = c["bytes"] / c["launches"]
+            per_launch_formula = c["bytes"] / c["launches"]
             per_launch_s = c["ms"] / c["launches"] / 1e3
-            ach = per_launch_bytes / per_launch_s / 1e9
             ca8 = 32 if a.backbone == "linknet" else 64     # z_attr8 channels (AEI_Net.py:110,118)
             # layers in the kernel: the formula bytes per launch are L * B*256^2*(2*64 + Ca)*2
-            nl = max(1, round(per_launch_bytes / (B * 65536 * (2 * 64 + ca8) * 2)))
+            nl = max(1, round(per_launch_formula / (B * 65536 * (2 * 64 + ca8) * 2)))
+            # minimum bytes of the fused kernel: h_in's 128x128 source once, z_attr8 once, nl outputs
+            per_launch_min = B * (128 * 128 * 64 + 65536 * ca8 + nl * 65536 * 64) * 2.0
+            ach = per_launch_min / per_launch_s / 1e9
             kname = f"aad_v4_kernel<{ca8}, {nl}, true>"
-            what = ("two AADLayers sharing h_in/z_attr" if nl == 2 else
-                    "the first AADLayer (its last_add_block partner runs in the fused tail)")
-            res["roofline"] = {"kernel": f"{kname}: AADBlk8's block-input AAD kernel at 256x256, {what}, h_in = "
-                                         "bilinear x2 of the 128x128 block output sampled in-kernel (IN-normalise, "
-                                         "sigmoid mask, MFMA gamma/beta, blend, ReLU), next tile in flight",
+            res["roofline"] = {"kernel": f"{kname}: AADBlk8's block-input AAD kernel at 256x256, {nl} AADLayer(s) "
+                                         "sharing h_in/z_attr, h_in = bilinear x2 of the 128x128 block output "
+                                         "sampled in-kernel (IN-normalise, sigmoid mask, MFMA gamma/beta, blend, "
+                                         "ReLU)",
                                "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kname),
-                               "bytes_note": "achieved counts SURVEY.md 8d bytes (|h_in|+|z_attr|+|out| per AADLayer, "
-                                             "h_in at 256x256); the kernel physically moves the 128x128 h_in once "
-                                             "for both layers: see physical_gbs / traffic",
-                               "bytes_per_launch": per_launch_bytes, "avg_launch_us": round(per_launch_s * 1e6, 2),
-                               "launches_timed": c["launches"]}
+                               "bytes_per_launch": per_launch_min,
+                               "bytes_note": "achieved = minimum bytes of the fused kernel (128x128 h_in source + "
+                                             "z_attr8 + outputs) / launch time; formula_* = SURVEY.md 8d's per-layer "
+                                             "|h_in|+|z_attr|+|out| with h_in counted at 256x256 per layer",
+                               "formula_bytes_per_launch": per_launch_formula,
+                               "formula_gbs": round(per_launch_formula / per_launch_s / 1e9, 1),
+                               "formula_frac": round(per_launch_formula / per_launch_s / 1e9 / HBM_PEAK_GBS, 4),
+                               "avg_launch_us": round(per_launch_s * 1e6, 2), "launches_timed": c["launches"]}
             tr = res["roofline"]["traffic"]
             if tr:
                 res["roofline"]["physical_gbs"] = round(tr["bytes_per_launch"] / per_launch_s / 1e9, 1)
@@ -265,10 +462,20 @@ def main():
             res["kernel_ms_per_step"] = {k: round(v["ms"] / a.steps, 3) for k, v in classes.items()}
             res["kernel_ms_per_step_note"] = ("aad_dual_256 from the timed region; the other classes from an "
                                               "untimed pass with every class bracketed by HIP events")
-        if world == 1 and a.arc_batch > 0:
-            res["arcface"] = arcface_leg(dev, a.arc_batch, max(3, a.steps // 2))
-        if world == 1 and a.cpu_seconds > 0:
-            res["cpu_baseline"] = cpu_baseline(a.backbone, a.num_blocks, a.cpu_seconds)
+        legs = [s for s in a.legs.split(",") if s] if world == 1 else []
+        if legs:
+            res["legs"] = {}
+        if "d2h" in legs:
+            res["legs"]["d2h"] = d2h_leg(G, crops, z, a.steps)
+        if "video" in legs and a.video > 0:
+            res["legs"]["config3_video"] = video_leg(G, dev, a.video)
+        if "config5" in legs:
+            res["legs"]["config5"] = config5_leg(dev, B, a.steps, 3)
+        if "arcface" in legs and a.arc_batch > 0:
+            res["legs"]["arcface"] = arcface_leg(dev, a.arc_batch, max(3, a.steps // 2))
+        batches = [int(b) for b in a.cpu_batches.split(",") if b]
+        if world == 1 and batches:
+            res["cpu_baseline"] = cpu_baseline(a.backbone, a.num_blocks, batches)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

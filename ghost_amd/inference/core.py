@@ -33,17 +33,39 @@ def transform_target_to_torch(resized_frs: np.ndarray, half: bool = True, device
 
 
 def swap_identity_frames(resized_frs: np.ndarray, present: Sequence[int], source_embed: torch.Tensor, G,
-                         BS: int = 60, device=None) -> List:
+                         BS: int = 60, device=None, return_device: bool = False):
     """core.py:57-88 for one identity: batched swap of the present crops, then re-insert ``[]``
-    for frames without a face so the result is indexed by frame (bit-exact crop indices)."""
+    for frames without a face so the result is indexed by frame (bit-exact crop indices).
+
+    The crops go to the device once (core.py:63 transfers the identity's frames at once); each
+    batch of BS is swapped into a device buffer and copied to pinned host memory on a copy stream
+    while the next batch is swapped (the reference's per-batch ``.cpu()``, faceshifter_run.py:22,
+    without serialising the GPU on it).  ``return_device=True`` also returns the device-resident
+    uint8 swaps [N,256,256,3] (for a device paste-back, ``blend.blend_swaps``)."""
     device = torch.device(device or "cuda")
-    crops = torch.from_numpy(np.ascontiguousarray(resized_frs)).to(device) if len(resized_frs) else None
-    outputs = []
-    if crops is not None:
-        for i in range(0, crops.shape[0], BS):
-            outputs.append(G.swap_u8(crops[i:i + BS], source_embed).cpu().numpy())
-    model_output = np.concatenate(outputs) if outputs else np.zeros((0, 256, 256, 3), np.uint8)
-    return reinsert_present(model_output, present)
+    n = len(resized_frs)
+    if n == 0:
+        final = reinsert_present(np.zeros((0, 256, 256, 3), np.uint8), present)
+        return (final, None) if return_device else final
+    host_in = torch.from_numpy(np.ascontiguousarray(resized_frs))
+    crops = host_in.pin_memory().to(device, non_blocking=True)
+    z = source_embed.to(device)
+    out = torch.empty(n, 256, 256, 3, dtype=torch.uint8, device=device)
+    host = torch.empty(n, 256, 256, 3, dtype=torch.uint8, pin_memory=True)
+    cur = torch.cuda.current_stream(device)
+    copy = torch.cuda.Stream(device)
+    for i in range(0, n, BS):
+        j = min(n, i + BS)
+        G.swap_u8(crops[i:j], z, out=out[i:j])
+        done = torch.cuda.Event()
+        done.record(cur)
+        with torch.cuda.stream(copy):
+            copy.wait_event(done)
+            host[i:j].copy_(out[i:j], non_blocking=True)
+    copy.synchronize()
+    out.record_stream(copy)
+    final = reinsert_present(host.numpy(), present)
+    return (final, out) if return_device else final
 
 
 def reinsert_present(model_output: np.ndarray, present: Sequence[int]) -> List:
