@@ -479,11 +479,19 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   }
 }
 
+// pixels per workgroup: one sample's block; C = 256 stages its weights once per 1024 pixels
+static int v3_ppw(int HW, int C) { return (HW >= 65536 || C == 256) ? 1024 : 512; }
+
 bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo) {
   if (dt != GHOST_BF16) return false;
-  const bool shape = (C == 64 && (Ca == 64 || Ca == 32)) || (C == 128 && (Ca == 128 || Ca == 64 || Ca == 32));
+  // C = 256 (the 64x64 stage): all four channel tiles' weight rows (139 KB at Ca = 128) resident, one
+  // workgroup per CU; the mask is computed in-kernel from the pixel's 256 channels, so no separate
+  // mask pass reads h_in (measured B = 64: the per-channel-tile aad_wide + mask pass took 92 + 25 us)
+  static const int c256 = GHOST_KNOB("GHOST_AAD_V3_C256", 1);
+  const bool shape = (C == 64 && (Ca == 64 || Ca == 32)) || (C == 128 && (Ca == 128 || Ca == 64 || Ca == 32)) ||
+                     (c256 && C == 256 && (Ca == 128 || Ca == 64));
   if (!shape || lda % 8 || ldh % 8 || ldo % 8) return false;
-  const int ppw = HW >= 65536 ? 1024 : 512;
+  const int ppw = v3_ppw(HW, C);
   return HW % ppw == 0 && (long)B * HW / ppw >= 32;
 }
 
@@ -498,7 +506,7 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
     a.idgb[l] = d.idgb[l]; a.out[l] = (bf16*)d.out[l]; a.ldo[l] = d.ldo[l];
   }
   a.lda = d.lda; a.ldh = d.ldh; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
-  a.PPW = d.HW >= 65536 ? 1024 : 512;
+  a.PPW = v3_ppw(d.HW, d.C);
   const bool up = d.up_H > 0;
   if (up) {
     if (4 * d.up_H * d.up_W != d.HW || d.up_W * 2 < 16 || (d.C != 64 && d.C != 128)) return -1;
@@ -559,6 +567,7 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   GHOST_V3W(128, 64, 2, false)
   // AADBlk7's block-input AADLayers read upsample2x(AADBlk6 output) on the fly (C = 128)
   GHOST_V3W(128, 128, 1, true) GHOST_V3W(128, 64, 1, true) GHOST_V3W(128, 32, 1, true)
+  GHOST_V3W(256, 128, 1, false) GHOST_V3W(256, 64, 1, false)
 #undef GHOST_V3W
 #undef GHOST_V3
   return -1;

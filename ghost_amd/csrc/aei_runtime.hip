@@ -1125,7 +1125,8 @@ extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, con
     return fail(GHOST_EINVAL, "aad_v3: up2x needs even H, W and C in {64, 128}");
   if (zup && (H % 2 || W % 2 || C != 64))
     return fail(GHOST_EINVAL, "aad_v3: z_attr through the upsample needs even H, W and C = 64");
-  const bool wide = C >= 256;   // aad_wide: one layer, C in {256, 512, 1024}, Ca <= 512
+  // aad_wide: one layer, C in {256, 512, 1024}, Ca <= 512, where the all-channel kernel does not fit
+  const bool wide = C >= 256 && !aad_v3_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[0]);
   if (wide && (L != 1 || up2x || zup || !aad_wide_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[0])))
     return fail(GHOST_EINVAL, "aad_wide: unsupported shape (one layer, C in {256,512,1024}, Ca <= 512)");
   for (int l = 0; l < L && !wide; ++l)

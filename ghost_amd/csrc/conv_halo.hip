@@ -25,23 +25,32 @@
 
 namespace ghost {
 
-// tile configurations: TH x TW output pixels, WM x WN waves of 64 pixels x 64 channels each
-template <int TH_, int TW_, int WM_, int WN_>
+// tile configurations: TH x TW output pixels, WM x WN waves of 64 pixels x 64 channels each.
+// IMG > 1: the tile is IMG whole TH x TW images (64 pixels, one per wave) of consecutive samples,
+// each with its own zero-padded halo — the generator's 8x8 stage (AADBlk3), where a 16 x 16 tile
+// would be three quarters padding and the implicit GEMM re-reads every pixel nine times.
+template <int TH_, int TW_, int WM_, int WN_, int IMG_ = 1>
 struct HaloCfg {
-  static constexpr int TH = TH_, TW = TW_, WM = WM_, WN = WN_;
+  static constexpr int TH = TH_, TW = TW_, WM = WM_, WN = WN_, IMG = IMG_;
   static constexpr int BN = 64 * WN, NW = WM * WN;
   static constexpr int HWW = TW + 2, HHH = TH + 2;
-  static constexpr int HP = HHH * HWW;                      // halo pixels
+  static constexpr int HIMG = HHH * HWW;                    // halo pixels of one image
+  static constexpr int HP = IMG * HIMG;                     // halo pixels
   static constexpr int HPIECES = (HP + 15) / 16;            // DMA pieces of 16 pixels x 64 B
   static constexpr int WPIECES = 9 * BN / 16;               // pieces of 16 weight rows x 64 B
   static constexpr int HALO_B = HPIECES * 1024;
   static constexpr int LDS_B = HALO_B + 9 * BN * 64;
   static constexpr int HPW = (HPIECES + NW - 1) / NW;       // halo pieces per wave
   static constexpr int WPW = (WPIECES + NW - 1) / NW;       // weight pieces per wave
-  static_assert(TH * TW == 64 * WM, "each wave owns 64 output pixels");
+  static_assert(IMG * TH * TW == 64 * WM, "each wave owns 64 output pixels");
+  static_assert(IMG == 1 || (TH * TW == 64 && WN == 1), "multi-image tiles: one image per wave");
+  // wave w's pixel p (0..63): halo pixel index of tap (0, 0) and output offset within the tile
+  GHOST_DEV static int hrow0(int w) { return IMG > 1 ? 0 : w * (64 / TW); }
+  GHOST_DEV static int himg(int w) { return IMG > 1 ? w * HIMG : 0; }
 };
 using HaloWide = HaloCfg<16, 32, 8, 1>;    // W % 32 == 0: 16 x 32 tile, 8 waves, 75 KB LDS
 using HaloSmall = HaloCfg<16, 16, 4, 1>;   // W == 16: 16 x 16 tile, 4 waves, 57 KB LDS
+using HaloImg8 = HaloCfg<8, 8, 4, 1, 4>;   // 8 x 8 images, four per tile, 4 waves, 61 KB per stage
 
 struct HaloArgs {
   const bf16* x;
@@ -247,14 +256,15 @@ template <class G, bool RESW, bool STATS, int NCB, int DBG = 0>
 __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloArgs a) {
   static_assert(NCB % 2 == 0 && NCB <= 32 && (!RESW || NCB == 2), "channel blocks per tile");
   constexpr bool EPX = G::TW == 16;   // small tiles: overhang masking + the extended epilogue
-  static_assert(!(EPX && STATS), "IN partials only from the exact 16 x 32 tiles");
+  static_assert(!(EPX && STATS), "IN partials only from exact tiles");
   // DBG (experiments only, GHOST_HALO_DBG): 2 no halo DMA, 4 no weight DMA, 8 no LDS reads/MFMA,
   // 16 no output stores
   // RESW: Cin <= 64 and N == 64 — the whole weight tensor (<= 2 blocks x 36 KB) stays resident in
   // LDS for the kernel and only the halo (39 KB) streams per stage; otherwise every stage carries
   // its channel block's 9 x 64 weight rows too (75 KB).
   constexpr int TW = G::TW, HWW = G::HWW, HP = G::HP, HPIECES = G::HPIECES, WPIECES = G::WPIECES;
-  constexpr int HALO_B = G::HALO_B, NW = G::NW, HPW = G::HPW, WPW = G::WPW, RPW = 64 / TW;
+  constexpr int HALO_B = G::HALO_B, NW = G::NW, HPW = G::HPW, WPW = G::WPW, IMG = G::IMG;
+  constexpr int NMAX = IMG > 1 ? 1024 : 512;   // channel tables (N <= NMAX)
   constexpr int WBLK_B = 9 * 64 * 64;                           // one channel block of weights
   constexpr int STAGE_B = RESW ? HALO_B : HALO_B + WBLK_B;
   // two stage buffers as DISTINCT objects, read/written in an unrolled ping-pong: hipcc then proves
@@ -263,7 +273,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   __shared__ __attribute__((aligned(1024))) unsigned char lds0[STAGE_B];
   __shared__ __attribute__((aligned(1024))) unsigned char lds1[STAGE_B];
   __shared__ __attribute__((aligned(1024))) unsigned char ldsw[RESW ? 2 * WBLK_B : 16];
-  __shared__ __attribute__((aligned(16))) float s_sc[512], s_sh[512];   // N <= 512 (conv3x3_pp_takes / conv3x3_halo)
+  __shared__ __attribute__((aligned(16))) float s_sc[NMAX], s_sh[NMAX];   // N <= NMAX (conv3x3_pp_takes / conv3x3_halo)
   __shared__ __attribute__((aligned(16))) float s_ex[EPX ? 3 * 512 : 4];   // PReLU slope, scale2, shift2 (EPX)
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
   const int prow = lane >> 2, slot = lane & 3;
@@ -316,7 +326,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     const int tx = t % a.tiles_x;
     t /= a.tiles_x;
     const int ty = t % a.tiles_y;
-    r.base = (long)(t / a.tiles_y) * a.H * a.W;
+    r.base = (long)(t / a.tiles_y) * IMG * a.H * a.W;   // IMG > 1: tiles_x = tiles_y = 1, t = image group
     r.y0 = ty * G::TH;
     r.x0 = tx * TW;
     r.n0 = nt * 64;
@@ -334,10 +344,11 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     for (int j = 0; j < HPW; ++j) {
       const int piece = wid + j * NW;
       const int P = piece * 16 + prow;
-      const int hy = P / HWW, hx = P - hy * HWW;
+      const int im = IMG > 1 ? P / G::HIMG : 0, hp = P - im * G::HIMG;
+      const int hy = hp / HWW, hx = hp - hy * HWW;
       const int iy = t.y0 - 1 + hy, ix = t.x0 - 1 + hx;
       const bool ok = piece < HPIECES && P < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-      h_off[j] = ok ? (iy * a.W + ix) * a.ldx + ((slot ^ hswz(P)) * 8) : 0;
+      h_off[j] = ok ? ((im * a.H + iy) * a.W + ix) * a.ldx + ((slot ^ hswz(P)) * 8) : 0;
       h_ok |= (ok ? 1u : 0u) << j;
     }
   };
@@ -411,7 +422,8 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int P = (wid * RPW + (i * 16) / TW + dy) * HWW + (i * 16) % TW + lr + dx;
+        const int q = i * 16 + lr;   // the wave's pixel (row q / TW, column q % TW of its 64)
+        const int P = G::himg(wid) + (G::hrow0(wid) + q / TW + dy) * HWW + q % TW + dx;
         p[i] = *reinterpret_cast<const bf16x8*>(buf + P * 64 + ((lq ^ hswz(P)) * 16));
       }
     };
@@ -437,8 +449,9 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     if (a.res) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int oy = cur.y0 + wid * RPW + (i * 16) / TW, ox = cur.x0 + (i * 16) % TW + lr;
-        const long pix = cur.base + (long)oy * a.W + ox;
+        const int q = i * 16 + lr;
+        const int oy = cur.y0 + G::hrow0(wid) + q / TW, ox = cur.x0 + q % TW;
+        const long pix = cur.base + (IMG > 1 ? (long)wid * a.H * a.W : 0L) + (long)oy * a.W + ox;
         const bool in = !EPX || (oy < a.H && ox < a.W);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -448,8 +461,9 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int oy = cur.y0 + wid * RPW + (i * 16) / TW, ox = cur.x0 + (i * 16) % TW + lr;
-      const long pix = cur.base + (long)oy * a.W + ox;
+      const int q = i * 16 + lr;
+      const int oy = cur.y0 + G::hrow0(wid) + q / TW, ox = cur.x0 + q % TW;
+      const long pix = cur.base + (IMG > 1 ? (long)wid * a.H * a.W : 0L) + (long)oy * a.W + ox;
       if constexpr (EPX) {
         if (oy >= a.H || ox >= a.W) {
 #pragma unroll
@@ -575,10 +589,16 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       const float S1 = mean;            // record = (mean, centred sum of squares) of 64 pixels
       const float S2 = reduce16(v1);
       // lane (lr, lq) holds channel n0 + 16 (lr >> 2) + 4 lq + (lr & 3)
-      const int tile = (cur.y0 / G::TH) * a.tiles_x + cur.x0 / TW;
-      const long b = cur.base / ((long)a.H * a.W);
       const int c = cur.n0 + (lr >> 2) * 16 + lq * 4 + (lr & 3);
-      float* dst = a.in_part + ((((b * a.tiles_x * a.tiles_y) + tile) * 8 + wid) * (long)a.N + c) * 2;
+      float* dst;
+      if constexpr (IMG > 1) {   // the wave's 64 pixels are its whole image: one record per sample
+        const long b = cur.base / ((long)a.H * a.W) + wid;
+        dst = a.in_part + (b * (long)a.N + c) * 2;
+      } else {
+        const int tile = (cur.y0 / G::TH) * a.tiles_x + cur.x0 / TW;
+        const long b = cur.base / ((long)a.H * a.W);
+        dst = a.in_part + ((((b * a.tiles_x * a.tiles_y) + tile) * 8 + wid) * (long)a.N + c) * 2;
+      }
       *reinterpret_cast<float2*>(dst) = make_float2(S1, S2);
     }
   };
@@ -782,6 +802,12 @@ int convT_halo(const ConvDesc& d, hipStream_t s) {
 // quarter of the work (ArcFace 112 / 56 / 28 / 14: 100 / 77 / 77 / 77 % of the tile pixels used;
 // 7x7 and the generator's 8x8 and below stay on the implicit GEMM)
 static bool halo_exact_wide(const ConvDesc& d) { return d.Wi % HaloWide::TW == 0 && d.Hi % HaloWide::TH == 0; }
+// the 8 x 8 stage: four whole images per tile (HaloImg8)
+static bool halo_img8(const ConvDesc& d) {
+  static const int on = GHOST_KNOB("GHOST_HALO_IMG8", 1);
+  return on && d.Hi == HaloImg8::TH && d.Wi == HaloImg8::TW && d.B % HaloImg8::IMG == 0 && d.N <= 1024 &&
+         !d.prelu && !d.y2 && !d.res_first && !d.tanh_out && d.Cin % 64 == 0 && d.Cin <= 1024;
+}
 static bool halo_small_ok(const ConvDesc& d) {
   const long tx = (d.Wi + HaloSmall::TW - 1) / HaloSmall::TW, ty = (d.Hi + HaloSmall::TH - 1) / HaloSmall::TH;
   return 4L * d.Hi * d.Wi >= 3L * tx * ty * HaloSmall::TW * HaloSmall::TH;
@@ -793,7 +819,7 @@ bool conv3x3_halo_supported(const ConvDesc& d) {
   if (d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD || d.u8 || d.force_split) return false;
   if (d.Cin % 32 || d.ldx % 8 || d.N % 64 || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
   if (d.y2 && (d.ldy2 % 4 || (uintptr_t)d.y2 % 8 || !d.scale2 || !d.shift2)) return false;
-  if ((!halo_exact_wide(d) && !halo_small_ok(d)) || d.Kpad < 9 * d.Cin || d.Npad < d.N) return false;
+  if ((!halo_exact_wide(d) && !halo_small_ok(d) && !halo_img8(d)) || d.Kpad < 9 * d.Cin || d.Npad < d.N) return false;
   if ((uintptr_t)d.x % 16 || (uintptr_t)d.w % 16 || (uintptr_t)d.y % 8 || (d.res && (uintptr_t)d.res % 8)) return false;
   if ((long)d.Hi * d.Wi * d.ldx >= (1L << 31) || (long)d.Npad * d.Kpad >= (1L << 31)) return false;   // 32-bit offsets
   // measured (tools/bench_ops.py, B = 64): faster than the implicit GEMM at every generator stage
@@ -848,7 +874,7 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   a.prelu = d.prelu; a.y2 = (bf16*)d.y2; a.scale2 = d.scale2; a.shift2 = d.shift2; a.ldy2 = d.ldy2;
   a.res_first = d.res_first;
   a.tiles_x = (d.Wi + G::TW - 1) / G::TW; a.tiles_y = (d.Hi + G::TH - 1) / G::TH; a.nNt = d.N / 64;
-  a.ntiles = d.B * a.tiles_x * a.tiles_y * a.nNt;
+  a.ntiles = d.B / G::IMG * a.tiles_x * a.tiles_y * a.nNt;
   static const int dbg = GHOST_KNOB("GHOST_HALO_DBG", 0);
   a.dbg = dbg;
   const int g = a.ntiles < num_cus() ? a.ntiles : num_cus();
@@ -871,7 +897,7 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
     }
   }
 #endif
-  constexpr bool CAN_ST = G::TW == 32;
+  constexpr bool CAN_ST = G::TW == 32 || G::IMG > 1;
 #define GHOST_PP(R, ST, NB) \
   hipLaunchKernelGGL((conv3x3_halo_pp_kernel<G, R, ST, NB>), dim3((unsigned)g), dim3(NT), 0, s, a)
 #define GHOST_PP2(R, NB)                                  \
@@ -903,6 +929,12 @@ bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
   static const int pp = GHOST_KNOB("GHOST_HALO_PP", 1);
   if (!conv3x3_halo_supported(d)) return false;
   if (d.prelu || d.y2 || d.res_first) return false;   // epilogue variants of the non-persistent kernel only
+  if (halo_img8(d)) {
+    const int ncb = d.Cin / 32;
+    const bool ok8 = ncb == 2 || ncb == 4 || ncb == 8 || ncb == 16 || ncb == 32;
+    if (ok8 && nrec) *nrec = 1;   // a wave's 64 pixels are one whole image
+    return ok8;
+  }
   const bool wide = halo_exact_wide(d);
   static const int max_cin = GHOST_KNOB("GHOST_HALO_PP_MAXCIN", 1024);
   // measured A/B (B = 64): the persistent form wins at every generator shape with W % 32 == 0 (256x256:
@@ -916,6 +948,7 @@ bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
 
 int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
   if (!conv3x3_halo_supported(d)) return -1;
+  if (halo_img8(d)) return conv3x3_pp_takes(d, nullptr) ? halo_pp_launch<HaloImg8>(d, s) : -1;
   if (conv3x3_pp_takes(d, nullptr)) return halo_pp_launch<HaloWide>(d, s);
   if (d.in_part) return -1;   // only the persistent 16 x 32 kernel writes InstanceNorm partials
   static const int pp = GHOST_KNOB("GHOST_HALO_PP", 1);

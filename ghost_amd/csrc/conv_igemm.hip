@@ -46,6 +46,7 @@ struct ConvArgs {
   int nsplit, kt_per_split;
   float slope;
   int tanh_out;
+  int nmajor;           // 1: tiles ordered N-major, so each XCD's contiguous run of tiles shares weight rows
 };
 
 // ---------------------------------------------------------------------------
@@ -385,6 +386,18 @@ GHOST_DEV void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// wait until at most `after` stages of LPS DMA instructions each are still in flight
+// (vmcnt counts this wave's outstanding vector-memory instructions, retired in order)
+template <int LPS, int K>
+GHOST_DEV void wait_stages(int after) {
+  if constexpr (K <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (after >= K) wait_vmcnt<K * LPS>();
+    else wait_stages<LPS, K - 1>(after);
+  }
+}
+
 // issue the LDS-DMA of K tile `kt` into ring slot `sb` (one 16-row piece per instruction)
 template <int BM, int NA, int NB>
 GHOST_DEV void glds_issue(const ConvArgs& a, const bf16* __restrict__ x, const bf16* const (&b_src)[NB],
@@ -417,12 +430,17 @@ __global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
   constexpr int NA = BM / 64, NB = BN / 64;        // DMA instructions per wave per stage (16 rows each)
   constexpr int LPS = NA + NB;
   constexpr int STAGE_B = (BM + BN) * 64;          // bytes per stage
-  static_assert(BM % 64 == 0 && BN % 64 == 0 && EPI != KEPI_AAD, "v2 tile");
+  static_assert(BM % 64 == 0 && BN % 64 == 0, "v2 tile");
+  static_assert(EPI != KEPI_AAD || (TN % 2 == 0 && WTN % 32 == 0), "AAD epilogue needs gamma/beta tile pairs");
+  static_assert((STAGES - 2) * LPS <= 63, "vmcnt range");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[STAGES * STAGE_B];
 
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
-  const int nt = tile % a.nNt, mt = tile / a.nNt;
+  // N-major order (deep ring): an XCD's run of tiles covers few channel tiles, whose weight rows
+  // then stay in that XCD's 4 MB L2 while every M tile streams past them
+  const int nMt = gridDim.x / a.nNt;
+  const int nt = a.nmajor ? tile / nMt : tile % a.nNt, mt = a.nmajor ? tile % nMt : tile / a.nNt;
   const int m0 = mt * BM, n0 = nt * BN;
   const int split = blockIdx.y, par = blockIdx.z, py = par >> 1, px = par & 1;
   const TI* __restrict__ x = reinterpret_cast<const TI*>(a.x);
@@ -485,14 +503,7 @@ __global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
   for (int it = 0; it < n; ++it) {
     // stages issued after `it` that may stay in flight
     const int after = min(STAGES - 2, n - 1 - it);
-    if constexpr (STAGES >= 4) {
-      if (after >= 2) wait_vmcnt<2 * LPS>();
-      else if (after == 1) wait_vmcnt<LPS>();
-      else wait_vmcnt<0>();
-    } else {
-      if (after >= 1) wait_vmcnt<LPS>();
-      else wait_vmcnt<0>();
-    }
+    wait_stages<LPS, STAGES - 2>(after);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (it + STAGES - 1 < n)
@@ -529,12 +540,23 @@ __global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
         float* dst = a.partial + (((long)par * a.nsplit + split) * a.M + m) * a.NT;
 #pragma unroll
         for (int j = 0; j < TN; ++j) dst[n0 + wn * WTN + j * 16 + lr] = acc[i][j][r];
-      } else {
+      } else if constexpr (EPI == KEPI_STD) {
         const long op = out_pixel(a, m, py, px);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int nn = n0 + wn * WTN + j * 16 + lr;
           if (nn < a.N) store_std<TO>(a, epi_std<TO>(a, acc[i][j][r], nn, op), nn, op);
+        }
+      } else {  // AAD: column tiles (2jp, 2jp+1) = (gamma, beta) of the same 16 channels
+#pragma unroll
+        for (int jp = 0; jp < TN / 2; ++jp) {
+          const int ng = n0 + wn * WTN + (2 * jp) * 16 + lr;
+          const int c = (ng >> 5) * 16 + lr;
+          if (c < a.C_aad) {
+            const float ga = acc[i][2 * jp][r] + a.shift[ng];
+            const float ba = acc[i][2 * jp + 1][r] + a.shift[ng + 16];
+            reinterpret_cast<TO*>(a.y)[(long)m * a.ldy + c] = from_f<TO>(epi_aad<TO>(a, ga, ba, c, m));
+          }
         }
       }
     }
@@ -550,6 +572,7 @@ struct Plan {
   int BM, BN, BK, nNt, nMt, npar, nsplit, kt_per_split, NT, M, Ho, Wo;
   bool fast;
   bool partial;   // GEMM writes fp32 partials, splitk_reduce_kernel applies the epilogue
+  int stages;     // > 0: the LDS-DMA ring kernel with this many stages (deep ring, low-resolution GEMMs)
 };
 
 
@@ -592,6 +615,19 @@ Plan make_plan(const ConvDesc& d) {
     p.BM = ((p.M + 127) / 128) * ((d.N + 127) / 128) * p.npar >= 512 ? 128 : 64;
   }
   if (!p.fast || p.BM >= 256) p.BK = force_bk == 64 && bk64_ok ? 64 : 32;
+  // Low-resolution GEMMs (the generator's 2x2..8x8 stages and the encoder's 16x16..2x2 convs at
+  // B = 64: M <= 8192 pixels, deep K): a register-staged tile keeps one K step in flight and waits
+  // out the memory latency on every step (measured 0.19 of MFMA peak on the 8x8 1024->1024 conv).
+  // The LDS-DMA ring keeps 6 K steps of 128x128 tiles in flight instead (128 KB of LDS, one
+  // workgroup per CU); split-K fills the CUs when the grid is small.
+  static const int deep = GHOST_KNOB("GHOST_CONV_DEEP", 8);
+  // (only grids that need split-K: with >= 256 tiles of 128 x 128 the two-workgroup register-staged
+  // kernel measured faster, e.g. the 8x8 AAD GEMM 55 vs 74 us)
+  const long tiles128 = (long)((p.M + 127) / 128) * ((d.N + 127) / 128) * p.npar;
+  if (deep > 0 && bf && p.fast && d.to == GHOST_BF16 && p.M <= 8192 && d.N >= 256 && d.Kpad >= 1024 &&
+      d.N % 128 == 0 && tiles128 < 256) {
+    p.BM = 128; p.BN = 128; p.BK = 32; p.stages = deep;
+  }
 #ifdef GHOST_TUNING
   static const char* force_tile = getenv("GHOST_CONV_TILE");   // tuning knob "BMxBN"
   if (force_tile && p.fast && d.epi != EPI_AAD) {
@@ -607,6 +643,13 @@ Plan make_plan(const ConvDesc& d) {
   int s = 1;
   if (d.force_split > 0) {
     s = d.force_split;
+  } else if (p.stages > 0) {
+    // deep ring: one resident workgroup per CU; split K until the grid covers the CUs
+    if (tiles < 256 && nk >= 16) {
+      s = (256 + tiles - 1) / tiles;
+      s = s < nk / 8 ? s : nk / 8;
+      if (s < 1) s = 1;
+    }
   } else if ((tiles < (d.min_wgs > 0 ? d.min_wgs : 256) && nk >= 16) ||
              (d.min_wgs <= 0 && tiles == 256 && nk >= 64)) {
     // one round of 256 tiles with a deep reduction splits in two as well (measured: the 4x4 deconv
@@ -646,6 +689,7 @@ ConvArgs make_args(const ConvDesc& d, const Plan& p, float* partial) {
   }
   a.nsplit = p.nsplit; a.kt_per_split = p.kt_per_split;
   a.slope = d.slope; a.tanh_out = d.tanh_out;
+  a.nmajor = p.stages > 0 ? GHOST_KNOB("GHOST_CONV_NMAJOR", 1) : 0;
   return a;
 }
 
@@ -693,13 +737,22 @@ int dispatch_tile(const ConvArgs& a, const Plan& p, hipStream_t s) {
 
 template <int EPI>
 bool launch_glds(const ConvArgs& a, const Plan& p, hipStream_t s) {
-  static const int stages = GHOST_KNOB("GHOST_CONV_STAGES", 3);
+  static const int stages_knob = GHOST_KNOB("GHOST_CONV_STAGES", 3);
+  const int stages = p.stages > 0 ? p.stages : stages_knob;
   dim3 grid(p.nMt * p.nNt, p.nsplit, p.npar);
+  if constexpr (EPI == KEPI_AAD) {
+    if (p.BM == 128 && p.BN == 128 && stages == 8) {
+      hipLaunchKernelGGL((conv_glds_kernel<128, 128, 8, EPI>), grid, dim3(256), 0, s, a);
+      return true;
+    }
+    return false;
+  }
 #define GHOST_G(bm, bn, st)                                                                      \
   if (p.BM == bm && p.BN == bn && stages == st) {                                                \
     hipLaunchKernelGGL((conv_glds_kernel<bm, bn, st, EPI>), grid, dim3(256), 0, s, a);           \
     return true;                                                                                  \
   }
+  GHOST_G(128, 128, 8) GHOST_G(128, 128, 6)
   GHOST_G(128, 128, 4) GHOST_G(256, 64, 4) GHOST_G(128, 64, 4) GHOST_G(64, 128, 4)
   GHOST_G(128, 128, 3) GHOST_G(256, 64, 3) GHOST_G(128, 64, 3) GHOST_G(64, 128, 3)
 #undef GHOST_G
@@ -723,13 +776,19 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
   static const int use_v2 = GHOST_KNOB("GHOST_CONV_V2", 1);
   if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
     // measured (tools/bench_ops.py): the DMA ring wins on the 128-row tiles, loses on 256x64
-    if (use_v2 && p.fast && p.BK == 32 && d.epi != EPI_AAD && p.BM <= 128 && p.partial == (p.nsplit > 1)) {
-      const bool ok = p.nsplit > 1 ? launch_glds<KEPI_SPLIT>(a, p, s) : launch_glds<KEPI_STD>(a, p, s);
+    if (use_v2 && p.fast && p.BK == 32 && (d.epi != EPI_AAD || p.stages > 0) && p.BM <= 128 &&
+        p.partial == (p.nsplit > 1)) {
+      const bool ok = p.nsplit > 1 ? launch_glds<KEPI_SPLIT>(a, p, s)
+                                   : (d.epi == EPI_AAD ? launch_glds<KEPI_AAD>(a, p, s) : launch_glds<KEPI_STD>(a, p, s));
       if (ok) {
         if (p.nsplit > 1) {
-          const long total = (long)p.M * d.N;
+          const int ncols = d.epi == EPI_AAD ? d.C_aad : d.N;
+          const long total = (long)p.M * ncols;
           dim3 grid((unsigned)((total + 255) / 256), 1, p.npar);
-          hipLaunchKernelGGL((splitk_reduce_kernel<TO, KEPI_STD>), grid, dim3(256), 0, s, a);
+          if (d.epi == EPI_AAD)
+            hipLaunchKernelGGL((splitk_reduce_kernel<TO, KEPI_AAD>), grid, dim3(256), 0, s, a);
+          else
+            hipLaunchKernelGGL((splitk_reduce_kernel<TO, KEPI_STD>), grid, dim3(256), 0, s, a);
         }
         return 0;
       }
