@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--cpu-batches", default="1,64", help="CPU baseline batch sizes ('' = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--arc-batch", type=int, default=64, help="faces per ArcFace embedding batch in its leg")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="AEI_Net plan option name=value (A/B runs), e.g. --opt fuse_stats=0")
     return ap.parse_args()
 
 
@@ -342,6 +344,9 @@ def main():
 
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     G = make_model(a.backbone, a.num_blocks, dt, dev)
+    for kv in a.opt:
+        name, val = kv.split("=")
+        G.set_option(name, int(val))
 
     B = a.batch
     rng = np.random.Generator(np.random.PCG64(1000 + rank))

@@ -10,8 +10,6 @@ struct AadV3Desc {
   // up_H > 0: h_in = upsample2x(hin) (bilinear x2, align_corners) with hin the [B, up_H, up_W]
   // source, sampled on the fly (values rounded to bf16 as upsample2x stores them)
   int up_H = 0, up_W = 0;
-  // zup_H > 0: z_attr = upsample2x(za) with za the [B, zup_H, zup_W, Ca] source (C = 64 only)
-  int zup_H = 0, zup_W = 0;
   const float* stat = nullptr;                       // [B][C][2] mean, rstd of h_in
   int B = 0, HW = 0, C = 0, L = 1, id_ld = 0;
   float slope = 0.f;

@@ -38,12 +38,11 @@ struct AadV3Args {
   int lda, ldh, id_ld, HW, PPW;
   float slope;
   Up2xSrc up;   // UP: h_in is the bilinear x2 upsample of hin (a [B, up.H, up.W] source)
-  Up2xSrc upz;  // UPZ: z_attr is the bilinear x2 upsample of za (a [B, upz.H, upz.W] source)
 };
 
 static constexpr int kWaves = 8;
 
-template <int C, int CA, int L, bool UP, bool UPZ = false, int NWV = kWaves>
+template <int C, int CA, int L, bool UP, int NWV = kWaves>
 GHOST_DEV void aad_v3_body(const AadV3Args& a) {
   constexpr int CT = C / 64;          // 64-channel tiles
   constexpr int KS = CA / 32;         // MFMA k-steps
@@ -106,27 +105,8 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
     asm volatile("" ::: "memory");
     const long p = p_begin + t * 16 + lr;
     u32x4 zc[KS], hc[NH];
-    if constexpr (UPZ) {
-      // z_attr through the x2 upsample (the unet z_attr8 = upsample(z_attr7), AEI_Net.py:94):
-      // the same interpolation and bf16 rounding as the upsample kernel that no longer runs
-      const int r = (int)(p - (long)b * a.HW);
-      const int oy = r / (2 * a.upz.W), ox = r - oy * (2 * a.upz.W);
-      const Up2xTap tz = up2x_tap(a.upz, oy, ox);
-      const bf16* zs = a.za + (long)b * a.upz.H * a.upz.W * a.lda;
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        float v[8];
-        up2x_load16_f(zs + ks * 32 + lq * 8, a.lda, tz, v);
-        bf16* zv = reinterpret_cast<bf16*>(&zc[ks]);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) zv[e] = (bf16)v[e];
-      }
-      // with h_in through the upsample too: its 4 x NH loads after z's (one raw set live at a time)
-      if constexpr (UP) asm volatile("" ::: "memory");
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + ks * 32 + lq * 8);
-    }
+    for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + ks * 32 + lq * 8);
     if constexpr (UP) {
       // the tile's 16 pixels lie on one output row; each chunk is interpolated from the four
       // source pixels (L1/L2 hits: a source pixel feeds ~4 outputs) and rounded to bf16
@@ -224,16 +204,6 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
 template <int C, int CA, int L, bool UP>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v3_kernel(const AadV3Args a) {
   aad_v3_body<C, CA, L, UP>(a);
-}
-// z_attr through the upsample: 8 waves held to 128 VGPRs (two workgroups per CU), or 4 waves with
-// the compiler's allocation (three workgroups per CU at <= 168 VGPRs) where the cap spills
-template <int C, int CA, int L, bool UP>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v3z_kernel(const AadV3Args a) {
-  aad_v3_body<C, CA, L, UP, true>(a);
-}
-template <int C, int CA, int L, bool UP>
-__global__ void __launch_bounds__(256) aad_v3z4_kernel(const AadV3Args a) {
-  aad_v3_body<C, CA, L, UP, true, 4>(a);
 }
 template <int C, int CA, int L, bool UP>
 __global__ void __launch_bounds__(512) aad_v3_wide_kernel(const AadV3Args a) {
@@ -512,29 +482,7 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
     if (4 * d.up_H * d.up_W != d.HW || d.up_W * 2 < 16 || (d.C != 64 && d.C != 128)) return -1;
     a.up = up2x_src(d.up_H, d.up_W);
   }
-  const bool upz = d.zup_H > 0;
-  if (upz) {
-    if (4 * d.zup_H * d.zup_W != d.HW || d.C != 64) return -1;
-    a.upz = up2x_src(d.zup_H, d.zup_W);
-  }
   dim3 grid((unsigned)((long)d.B * d.HW / a.PPW));
-  if (upz) {
-    static const int z4 = GHOST_KNOB("GHOST_AAD_Z4", 2);
-    // by shape: 4 waves where the 128-VGPR cap spills (h_in through the upsample as well)
-    const bool four = z4 == 1 || (z4 == 2 && up);
-#define GHOST_V3Z(ca, l, u)                                                                          \
-    if (d.Ca == ca && d.L == l && up == u) {                                                         \
-      if (four)                                                                                      \
-        hipLaunchKernelGGL((aad_v3z4_kernel<64, ca, l, u>), grid, dim3(256), 0, s, a);              \
-      else                                                                                           \
-        hipLaunchKernelGGL((aad_v3z_kernel<64, ca, l, u>), grid, dim3(512), 0, s, a);               \
-      return (int)hipGetLastError();                                                                 \
-    }
-    GHOST_V3Z(64, 1, false) GHOST_V3Z(64, 2, true) GHOST_V3Z(32, 1, false) GHOST_V3Z(32, 2, true)
-    GHOST_V3Z(64, 2, false) GHOST_V3Z(64, 1, true) GHOST_V3Z(32, 2, false) GHOST_V3Z(32, 1, true)
-#undef GHOST_V3Z
-    return -1;
-  }
   static const int use_v4 = GHOST_KNOB("GHOST_AAD_V4", 1);
   // v4 (prefetching) only for the through-upsample form: measured B = 64, 256x256 L = 2: 724 vs 734 us
   // with the upsample, 604 vs 550 us without it (there v3's register loads win)

@@ -69,7 +69,7 @@ struct ghost_aei {
   std::map<std::string, const void*> slots;   // name -> device pointer (nullptr = unbound)
   int id_total = 0;                            // sum over AAD layers of 2*c_x
   // per-handle plan options (ghost_aei_set_option); defaults are the measured choices
-  int opt[GHOST_AEI_NOPT] = {1, 1, 0};
+  int opt[GHOST_AEI_NOPT] = {1, 1};
   void* taps[8] = {nullptr};                   // ghost_aei_set_taps: AADBlk1..7 outputs copied here
   // profiling
   int prof_mask = 0;
@@ -295,8 +295,7 @@ void encoder_resnet(Ctx& c, const void* xin, int B, void* const attr[8]) {
   }
 }
 
-// z8_virtual: z_attr8 = upsample2x(z_attr7) is not written; its readers sample it (AEI_Net.py:94)
-void encoder(Ctx& c, const void* xin, int B, void* const attr[8], bool z8_virtual = false) {
+void encoder(Ctx& c, const void* xin, int B, void* const attr[8]) {
   ghost_aei* h = c.h;
   if (h->resnet) {
     encoder_resnet(c, xin, B, attr);
@@ -360,7 +359,7 @@ void encoder(Ctx& c, const void* xin, int B, void* const attr[8], bool z8_virtua
   int C7, H7, C8, H8;
   h->attr_geom(7, C7, H7);
   h->attr_geom(8, C8, H8);
-  if (!z8_virtual) run_up(c, attr[6], C7, attr[7], C8, B, H7, H7, C7);
+  run_up(c, attr[6], C7, attr[7], C8, B, H7, H7, C7);   // z_attr8 = F.interpolate(z_attr7) (AEI_Net.py:94)
 }
 
 // ---------------------------------------------------------------------------
@@ -420,13 +419,12 @@ struct AadOut {
 // AADLayers that read the same h_in / z_attr: the register-epilogue kernel takes up to two at
 // once (one pass over the inputs); other shapes run one fused / split AAD kernel per layer
 // up_src: h_in is upsample2x of the [B, n/2, n/2] tensor hin (the through-upsample AAD kernel)
-// z_up: za is the [B, n/2, n/2, Ca] source of z_attr = upsample2x(za)
 void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, const float* stat, const void* za,
-               int lda, int Ca, int B, int n, int C, const float* idgb, bool up_src = false, bool z_up = false) {
+               int lda, int Ca, int B, int n, int C, const float* idgb, bool up_src = false) {
   ghost_aei* h = c.h;
   bool v3 = aad_v3_supported(h->dt, B, n * n, C, Ca, lda, ldh, 8);
   for (auto& l : ls) v3 = v3 && l.ldo % 8 == 0;
-  if ((up_src || z_up) && !v3) {
+  if (up_src && !v3) {
     c.check(GHOST_EINVAL, "aad_group: through-upsample input needs the v3 kernel");
     return;
   }
@@ -482,7 +480,6 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     d.B = B; d.HW = n * n; d.C = C; d.id_ld = h->id_total; d.slope = 0.0f;   // + the ReLU that follows
     d.L = (int)std::min(lmax, ls.size() - i0);
     if (up_src) d.up_H = d.up_W = n / 2;
-    if (z_up) d.zup_H = d.zup_W = n / 2;
     for (int l = 0; l < d.L; ++l) {
       const AadOut& o = ls[i0 + l];
       d.w3[l] = c.W(o.name + ".w3");
@@ -500,7 +497,7 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     const double bytes = Pn * (double)d.L * (2.0 * C + Ca) * h->esz;
     const double flops = 2.0 * Pn * 2.0 * C * Ca * d.L;
     if (g_trace)
-      fprintf(stderr, "[plan] aad_v3 %dx%d C=%d Ca=%d L=%d up=%d zup=%d\n", n, n, C, Ca, d.L, (int)up_src, (int)z_up);
+      fprintf(stderr, "[plan] aad_v3 %dx%d C=%d Ca=%d L=%d up=%d\n", n, n, C, Ca, d.L, (int)up_src);
     int e_all = c.prof_begin(0);
     // class 1: the block-input AAD kernel at 256x256 (reads h_in through the x2 upsample; one or two layers)
     int e_big = (n == 256 && up_src) ? c.prof_begin(1) : -1;
@@ -546,8 +543,7 @@ bool conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, 
   return fused;
 }
 
-void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, void* y_out, uint8_t* u8,
-               bool z8_virtual = false) {
+void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, void* y_out, uint8_t* u8) {
   ghost_aei* h = c.h;
   const int es = h->esz;
   const int nb = h->nb;
@@ -582,8 +578,7 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     const int cin = h->gen()[k - 1][0], cout = h->gen()[k - 1][1];
     int Ca, n;
     h->attr_geom(k, Ca, n);
-    const bool zv = k == 8 && z8_virtual;    // z_attr8 sampled through the upsample of z_attr7
-    const void* za = zv ? attr[6] : attr[k - 1];
+    const void* za = attr[k - 1];
     const std::string blk = "gen.blk" + std::to_string(k);
     const size_t P = (size_t)B * n * n;
     const bool last_k = k == 8;
@@ -610,7 +605,7 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
       group.push_back({blk + ".aad" + std::to_string(i), base + 2 * cin * i, a, lda_out});
       if (i == 0 && split)   // last_add_block's AADLayer reads the block input m as well
         group.push_back({blk + ".aadlast", base + 2 * cin * nb, (char*)cat + (size_t)cin * es, 2 * cin});
-      aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb, i == 0 && m_virtual, zv);
+      aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb, i == 0 && m_virtual);
       if (!last) {
         void* xn = c.alloc(P * cin * es);
         float* st = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
@@ -727,21 +722,9 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
   ghost_aei* h = c.h;
   const int es = h->esz;
   void* attr[8];
-  // swaps never hand z_attr8 out: AADBlk8's AADLayers sample upsample2x(z_attr7) instead of reading it
-  // (unet / linknet, where z_attr8 is that upsample; C = 64 register-epilogue kernels only)
-  bool z8v = false;
-  {
-    int C7, H7, C8, H8;
-    h->attr_geom(7, C7, H7);
-    h->attr_geom(8, C8, H8);
-    const int cin8 = h->gen()[7][0];
-    z8v = mode == M_SWAP && h->opt[GHOST_AEI_OPT_FUSE_ZUP] && !h->resnet && C7 == C8 && H8 == 2 * H7 && cin8 == 64 &&
-          h->dt == GHOST_BF16 && aad_v3_supported(h->dt, B, H8 * H8, cin8, C8, C8, cin8, 8);
-  }
   for (int k = 1; k <= 8; ++k) {
     int C, H;
     h->attr_geom(k, C, H);
-    if (k == 8 && z8v) { attr[k - 1] = nullptr; continue; }
     attr[k - 1] = (mode == M_SWAP) ? c.alloc((size_t)B * H * H * C * es) : io.attr[k - 1];
   }
   // network input NHWC with a zero fourth channel: 8-byte (bf16) pixels for the first conv
@@ -752,12 +735,12 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
     else
       c.check(input_to_nhwc(io.xt_dtype, io.xt, io.st, B, 3, 256, 256, h->dt, xin, c.s, 4), "input_to_nhwc");
   }
-  encoder(c, xin, B, attr, z8v);
+  encoder(c, xin, B, attr);
   if (mode == M_ATTR) return;
   float* zid32 = (float*)c.alloc((size_t)B * h->c_id * sizeof(float));
   if (!c.dry && c.ok()) c.check(rows_to_f32(io.zid_dtype, io.zid, io.zid_rs, B, h->c_id, zid32, c.s), "rows_to_f32");
   void* y = (mode == M_SWAP) ? c.alloc((size_t)B * 256 * 256 * 3 * es) : io.y;
-  generator(c, B, attr, zid32, y, io.u8, z8v);
+  generator(c, B, attr, zid32, y, io.u8);
 }
 
 int64_t plan_bytes(ghost_aei* h, Mode mode, int B) {
@@ -1118,16 +1101,12 @@ extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, con
   hipStream_t s = (hipStream_t)stream;
   const int HW = H * W;
   if (L < 1 || L > 2) return fail(GHOST_EINVAL, "aad_v3: L must be 1 or 2");
-  if (up2x & ~3) return fail(GHOST_EINVAL, "aad_v3: up2x is a mask of 1 (h_in) and 2 (z_attr)");
-  const bool zup = (up2x & 2) != 0;
-  up2x &= 1;
+  if (up2x & ~1) return fail(GHOST_EINVAL, "aad_v3: up2x must be 0 or 1");
   if (up2x && (H % 2 || W % 2 || (C != 64 && C != 128)))
     return fail(GHOST_EINVAL, "aad_v3: up2x needs even H, W and C in {64, 128}");
-  if (zup && (H % 2 || W % 2 || C != 64))
-    return fail(GHOST_EINVAL, "aad_v3: z_attr through the upsample needs even H, W and C = 64");
   // aad_wide: one layer, C in {256, 512, 1024}, Ca <= 512, where the all-channel kernel does not fit
   const bool wide = C >= 256 && !aad_v3_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[0]);
-  if (wide && (L != 1 || up2x || zup || !aad_wide_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[0])))
+  if (wide && (L != 1 || up2x || !aad_wide_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[0])))
     return fail(GHOST_EINVAL, "aad_wide: unsupported shape (one layer, C in {256,512,1024}, Ca <= 512)");
   for (int l = 0; l < L && !wide; ++l)
     if (!aad_v3_supported(GHOST_BF16, B, HW, C, Ca, lda, ldh, ldo[l]))
@@ -1160,10 +1139,6 @@ extern "C" int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, con
   if (up2x) {
     d.up_H = H / 2;
     d.up_W = W / 2;
-  }
-  if (zup) {
-    d.zup_H = H / 2;
-    d.zup_W = W / 2;
   }
   for (int l = 0; l < L; ++l) {
     d.w3[l] = w3[l]; d.b3[l] = b3[l]; d.wh[l] = wh[l]; d.bh[l] = bh[l]; d.idgb[l] = idgb[l];

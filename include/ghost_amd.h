@@ -82,10 +82,8 @@ int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_str
  *                                    instead of reading a materialised upsample (0 materialises it)
  *   GHOST_AEI_OPT_FUSE_STATS (1):    the persistent 3x3 conv emits the InstanceNorm partials of its output
  *                                    (0: a separate statistics pass)
- *   GHOST_AEI_OPT_FUSE_ZUP (0):      swaps sample z_attr8 = upsample2x(z_attr7) inside AADBlk8's AADLayers
- *                                    instead of materialising it (unet / linknet, bf16)
  * value is 0 or 1.  A handle is not shared across threads without external synchronisation. */
-enum { GHOST_AEI_OPT_FUSE_UPSAMPLE = 0, GHOST_AEI_OPT_FUSE_STATS = 1, GHOST_AEI_OPT_FUSE_ZUP = 2, GHOST_AEI_NOPT = 3 };
+enum { GHOST_AEI_OPT_FUSE_UPSAMPLE = 0, GHOST_AEI_OPT_FUSE_STATS = 1, GHOST_AEI_NOPT = 2 };
 int ghost_aei_set_option(ghost_aei* h, int option, int value);
 int ghost_aei_get_option(ghost_aei* h, int option, int* value);
 /* Diagnostic taps (parity bisection): while set, every forward / swap of the handle copies the stored
@@ -167,9 +165,8 @@ int ghost_aad_layer_nhwc(int dtype, const void* h_in, int ldh, const void* z_att
  * w3/b3 per layer in the permuted layout of pack.py pack_aad_v3; InstanceNorm statistics of h_in
  * are computed into the workspace first.  up2x = 1: h_in is upsample2x of the [B, H/2, W/2, C]
  * tensor passed as h_in (F.interpolate of AEI_Net.py:135-137 fused into the AADLayer read; C in {64, 128}).
- * up2x bit 2 (value 2): z_attr is upsample2x of the [B, H/2, W/2, Ca] tensor passed as z_attr (the unet
- * z_attr8 = F.interpolate(z_attr7), AEI_Net.py:94; C = 64).
- * C in {256, 512, 1024} (L = 1, Ca <= 512) runs the per-channel-tile kernel of aad_wide.hip. */
+ * C = 256 (L = 1, Ca in {64, 128}) keeps all channels in one workgroup; C in {256, 512, 1024} otherwise
+ * (L = 1, Ca <= 512) runs the per-channel-tile kernel of aad_wide.hip. */
 int ghost_aad_layers_v3_nhwc(const void* h_in, int ldh, int up2x, const void* z_attr, int lda, int B, int H, int W,
                              int C, int Ca, int L, const void* const w3[], const float* const b3[],
                              const float* const wh[], const float* const bh[], const float* const idgb[], int id_ld,
