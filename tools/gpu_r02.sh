@@ -8,6 +8,7 @@ for w in "$@"; do
     bisect) timeout -k 10 300 python tools/bf16_bisect.py --backbone unet --num-blocks 2 --fp16 --json gpurun_out/bisect_unet2.json > gpurun_out/bisect_unet2.log 2>&1
             timeout -k 10 300 python tools/bf16_bisect.py --backbone linknet --num-blocks 3 --fp16 --json gpurun_out/bisect_linknet3.json > gpurun_out/bisect_linknet3.log 2>&1 ;;
     bench) timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 ;;
+    arc) timeout -k 10 300 python bench.py --legs arcface --cpu-batches "" --steps 10 > gpurun_out/bench_arc.log 2>&1 ;;
     quick) timeout -k 10 200 python bench.py --legs "" --cpu-batches "" > gpurun_out/bench_quick.log 2>&1 ;;
     trace) export TMPDIR=/tmp; R=/tmp/ghost_trace; rm -rf $R; mkdir -p $R
            timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R -o run -- python3 bench.py --steps 5 --warmup 2 --legs "" --cpu-batches "" > gpurun_out/trace_bench.log 2>&1
