@@ -153,6 +153,139 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 8))
   aad_wide_body<C, CA>(a);
 }
 
+// ---------------------------------------------------------------------------------------------
+// aad_gemm: the same layer as a 256 x 256 MFMA tile GEMM (the 16x16 stage: C % 128 == 0, Ca = 512).
+//
+// aad_wide re-reads the z_attr row for every 64-channel tile (C / 64 times: 16x at C = 1024) and keeps
+// one 16-pixel tile per wave, so it runs on the L2 -> CU path (measured 78-83 us for a 16x16 layer
+// whose HBM and MFMA floors are ~14 us each).  Here a workgroup owns 256 weight rows (two 64-channel
+// tiles of the permuted pack_aad_v3 layout) x 256 pixels of one sample, K = Ca streamed in 64-deep
+// stages by LDS-DMA into two buffers (128 B rows, chunk c of row r at c ^ ((r >> 1) & 7): conflict-
+// free 16-row fragment reads).  4 waves, each 128 rows x 128 pixels (64 accumulator tiles): the
+// operands of 64 MFMAs cost 16 fragment reads.  The epilogue is aad_v3's register blend (a lane holds
+// gamma / beta of 8 channels of one pixel) with the mask of the aad_mask pass.
+// ---------------------------------------------------------------------------------------------
+GHOST_DEV int gswz(int r) { return (r >> 1) & 7; }
+
+template <int CA>
+__global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int C) {
+  constexpr int NST = CA / 64;                 // K stages
+  static_assert(NST % 2 == 0, "stages are ping-ponged in pairs");
+  constexpr int STAGE_B = 512 * 128;           // 256 weight rows + 256 pixel rows, 128 B each
+  __shared__ __attribute__((aligned(1024))) unsigned char lds0[STAGE_B];
+  __shared__ __attribute__((aligned(1024))) unsigned char lds1[STAGE_B];
+  __shared__ __attribute__((aligned(16))) float s_b[256];
+  __shared__ __attribute__((aligned(16))) float s_rs[128], s_nm[128], s_gi[128], s_bi[128];
+
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int ncp = C / 128;
+  const int tile = wide_xcd_tile(blockIdx.x, gridDim.x);
+  const int cp = tile % ncp, pb = tile / ncp;
+  const long p0 = (long)pb * 256;
+  const int b = (int)(p0 / a.HW);              // HW % 256 == 0: one sample per tile
+  const int c0 = cp * 128;                     // first channel; weight rows cp*256 .. +256
+  const bf16* wsrc = a.w3 + (long)cp * 256 * CA;
+  const bf16* zsrc = a.za + p0 * a.lda;
+
+  // DMA: 64 pieces of 8 rows x 128 B per stage (32 weight + 32 pixel), 16 per wave
+  const int prow = lane >> 3, pch = lane & 7;
+  auto issue = [&](unsigned char* buf, int st) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int k0 = st * 64;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int q = wid + 4 * j;               // piece 0..63: < 32 weights, >= 32 pixels
+      const int row = (q & 31) * 8 + prow;
+      const int lc = pch ^ gswz(row);          // logical chunk this lane's physical slot holds
+      const bf16* src = q < 32 ? wsrc + (long)row * CA + k0 + lc * 8 : zsrc + (long)row * a.lda + k0 + lc * 8;
+      __builtin_amdgcn_global_load_lds(src, buf + q * 1024, 16, 0, 0);
+    }
+#endif
+  };
+  issue(lds0, 0);
+
+  for (int i = tid; i < 256; i += 256) s_b[i] = a.b3[cp * 256 + i];
+  if (tid < 128) {
+    const int c = c0 + tid;
+    const float mu = a.stat[((long)b * C + c) * 2], rs = a.stat[((long)b * C + c) * 2 + 1];
+    s_rs[tid] = rs;
+    s_nm[tid] = -mu * rs;
+    s_gi[tid] = a.idgb[(long)b * a.id_ld + c];
+    s_bi[tid] = a.idgb[(long)b * a.id_ld + C + c];
+  }
+
+  const int wr = wid & 1, wp = wid >> 1;       // rows wr*128.. (channel tile), pixels wp*128..
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int rt = 0; rt < 8; ++rt)
+#pragma unroll
+    for (int pf = 0; pf < 8; ++pf) acc[rt][pf] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](const unsigned char* buf) {
+    const unsigned char* Wb = buf;
+    const unsigned char* Zb = buf + 256 * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[8], bfr[8];
+#pragma unroll
+      for (int rt = 0; rt < 8; ++rt) {
+        const int row = wr * 128 + rt * 16 + lr;
+        af[rt] = *reinterpret_cast<const bf16x8*>(Wb + row * 128 + (((ks * 4 + lq) ^ gswz(row)) * 16));
+      }
+#pragma unroll
+      for (int pf = 0; pf < 8; ++pf) {
+        const int row = wp * 128 + pf * 16 + lr;
+        bfr[pf] = *reinterpret_cast<const bf16x8*>(Zb + row * 128 + (((ks * 4 + lq) ^ gswz(row)) * 16));
+      }
+#pragma unroll
+      for (int rt = 0; rt < 8; ++rt)
+#pragma unroll
+        for (int pf = 0; pf < 8; ++pf)
+          acc[rt][pf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rt], bfr[pf], acc[rt][pf], 0, 0, 0);
+    }
+  };
+  // stage pairs: even stages read lds0 and prefetch into lds1, odd ones the reverse (distinct LDS
+  // objects, static waits: the compiler does not drain the in-flight DMA before the fragment reads)
+  for (int st = 0; st < NST; st += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    issue(lds1, st + 1);
+    compute(lds0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (st + 2 < NST) issue(lds0, st + 2);
+    compute(lds1);
+  }
+
+  // epilogue (aad_v3's register blend): lane holds, per pixel fragment pf and half sh, gamma / beta of
+  // channels wr*64 + 32sh + 8lq + e (e < 8) of pixel wp*128 + 16pf + lr
+#pragma unroll
+  for (int pf = 0; pf < 8; ++pf) {
+    const long p = p0 + wp * 128 + pf * 16 + lr;
+    const float Mk = a.mask[p];
+#pragma unroll
+    for (int sh = 0; sh < 2; ++sh) {
+      const int cl = wr * 64 + sh * 32 + lq * 8;           // channel within the 128 of the tile
+      float hv[8];
+      load16_f(a.hin + p * a.ldh + c0 + cl, hv);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i0 = e >> 2, r = e & 3;
+        const int rg = (i0 & 1) + 2 * sh, rb = rg + 4;       // gamma / beta row tiles
+        const float g = acc[rg][pf][r] + s_b[wr * 128 + rg * 16 + lq * 4 + r];
+        const float be = acc[rb][pf][r] + s_b[wr * 128 + rb * 16 + lq * 4 + r];
+        const float hh = fmaf(hv[e], s_rs[cl + e], s_nm[cl + e]);
+        const float A = fmaf(g, hh, be);
+        const float I = fmaf(s_gi[cl + e], hh, s_bi[cl + e]);
+        const float v = fmaf(Mk, I - A, A);
+        o[e] = v > 0.f ? v : v * a.slope;
+      }
+      store16_f(a.out + p * a.ldo + c0 + cl, o);
+    }
+  }
+}
+
 namespace {
 int wide_ppw(int B, int HW, int C, int Ca) {
   // as many pixels per workgroup as keep a full round of workgroups (two per CU; one for the
@@ -176,12 +309,26 @@ bool aad_wide_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, 
   return ppw > 0 && (long)B * HW / ppw * (C / 64) >= 256;
 }
 
+static bool aad_gemm_ok(const AadWideDesc& d) {
+  static const int on = GHOST_KNOB("GHOST_AAD_GEMM", 1);
+  // Ca = 512 only: at Ca = 256 (the 32x32 stage) four K stages do not amortise the tile's prologue and
+  // epilogue at one workgroup per CU (measured 80-86 us against aad_wide's 52-57 us; Ca = 512: 62-66
+  // against 78-83 us)
+  return on && d.HW % 256 == 0 && d.C % 128 == 0 && d.Ca == 512 && d.lda % 8 == 0 &&
+         d.ldh % 8 == 0 && d.ldo % 8 == 0 && (uintptr_t)d.za % 16 == 0 && (uintptr_t)d.w3 % 16 == 0;
+}
+
 int aad_wide(const AadWideDesc& d, hipStream_t s) {
   if (!aad_wide_supported(GHOST_BF16, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo) || !d.mask) return -1;
   AadWideArgs a{};
   a.za = (const bf16*)d.za; a.hin = (const bf16*)d.hin; a.stat = d.stat;
   a.w3 = (const bf16*)d.w3; a.b3 = d.b3; a.wh = d.wh; a.bh = d.bh; a.idgb = d.idgb; a.mask = d.mask; a.out = (bf16*)d.out;
   a.lda = d.lda; a.ldh = d.ldh; a.ldo = d.ldo; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
+  if (aad_gemm_ok(d)) {
+    dim3 g((unsigned)((long)d.B * d.HW / 256 * (d.C / 128)));
+    hipLaunchKernelGGL(aad_gemm_kernel<512>, g, dim3(256), 0, s, a, d.C);
+    return (int)hipGetLastError();
+  }
   a.PPW = wide_ppw(d.B, d.HW, d.C, d.Ca);
   a.nblk = (int)((long)d.B * d.HW / a.PPW);
   dim3 grid((unsigned)(a.nblk * (d.C / 64)));

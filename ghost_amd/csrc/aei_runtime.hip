@@ -223,6 +223,22 @@ void run_mask(Ctx& c, const void* x, int ldx, int B, int HW, int C, const float*
   c.prof_end(4, e, (double)B * HW * C * c.h->esz, 0);
 }
 
+// small images (2x2 .. 8x8): statistics + the masks of the AADLayers named in `ls` (<= 2) in one launch
+void run_stats_masks(Ctx& c, const void* x, int ldx, int B, int HW, int C, float* stat, const std::string* ls, int L,
+                     float* masks[2]) {
+  const float* wh[2] = {nullptr, nullptr};
+  const float* bh[2] = {nullptr, nullptr};
+  for (int l = 0; l < L; ++l) {
+    wh[l] = (const float*)c.W(ls[l] + ".wh");
+    bh[l] = (const float*)c.W(ls[l] + ".bh");
+  }
+  if (!c.ok() || c.dry) return;
+  int e = c.prof_begin(4);
+  c.check(stats_mask_small(c.h->dt, x, ldx, B, HW, C, stat, wh[0], bh[0], masks[0], wh[1], bh[1], masks[1], c.s),
+          "stats_mask_small");
+  c.prof_end(4, e, (double)B * HW * C * c.h->esz, 0);
+}
+
 void run_up(Ctx& c, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C) {
   if (!c.ok() || c.dry) return;
   int e = c.prof_begin(6);
@@ -372,7 +388,8 @@ struct GenShared {
 
 // one AADLayer (+ fused ReLU) -> out
 void aad(Ctx& c, const std::string& name, const void* hin, int ldh, const float* stat, const void* za, int lda,
-         int Ca, int B, int n, int C, int id_off, const float* idgb, void* out, int ldo) {
+         int Ca, int B, int n, int C, int id_off, const float* idgb, void* out, int ldo,
+         const float* pre_mask = nullptr) {
   ghost_aei* h = c.h;
   const double P = (double)B * n * n;
   const double bytes = P * (2.0 * C + Ca) * (double)h->esz;   // |h_in| + |z_attr| + |out|
@@ -392,8 +409,12 @@ void aad(Ctx& c, const std::string& name, const void* hin, int ldh, const float*
     if (e_all >= 0) c.prof_end(0, e_all, bytes, flops);
     return;
   }
-  float* mask = (float*)c.alloc((size_t)B * n * n * sizeof(float));
-  run_mask(c, hin, ldh, B, n * n, C, stat, wh, bh, mask);
+  const float* mask = pre_mask;
+  if (!mask) {
+    float* m = (float*)c.alloc((size_t)B * n * n * sizeof(float));
+    run_mask(c, hin, ldh, B, n * n, C, stat, wh, bh, m);
+    mask = m;
+  }
   ConvDesc d;
   d.ti = d.to = h->dt;
   d.x = za; d.B = B; d.Hi = n; d.Wi = n; d.Cin = Ca; d.ldx = lda;
@@ -419,8 +440,10 @@ struct AadOut {
 // AADLayers that read the same h_in / z_attr: the register-epilogue kernel takes up to two at
 // once (one pass over the inputs); other shapes run one fused / split AAD kernel per layer
 // up_src: h_in is upsample2x of the [B, n/2, n/2] tensor hin (the through-upsample AAD kernel)
+// pre_masks: the layers' masks when the statistics pass produced them (run_stats_masks)
 void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, const float* stat, const void* za,
-               int lda, int Ca, int B, int n, int C, const float* idgb, bool up_src = false) {
+               int lda, int Ca, int B, int n, int C, const float* idgb, bool up_src = false,
+               float* const* pre_masks = nullptr) {
   ghost_aei* h = c.h;
   bool v3 = aad_v3_supported(h->dt, B, n * n, C, Ca, lda, ldh, 8);
   for (auto& l : ls) v3 = v3 && l.ldo % 8 == 0;
@@ -433,7 +456,10 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     for (auto& l : ls) wide = wide && l.ldo % 8 == 0;
     // the masks of every layer of the group from one pass over h_in
     float* masks[2] = {nullptr, nullptr};
-    if (wide) {
+    if (wide && pre_masks) {
+      masks[0] = pre_masks[0];
+      masks[1] = pre_masks[1];
+    } else if (wide) {
       for (size_t i = 0; i < ls.size(); ++i) masks[i] = (float*)c.alloc((size_t)B * n * n * sizeof(float));
       const float* wh0 = (const float*)c.W(ls[0].name + ".wh");
       const float* bh0 = (const float*)c.W(ls[0].name + ".bh");
@@ -449,7 +475,8 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     for (size_t li = 0; li < ls.size(); ++li) {
       const AadOut& l = ls[li];
       if (!wide) {
-        aad(c, l.name, hin, ldh, stat, za, lda, Ca, B, n, C, l.id_off, idgb, l.out, l.ldo);
+        aad(c, l.name, hin, ldh, stat, za, lda, Ca, B, n, C, l.id_off, idgb, l.out, l.ldo,
+            pre_masks ? pre_masks[li] : nullptr);
         continue;
       }
       AadWideDesc d;
@@ -585,7 +612,19 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     const bool split = cin != cout;          // AAD_ResBlk has a last_add_block (AADLayer.py:68-72)
     const int base = id_off;                  // idgb offset of this block's first AADLayer
     float* stat_m = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
-    if (m_virtual)
+    // 2x2 and 4x4: statistics and the AAD masks of each layer group from one launch per group
+    const bool small = !m_virtual && h->opt[GHOST_AEI_OPT_FUSE_STATS] && stats_mask_small_ok(h->dt, n * n, cin, cin);
+    float* gmask[2] = {nullptr, nullptr};
+    auto small_masks = [&](const void* xin, float* st, int i) {
+      std::string ln[2] = {blk + ".aad" + std::to_string(i), blk + ".aadlast"};
+      const int L = (i == 0 && split) ? 2 : 1;
+      for (int l = 0; l < L; ++l) gmask[l] = (float*)c.alloc((size_t)B * n * n * sizeof(float));
+      gmask[1] = L > 1 ? gmask[1] : nullptr;
+      run_stats_masks(c, xin, cin, B, n * n, cin, st, ln, L, gmask);
+    };
+    if (small)
+      small_masks(m, stat_m, 0);
+    else if (m_virtual)
       run_stats_up(c, m, cin, B, n / 2, n / 2, cin, stat_m);
     else if (m_src && in_stats_up2x_closed_form(h->dt, n / 2, n / 2, cin, cin))
       run_stats_up(c, m_src, cin, B, n / 2, n / 2, cin, stat_m);   // one pass over the 4x smaller source
@@ -605,14 +644,18 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
       group.push_back({blk + ".aad" + std::to_string(i), base + 2 * cin * i, a, lda_out});
       if (i == 0 && split)   // last_add_block's AADLayer reads the block input m as well
         group.push_back({blk + ".aadlast", base + 2 * cin * nb, (char*)cat + (size_t)cin * es, 2 * cin});
-      aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb, i == 0 && m_virtual);
+      aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb, i == 0 && m_virtual, small ? gmask : nullptr);
       if (!last) {
         void* xn = c.alloc(P * cin * es);
         float* st = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
         // the persistent conv writes the InstanceNorm partials of its output in its epilogue
         // (one pass less over xn); other conv kernels: a separate statistics pass
-        if (!conv3x3(c, cn, a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr, st))
+        if (small) {
+          conv3x3(c, cn, a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr, nullptr);
+          small_masks(xn, st, i + 1);
+        } else if (!conv3x3(c, cn, a, cin, cin, B, n, cin, xn, cin, nullptr, 0, 0, nullptr, st)) {
           run_stats(c, xn, cin, B, n * n, cin, st);
+        }
         x = xn;
         stat_x = st;
       } else if (!split) {

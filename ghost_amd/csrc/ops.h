@@ -31,6 +31,12 @@ int aad_mask(int dt, const void* h, int ldh, int B, int HW, int C, const float* 
 int aad_mask2(int dt, const void* h, int ldh, int B, int HW, int C, const float* stat, const float* wh0,
               const float* bh0, float* mask0, const float* wh1, const float* bh1, float* mask1, hipStream_t s);
 
+// HW <= 16 (2x2, 4x4): the statistics above AND the masks of one or two AADLayers (wh1 == nullptr:
+// one) from one launch, one workgroup per sample
+bool stats_mask_small_ok(int dt, int HW, int C, int ldx);
+int stats_mask_small(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, const float* wh0,
+                     const float* bh0, float* mask0, const float* wh1, const float* bh1, float* mask1, hipStream_t s);
+
 // bilinear x2, align_corners=True, NHWC (AEI_Net.py:94,125-137)
 int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C, hipStream_t s);
 
