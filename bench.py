@@ -18,7 +18,7 @@ Besides the JSON line's throughput, rank 0 at N = 1 reports
   128x128 source of h_in once, z_attr8 once, the two 256x256 outputs: 2.147 GB at B = 64) / its
   average launch time, timed with HIP events recorded on the launch stream around each of its
   launches inside the timed region; ``traffic`` = its PMC-measured HBM bytes per launch
-  (profiles/traffic_latest.json); ``formula_frac`` keeps SURVEY.md §8d's per-layer formula
+  (the newest profiles/rNN_traffic.json); ``formula_frac`` keeps SURVEY.md §8d's per-layer formula
   (|h_in|+|z_attr|+|out| per AADLayer, 3.22 GB), which counts bytes the fused kernel never moves;
 * roofline_conv3x3 (MFMA-bound, all generator 3x3 convs) and aad_decoder_gbs (SURVEY.md §8d
   definition: AADLayer bytes / total AAD kernel time);
@@ -77,15 +77,20 @@ def parse():
 def pmc_traffic(kernel_substr):
     """HBM bytes per launch of a kernel from the committed PMC summary (tools/pmc_traffic.py over
     separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 FETCH x2 correction)."""
-    path = os.path.join(REPO, "profiles", "traffic_latest.json")
+    import glob
+    rounds = sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]_traffic.json")))
+    if not rounds:
+        return None
+    path = rounds[-1]
     try:
         data = json.load(open(path))
     except (OSError, ValueError):
         return None
+    rel = os.path.relpath(path, REPO)
     for k in data.get("kernels", []):
         if kernel_substr in k["kernel"] and k.get("hbm_bytes"):
             return {"bytes_per_launch": k["hbm_bytes"], "read": k["read_bytes"], "write": k["write_bytes"],
-                    "source": "profiles/traffic_latest.json (" + data.get("source", "rocprofv3 --pmc") + ")"}
+                    "source": rel + " (" + data.get("source", "rocprofv3 --pmc") + ")"}
     return None
 
 
