@@ -17,13 +17,14 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-OBJ = os.path.join(HERE, "_build")
-LIB = os.path.join(HERE, "libghost_amd.so")
+TUNING = os.environ.get("GHOST_TUNING") == "1"   # A/B build: GHOST_KNOB switches read the environment
+OBJ = os.path.join(HERE, "_build_tuning" if TUNING else "_build")
+LIB = os.path.join(HERE, "libghost_amd_tuning.so" if TUNING else "libghost_amd.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + CSRC, "-I" + INCLUDE,
-          "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+          "-Wall", "-Wno-unused-function", "-Wno-unused-variable"] + (["-DGHOST_TUNING"] if TUNING else [])
 
 
 def _sources():

@@ -217,11 +217,18 @@ __global__ void __launch_bounds__(512) aad_v3_wide_kernel(const AadV3Args a) {
 // time (SQ_WAIT_ANY).  Here every wave keeps TWO 16-pixel tiles in flight: at the top of tile t it
 // issues tile t+1's z_attr fragments (to registers) and its h_in pixels (LDS-DMA into a wave-private
 // slot; for the through-upsample form the <= 10 source pixels of each of the two source rows), then
-// computes tile t.  The two slots are distinct LDS objects and the loop is unrolled by two, so the
-// compiler's own waitcnt pass knows which DMA a read depends on: the waits it emits leave tile t+1's
-// loads (and tile t-1's stores) in flight.  The h_in slot is XOR-swizzled on the source side
+// computes tile t, so tile t+1's loads overlap tile t's arithmetic.  (They do not overlap tile t's
+// stores: with loads and stores both outstanding the vmcnt counter is not in order, and the waitcnt
+// pass waits for zero before the next slot read; peeling / unrolling the loop so every wait could be
+// a partial count was measured and only added spills.)  The h_in slot is XOR-swizzled on the source side
 // (chunk c of pixel p lands at chunk c ^ (p & 7)) so the 16 pixels a lane group reads hit 16 bank
 // groups.
+// The per-pixel arithmetic (bilinear mix, mask dot product, normalise / blend) runs two channels per
+// packed-fp32 instruction (v_pk_fma_f32 etc., same per-element rounding as the scalar form), the
+// ReLU that follows every AADLayer is a template flag (one v_max instead of compare + select), and
+// the wave index goes through readfirstlane so every per-tile address is scalar arithmetic: measured
+// (B = 64, 256x256, L = 2) 474 -> 453 us with VALU instructions per tile 728 -> 492 (PMC: the round-2
+// kernel issued 661 VALU per 16-pixel tile, ~60 % of its SIMD cycles).
 // ---------------------------------------------------------------------------------------------
 template <int CA, int L, bool UP>
 struct V4Cfg {
@@ -231,8 +238,9 @@ struct V4Cfg {
   static constexpr int SLOT_B = ROWS * SPX * 128;  // bytes per wave per slot
 };
 
-template <int CA, int L, bool UP>
+template <int CA, int L, bool UP, bool RELU>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v4_kernel(const AadV3Args a) {
+  static_assert(UP, "v4 is the through-upsample form (v3's register loads win without the upsample)");
   using K = V4Cfg<CA, L, UP>;
   constexpr int C = 64, KS = K::KS, WLD = K::WLD, SPX = K::SPX, SLOT_B = K::SLOT_B;
   __shared__ __attribute__((aligned(16))) bf16 s_w[L * 128 * WLD];
@@ -246,7 +254,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   __shared__ __attribute__((aligned(1024))) unsigned char s_hA[kWaves * SLOT_B];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hB[kWaves * SLOT_B];
 
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  // wid through readfirstlane: tile indices and everything derived from them are wave-uniform (SGPRs),
+  // so the per-tile address arithmetic runs on the scalar unit and the VALU keeps only lane offsets
+  const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, lr = lane & 15,
+            lq = lane >> 4;
   const long p_begin = (long)blockIdx.x * a.PPW;
   const int b = (int)(p_begin / a.HW);
 
@@ -287,38 +298,34 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   // this wave's tiles: t = wid + 8 i, i = 0 .. nw-1 (nw even: PPW is a multiple of 256)
   const int nw = ntiles / kWaves;
 
+  const int r_begin = (int)(p_begin - (long)b * a.HW);   // first output pixel of the block in its sample
+  const int OW = 2 * a.up.W;
+  // lane parts of the addresses (the tile parts are scalar)
+  const int z_lane = lr * a.lda + lq * 8;
+
   // z fragments of tile t (registers) + its h_in pixels (DMA into slot `slot` of this wave)
   auto issue = [&](int t, u32x4 (&zc)[KS], unsigned char* slot) {
-    const long p = p_begin + t * 16 + lr;
+    const bf16* zt = a.za + (p_begin + t * 16) * a.lda;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + ks * 32 + lq * 8);
+    for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(zt + z_lane + ks * 32);
 #if defined(__HIP_DEVICE_COMPILE__)
     unsigned char* dst = slot + wid * SLOT_B;
-    if constexpr (UP) {
-      const int r = (int)(p_begin - (long)b * a.HW) + t * 16;     // first output pixel of the tile
-      const int oy = r / (2 * a.up.W), ox0 = r - oy * (2 * a.up.W);
-      float ry = a.up.sh * (float)oy, rx = a.up.sw * (float)ox0;
-      asm volatile("" : "+v"(ry), "+v"(rx));
-      const int y0 = (int)ry, x_lo = (int)rx;
-      const int y1 = y0 + (y0 < a.up.H - 1 ? 1 : 0);
+    const int r = r_begin + t * 16;                               // first output pixel of the tile
+    const int oy = r / OW, ox0 = r - oy * OW;
+    float ry = a.up.sh * (float)oy, rx = a.up.sw * (float)ox0;
+    asm volatile("" : "+v"(ry), "+v"(rx));
+    const int y0 = __builtin_amdgcn_readfirstlane((int)ry), x_lo = __builtin_amdgcn_readfirstlane((int)rx);
+    const int y1 = y0 + (y0 < a.up.H - 1 ? 1 : 0);
 #pragma unroll
-      for (int row = 0; row < 2; ++row) {
-        const int sy = row ? y1 : y0;
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const int pl = k * 8 + (lane >> 3), cl = lane & 7;     // LDS pixel / chunk this lane fills
-          if (k == 1 && lane >= 16) continue;                    // 10 pixels per row
-          const int sx = min(x_lo + pl, a.up.W - 1);
-          const bf16* g = src + ((long)sy * a.up.W + sx) * a.ldh + ((cl ^ (pl & 7)) * 8);
-          __builtin_amdgcn_global_load_lds(g, dst + row * SPX * 128 + k * 1024, 16, 0, 0);
-        }
-      }
-    } else {
+    for (int row = 0; row < 2; ++row) {
+      const bf16* srow = src + (long)(row ? y1 : y0) * a.up.W * a.ldh;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
-        const int pl = k * 8 + (lane >> 3), cl = lane & 7;
-        const bf16* g = a.hin + (p_begin + t * 16 + pl) * a.ldh + ((cl ^ (pl & 7)) * 8);
-        __builtin_amdgcn_global_load_lds(g, dst + k * 1024, 16, 0, 0);
+        const int pl = k * 8 + (lane >> 3), cl = lane & 7;     // LDS pixel / chunk this lane fills
+        if (k == 1 && lane >= 16) continue;                    // 10 pixels per row
+        const int sx = min(x_lo + pl, a.up.W - 1);
+        __builtin_amdgcn_global_load_lds(srow + sx * a.ldh + ((cl ^ (pl & 7)) * 8), dst + row * SPX * 128 + k * 1024,
+                                         16, 0, 0);
       }
     }
 #endif
@@ -326,34 +333,38 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 
   // phase 1: tile t's h_in chunks out of its LDS slot (through the bilinear x2 when UP)
   auto hload = [&](int t, const unsigned char* slot, u32x4 (&hc)[2]) {
-    const long p = p_begin + t * 16 + lr;
     const unsigned char* hs = slot + wid * SLOT_B;
     if constexpr (UP) {
-      const int r = (int)(p - (long)b * a.HW);
-      const int oy = r / (2 * a.up.W), ox = r - oy * (2 * a.up.W);
-      const int ox0 = ox - lr;
+      const int r = r_begin + t * 16;                             // the tile's output row and first column
+      const int oy = r / OW, ox0 = r - oy * OW;
       float rx0 = a.up.sw * (float)ox0;
       asm volatile("" : "+v"(rx0));
-      const int x_lo = (int)rx0;
-      const Up2xTap tp = up2x_tap(a.up, oy, ox);
-      // tap offsets o00 = y0*W + x0 etc.: recover the columns relative to the slot's first pixel
-      const int x0 = tp.o00 % a.up.W, x1 = tp.o01 % a.up.W;
+      const int x_lo = __builtin_amdgcn_readfirstlane((int)rx0);
+      // up2x_tap's arithmetic for this lane's output pixel (oy, ox0 + lr); the slot holds rows y0, y1
+      float ry = a.up.sh * (float)oy, rx = a.up.sw * (float)(ox0 + lr);
+      asm volatile("" : "+v"(ry), "+v"(rx));
+      const int y0 = (int)ry, x0 = (int)rx;
+      const int x1 = x0 + (x0 < a.up.W - 1 ? 1 : 0);
+      const float fly1 = ry - (float)y0, flx1 = rx - (float)x0;
       const int c0 = x0 - x_lo, c1 = x1 - x_lo;
+      const f32x2 ly0 = {1.f - fly1, 1.f - fly1}, ly1 = {fly1, fly1}, lx0 = {1.f - flx1, 1.f - flx1}, lx1 = {flx1, flx1};
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int ch = j * 4 + lq;                    // 16-byte chunk of channels 8ch .. 8ch+7
         auto ld = [&](int row, int col) {
           return *reinterpret_cast<const u32x4*>(hs + row * SPX * 128 + col * 128 + ((ch ^ (col & 7)) * 16));
         };
-        // same arithmetic as up2x_load16_f (up2x_mix)
+        // up2x_mix's arithmetic, two channels per packed-fp32 instruction
         const u32x4 r00 = ld(0, c0), r01 = ld(0, c1), r10 = ld(1, c0), r11 = ld(1, c1);
-        const bf16 *e00 = reinterpret_cast<const bf16*>(&r00), *e01 = reinterpret_cast<const bf16*>(&r01);
-        const bf16 *e10 = reinterpret_cast<const bf16*>(&r10), *e11 = reinterpret_cast<const bf16*>(&r11);
         bf16* hv = reinterpret_cast<bf16*>(&hc[j]);
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-          hv[q] = (bf16)up2x_mix(tp.ly0, tp.ly1, tp.lx0, tp.lx1, (float)e00[q], (float)e01[q], (float)e10[q],
-                                 (float)e11[q]);
+        for (int k = 0; k < 4; ++k) {
+          const f32x2 top = fma2(lx0, bf16x2_f(r00[k]), lx1 * bf16x2_f(r01[k]));
+          const f32x2 bot = fma2(lx0, bf16x2_f(r10[k]), lx1 * bf16x2_f(r11[k]));
+          const f32x2 v = fma2(ly0, top, ly1 * bot);
+          hv[2 * k] = (bf16)v.x;
+          hv[2 * k + 1] = (bf16)v.y;
+        }
       }
     } else {
 #pragma unroll
@@ -365,26 +376,27 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   };
   // phase 2: mask, gamma/beta MFMAs, blend and the stores of tile t
   auto compute = [&](int t, const u32x4 (&zc)[KS], const u32x4 (&hc)[2]) {
-    const long p = p_begin + t * 16 + lr;
-    float ms[L];
+    const long p0 = p_begin + t * 16;
+    f32x2 ms[L];
 #pragma unroll
-    for (int l = 0; l < L; ++l) ms[l] = 0.f;
+    for (int l = 0; l < L; ++l) ms[l] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int c0 = j * 32 + lq * 8;
-      const bf16* hv = reinterpret_cast<const bf16*>(&hc[j]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
+      for (int k = 0; k < 4; ++k) {
+        const f32x2 h2 = bf16x2_f(hc[j][k]);
 #pragma unroll
-        for (int l = 0; l < L; ++l) ms[l] = fmaf(s_cf[l * C + c0 + e], (float)hv[e], ms[l]);
+        for (int l = 0; l < L; ++l) ms[l] = fma2(*reinterpret_cast<const f32x2*>(&s_cf[l * C + c0 + 2 * k]), h2, ms[l]);
+      }
     }
     float Mk[L];
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-      float sm = ms[l];
+      float sm = ms[l].x + ms[l].y;
       sm += __shfl_xor(sm, 16, 64);
       sm += __shfl_xor(sm, 32, 64);
-      Mk[l] = sigmoidf_ref(sm + bh[l]);
+      Mk[l] = sigmoid_fast(sm + bh[l]);
     }
 #pragma unroll
     for (int l = 0; l < L; ++l) {
@@ -411,19 +423,28 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
           }
         }
         const int c0 = sh * 32 + lq * 8;
-        const bf16* hv = reinterpret_cast<const bf16*>(&hc[sh]);
+        const f32x2 M2 = {Mk[l], Mk[l]};
         float o[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float hh = fmaf((float)hv[e], s_rs[c0 + e], s_nm[c0 + e]);
-          const float g = acc[e >> 2][e & 3];
-          const float be = acc[2 + (e >> 2)][e & 3];
-          const float A = fmaf(g, hh, be);
-          const float I = fmaf(s_gi[l * C + c0 + e], hh, s_bi[l * C + c0 + e]);
-          const float v = fmaf(Mk[l], I - A, A);
-          o[e] = v > 0.f ? v : v * a.slope;
+        for (int k = 0; k < 4; ++k) {   // channels c0 + 2k, c0 + 2k + 1
+          const int c = c0 + 2 * k;
+          const f32x2 hh = fma2(bf16x2_f(hc[sh][k]), *reinterpret_cast<const f32x2*>(&s_rs[c]),
+                                *reinterpret_cast<const f32x2*>(&s_nm[c]));
+          const f32x2 g = {acc[k >> 1][(2 * k) & 3], acc[k >> 1][(2 * k + 1) & 3]};
+          const f32x2 be = {acc[2 + (k >> 1)][(2 * k) & 3], acc[2 + (k >> 1)][(2 * k + 1) & 3]};
+          const f32x2 A = fma2(g, hh, be);
+          const f32x2 I = fma2(*reinterpret_cast<const f32x2*>(&s_gi[l * C + c]), hh,
+                               *reinterpret_cast<const f32x2*>(&s_bi[l * C + c]));
+          const f32x2 v = fma2(M2, I - A, A);
+          if constexpr (RELU) {
+            o[2 * k] = fmaxf(v.x, 0.f);
+            o[2 * k + 1] = fmaxf(v.y, 0.f);
+          } else {
+            o[2 * k] = v.x > 0.f ? v.x : v.x * a.slope;
+            o[2 * k + 1] = v.y > 0.f ? v.y : v.y * a.slope;
+          }
         }
-        store16_f(a.out[l] + p * a.ldo[l] + c0, o);
+        store16_f(a.out[l] + p0 * a.ldo[l] + (lr * a.ldo[l] + c0), o);
       }
     }
   };
@@ -490,10 +511,12 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   if (use_v4 && up && d.C == 64 && a.PPW % 256 == 0 && d.ldh % 8 == 0) {
 #define GHOST_V4(ca, l, u)                                                                       \
     if (d.Ca == ca && d.L == l && up == u) {                                                     \
-      hipLaunchKernelGGL((aad_v4_kernel<ca, l, u>), grid, dim3(kWaves * 64), dyn_lds, s, a);     \
+      if (d.slope == 0.f)                                                                        \
+        hipLaunchKernelGGL((aad_v4_kernel<ca, l, u, true>), grid, dim3(kWaves * 64), dyn_lds, s, a); \
+      else                                                                                       \
+        hipLaunchKernelGGL((aad_v4_kernel<ca, l, u, false>), grid, dim3(kWaves * 64), dyn_lds, s, a); \
       return (int)hipGetLastError();                                                             \
     }
-    GHOST_V4(64, 1, false) GHOST_V4(64, 2, false) GHOST_V4(32, 1, false) GHOST_V4(32, 2, false)
     GHOST_V4(64, 1, true) GHOST_V4(64, 2, true) GHOST_V4(32, 1, true) GHOST_V4(32, 2, true)
 #undef GHOST_V4
   }

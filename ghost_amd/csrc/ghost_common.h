@@ -63,6 +63,14 @@ template <typename T> GHOST_DEV void store16_f(T* p, const float* in) {
 }
 
 GHOST_DEV float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
+// v_exp_f32 + v_rcp_f32 (a few ulp from sigmoidf_ref): for masks blended into bf16 outputs
+GHOST_DEV float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+
+// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth of fp32 per instruction)
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+GHOST_DEV f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+// the two bf16 of a 32-bit word (element 0 in the low half) as fp32
+GHOST_DEV f32x2 bf16x2_f(unsigned w) { return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)}; }
 
 // shuffle-xor reduction over `width` lanes (width power of two, <= 64)
 GHOST_DEV float group_sum(float v, int width) {
