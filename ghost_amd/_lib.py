@@ -16,8 +16,9 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 # GHOST_TUNING=1 selects the A/B tuning build (python -m ghost_amd.build with GHOST_TUNING=1: the
 # same sources with -DGHOST_TUNING, whose GHOST_KNOB switches read the environment)
-LIB_PATH = os.path.join(HERE, "libghost_amd_tuning.so" if os.environ.get("GHOST_TUNING") == "1"
-                        else "libghost_amd.so")
+# GHOST_LIB_FILE=<name> loads another in-tree build (same-box A/B against a saved library)
+LIB_PATH = os.path.join(HERE, os.environ.get("GHOST_LIB_FILE") or
+                        ("libghost_amd_tuning.so" if os.environ.get("GHOST_TUNING") == "1" else "libghost_amd.so"))
 HEADER = os.path.join(os.path.dirname(HERE), "include", "ghost_amd.h")
 
 F32, BF16, F16, U8 = 0, 1, 2, 3
