@@ -893,6 +893,8 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
       GHOST_PP_DBG(true, 2, 2) GHOST_PP_DBG(true, 2, 8) GHOST_PP_DBG(true, 2, 16) GHOST_PP_DBG(true, 2, 18)
       GHOST_PP_DBG(true, 2, 26) GHOST_PP_DBG(true, 2, 24)
       GHOST_PP_DBG(false, 4, 6) GHOST_PP_DBG(false, 4, 8) GHOST_PP_DBG(false, 4, 16) GHOST_PP_DBG(false, 4, 22)
+      GHOST_PP_DBG(false, 8, 6) GHOST_PP_DBG(false, 8, 8) GHOST_PP_DBG(false, 8, 16) GHOST_PP_DBG(false, 8, 22)
+      GHOST_PP_DBG(false, 8, 24) GHOST_PP_DBG(false, 8, 30) GHOST_PP_DBG(false, 8, 2) GHOST_PP_DBG(false, 8, 4)
 #undef GHOST_PP_DBG
     }
   }

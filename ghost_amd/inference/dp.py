@@ -16,7 +16,7 @@ No collective other than that all-gather is on the data path.
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, List, NamedTuple, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -79,6 +79,14 @@ def swap_mixed_identities(crops: torch.Tensor, identity_index: torch.Tensor, sou
     return G.swap_u8(crops, z, out=out)
 
 
+class Ticket(NamedTuple):
+    """What ``GatherPipeline.submit`` hands back: the buffer slot, the slot's generation when this batch
+    was written to it, and every rank's count of valid rows in it."""
+    slot: int
+    gen: int
+    counts: Tuple[int, ...]
+
+
 class GatherPipeline:
     """A stream of per-rank batches, each swapped on this GPU and then all-gathered to every rank,
     with the all-gather of batch k in flight (RCCL's own stream, over xGMI) while batch k+1 is
@@ -87,18 +95,27 @@ class GatherPipeline:
     before the swap overwrites it, so no batch's bytes change while a collective reads them.
 
     ``swap(crops, out)`` writes the uint8 swaps of ``crops`` into ``out`` (``AEI_Net.swap_u8``).
-    ``submit`` returns the slot whose ``result`` is the gathered [world * B, ...] batch in rank order.
+    ``submit(crops, counts)`` returns a ``Ticket``; ``result(ticket)`` is the gathered batch in rank
+    order.  A slot is rewritten ``depth`` submits later: reading a ticket whose slot has been reused
+    raises instead of returning another batch's bytes.  A short batch (fewer rows than
+    ``batch_shape[0]``, e.g. the last one of a shard) needs ``counts``, the valid-row count of every rank
+    for this submit (known to all ranks from ``shard_bounds``); ``result`` then returns only the valid
+    rows, rank by rank.  Rows past a rank's count travel as padding and are dropped.
     """
 
     def __init__(self, swap: Callable, batch_shape, device, dtype=torch.uint8, group=None, depth: int = 2):
         self.swap, self.group, self.depth = swap, group, max(1, depth)
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        dist_on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if dist_on else 1
+        self.rank = dist.get_rank(group) if dist_on else 0
         self.nccl = self.world > 1 and dist.get_backend(group) == "nccl"
         shape = tuple(batch_shape)
+        self.rows = shape[0]
         self.outs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(self.depth)]
         self.gath = ([torch.empty((self.world * shape[0],) + shape[1:], dtype=dtype, device=device)
                       for _ in range(self.depth)] if self.world > 1 else self.outs)
         self.pending: List[Optional[object]] = [None] * self.depth
+        self.gen = [0] * self.depth
         self.k = 0
 
     def _wait(self, slot: int):
@@ -107,10 +124,22 @@ class GatherPipeline:
             w.wait()
             self.pending[slot] = None
 
-    def submit(self, crops: torch.Tensor) -> int:
+    def submit(self, crops: torch.Tensor, counts: Optional[Sequence[int]] = None) -> Ticket:
+        n = crops.shape[0]
+        if n > self.rows:
+            raise ValueError(f"GatherPipeline: batch of {n} rows exceeds the pipeline's {self.rows}")
+        if counts is None:
+            if n != self.rows:
+                raise ValueError("GatherPipeline: a short batch needs counts (every rank's valid rows)")
+            counts = (self.rows,) * self.world
+        counts = tuple(int(c) for c in counts)
+        if len(counts) != self.world or counts[self.rank] != n or any(c < 0 or c > self.rows for c in counts):
+            raise ValueError(f"GatherPipeline: counts {counts} do not fit world {self.world}, rank {self.rank} "
+                             f"with {n} rows of at most {self.rows}")
         slot = self.k % self.depth
         self._wait(slot)                      # the collective still reading this slot's buffer
-        self.swap(crops, self.outs[slot])
+        if n:
+            self.swap(crops, self.outs[slot][:n])
         if self.world > 1:
             if self.nccl:
                 self.pending[slot] = dist.all_gather_into_tensor(self.gath[slot], self.outs[slot], group=self.group,
@@ -118,12 +147,21 @@ class GatherPipeline:
             else:
                 self.pending[slot] = dist.all_gather(list(self.gath[slot].chunk(self.world)), self.outs[slot],
                                                      group=self.group, async_op=True)
+        self.gen[slot] += 1
         self.k += 1
-        return slot
+        return Ticket(slot, self.gen[slot], counts)
 
-    def result(self, slot: int) -> torch.Tensor:
-        self._wait(slot)
-        return self.gath[slot]
+    def result(self, ticket: Ticket) -> torch.Tensor:
+        if not isinstance(ticket, Ticket):
+            raise TypeError("GatherPipeline.result takes the Ticket that submit returned")
+        if self.gen[ticket.slot] != ticket.gen:
+            raise RuntimeError(f"GatherPipeline: the batch of this ticket was overwritten ({self.gen[ticket.slot] - ticket.gen}"
+                               f" later submit(s) reused slot {ticket.slot}; depth {self.depth})")
+        self._wait(ticket.slot)
+        g = self.gath[ticket.slot]
+        if all(c == self.rows for c in ticket.counts):
+            return g
+        return torch.cat([g[r * self.rows:r * self.rows + c] for r, c in enumerate(ticket.counts)])
 
     def drain(self):
         for s in range(self.depth):

@@ -69,15 +69,23 @@ def _pipe_worker(rank, world, port, depth, q):
         pipe = GatherPipeline(lambda c, o: o.copy_(fake_swap(c)), (B, 4, 4, 3), torch.device("cpu"), depth=depth)
         batches = [torch.full((B, 4, 4, 3), 10 * k + rank, dtype=torch.uint8) + torch.arange(B, dtype=torch.uint8)
                    .view(B, 1, 1, 1) for k in range(5)]
-        got, prev = [], None
+        got, prev, stale = [], None, 0
         for k, bt in enumerate(batches):
-            slot = pipe.submit(bt)
+            t = pipe.submit(bt)
             if prev is not None:      # batch k-1's gather, read while batch k's is in flight
-                got.append(pipe.result(prev).clone())
-            prev = slot
+                try:
+                    got.append(pipe.result(prev).clone())
+                except RuntimeError:  # depth 1: batch k reused batch k-1's slot
+                    got.append(None)
+                    stale += 1
+            prev = t
         got.append(pipe.result(prev).clone())
+        # a short last batch: rank r holds r + 1 valid rows, every rank passes all counts
+        counts = [r + 1 for r in range(world)]
+        t = pipe.submit(batches[0][:rank + 1], counts=counts)
+        short = pipe.result(t).clone()
         pipe.drain()
-        q.put((rank, [g.numpy() for g in got]))
+        q.put((rank, [None if g is None else g.numpy() for g in got], stale, short.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -85,7 +93,8 @@ def _pipe_worker(rank, world, port, depth, q):
 @pytest.mark.parametrize("depth", [1, 2, 3])
 def test_gather_pipeline_gloo(depth):
     """dp.GatherPipeline (bench.py's swap -> all-gather stream): batch k's gathered swaps, in rank
-    order, on every rank, with batch k+1 submitted before batch k is read."""
+    order, on every rank, with batch k+1 submitted before batch k is read; a ticket whose slot was
+    reused raises; a short batch returns only every rank's valid rows."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -93,18 +102,39 @@ def test_gather_pipeline_gloo(depth):
     procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, depth, q)) for r in range(world)]
     for p in procs:
         p.start()
-    results = dict(q.get(timeout=120) for _ in range(world))
+    results = {r: (got, stale, short) for r, got, stale, short in (q.get(timeout=120) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     B = 3
-    for k in range(5):
-        expect = torch.cat([fake_swap(torch.full((B, 4, 4, 3), 10 * k + r, dtype=torch.uint8)
-                                      + torch.arange(B, dtype=torch.uint8).view(B, 1, 1, 1)) for r in range(world)])
-        for r in range(world):
+    for r in range(world):
+        got, stale, short = results[r]
+        assert stale == (4 if depth == 1 else 0)
+        for k in range(5):
+            expect = torch.cat([fake_swap(torch.full((B, 4, 4, 3), 10 * k + rr, dtype=torch.uint8)
+                                          + torch.arange(B, dtype=torch.uint8).view(B, 1, 1, 1)) for rr in range(world)])
             if depth == 1 and k < 4:
-                continue      # depth 1 reuses the slot: only the last batch is still readable
-            assert np.array_equal(results[r][k], expect.numpy()), (r, k)
+                assert got[k] is None
+                continue
+            assert np.array_equal(got[k], expect.numpy()), (r, k)
+        expect = torch.cat([fake_swap(torch.full((rr + 1, 4, 4, 3), rr, dtype=torch.uint8)
+                                      + torch.arange(rr + 1, dtype=torch.uint8).view(rr + 1, 1, 1, 1))
+                            for rr in range(world)])
+        assert np.array_equal(short, expect.numpy()), r
+
+
+def test_gather_pipeline_rejects_bad_batches():
+    from ghost_amd.inference.dp import GatherPipeline
+    pipe = GatherPipeline(lambda c, o: o.copy_(c), (3, 2), torch.device("cpu"), depth=1)
+    with pytest.raises(ValueError, match="counts"):
+        pipe.submit(torch.zeros(2, 2, dtype=torch.uint8))
+    with pytest.raises(ValueError, match="exceeds"):
+        pipe.submit(torch.zeros(4, 2, dtype=torch.uint8))
+    t0 = pipe.submit(torch.ones(3, 2, dtype=torch.uint8))
+    t1 = pipe.submit(torch.full((2, 2), 7, dtype=torch.uint8), counts=[2])
+    with pytest.raises(RuntimeError, match="overwritten"):
+        pipe.result(t0)
+    assert pipe.result(t1).tolist() == [[7, 7], [7, 7]]
 
 
 def test_shard_bounds_partition():
