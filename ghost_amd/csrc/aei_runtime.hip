@@ -69,7 +69,12 @@ struct ghost_aei {
   std::map<std::string, const void*> slots;   // name -> device pointer (nullptr = unbound)
   int id_total = 0;                            // sum over AAD layers of 2*c_x
   // per-handle plan options (ghost_aei_set_option); defaults are the measured choices
-  int opt[GHOST_AEI_NOPT] = {1, 1};
+  int opt[GHOST_AEI_NOPT] = {1, 1, 1};
+  // GHOST_AEI_OPT_TWO_STREAMS: the encoder up path's stream and its events (created on first use, on the
+  // device current then): zev[k] = z_attr_k written (k = 2..8), zev[0] = the down path done
+  hipStream_t s_up = nullptr;
+  int s_up_dev = -1;
+  hipEvent_t zev[9] = {nullptr};
   void* taps[8] = {nullptr};                   // ghost_aei_set_taps: AADBlk1..7 outputs copied here
   // profiling
   int prof_mask = 0;
@@ -106,6 +111,11 @@ struct Ctx {
   char* scratch = nullptr;
   size_t scratch_cap = 0;
   hipStream_t s;
+  // two-stream plan: the up path's stream and its own scratch region (the launches of the two streams
+  // overlap, so they cannot share the split-K / statistics partials)
+  bool dual = false, force_single = false;
+  hipStream_t s_up = nullptr;
+  char* scratch_up = nullptr;
   int rc = 0;
   std::string where;
 
@@ -353,7 +363,18 @@ void encoder(Ctx& c, const void* xin, int B, void* const attr[8]) {
     in = out;
     Hs /= 2;
   }
-  // up path: deconv_i = ConvT4x4/s2/p1 -> BN -> LReLU -> cat((x, skip)) | x + skip
+  // up path: deconv_i = ConvT4x4/s2/p1 -> BN -> LReLU -> cat((x, skip)) | x + skip.  Two-stream plan: it
+  // runs on the handle's second stream after the down path, and z_attr_{i+1} is published by an event
+  // the generator's AADBlk(i+1) waits for (AADBlk1 reads z_attr1, the down path's last output)
+  hipStream_t s_main = c.s;
+  char* scr_main = c.scratch;
+  const bool dual = c.dual && !c.dry;
+  if (dual && c.ok()) {
+    c.check((int)hipEventRecord(h->zev[0], c.s), "event record");
+    c.check((int)hipStreamWaitEvent(c.s_up, h->zev[0], 0), "stream wait");
+    c.s = c.s_up;
+    c.scratch = c.scratch_up;
+  }
   for (int i = 1; i <= 6; ++i) {
     int Cin, H, Cout, Ho;
     h->attr_geom(i, Cin, H);
@@ -371,11 +392,17 @@ void encoder(Ctx& c, const void* xin, int B, void* const attr[8]) {
     d.slope = kBnLrelu;
     if (h->linknet) { d.res = feat[7 - i].p; d.ldres = feat[7 - i].ld; }
     run_conv(c, d, 5, -1, 2.0 * B * Ho * Ho * co * 4.0 * Cin);
+    if (dual && c.ok()) c.check((int)hipEventRecord(h->zev[i + 1], c.s), "event record");
   }
   int C7, H7, C8, H8;
   h->attr_geom(7, C7, H7);
   h->attr_geom(8, C8, H8);
   run_up(c, attr[6], C7, attr[7], C8, B, H7, H7, C7);   // z_attr8 = F.interpolate(z_attr7) (AEI_Net.py:94)
+  if (dual) {
+    if (c.ok()) c.check((int)hipEventRecord(h->zev[8], c.s), "event record");
+    c.s = s_main;
+    c.scratch = scr_main;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -606,6 +633,8 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     int Ca, n;
     h->attr_geom(k, Ca, n);
     const void* za = attr[k - 1];
+    if (c.dual && !c.dry && k >= 2 && c.ok())   // z_attr_k comes from the encoder's up-path stream
+      c.check((int)hipStreamWaitEvent(c.s, h->zev[k], 0), "stream wait");
     const std::string blk = "gen.blk" + std::to_string(k);
     const size_t P = (size_t)B * n * n;
     const bool last_k = k == 8;
@@ -778,12 +807,16 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
     else
       c.check(input_to_nhwc(io.xt_dtype, io.xt, io.st, B, 3, 256, 256, h->dt, xin, c.s, 4), "input_to_nhwc");
   }
+  // the resnet encoder and get_attr run on one stream; the dry run sizes a second scratch region
+  c.dual = h->opt[GHOST_AEI_OPT_TWO_STREAMS] && mode != M_ATTR && !h->resnet && !c.force_single;
   encoder(c, xin, B, attr);
   if (mode == M_ATTR) return;
   float* zid32 = (float*)c.alloc((size_t)B * h->c_id * sizeof(float));
   if (!c.dry && c.ok()) c.check(rows_to_f32(io.zid_dtype, io.zid, io.zid_rs, B, h->c_id, zid32, c.s), "rows_to_f32");
   void* y = (mode == M_SWAP) ? c.alloc((size_t)B * 256 * 256 * 3 * es) : io.y;
   generator(c, B, attr, zid32, y, io.u8);
+  // the caller's stream waits for everything the up-path stream did (also when a launch failed midway)
+  if (c.dual && !c.dry) (void)hipStreamWaitEvent(c.s, h->zev[8], 0);
 }
 
 int64_t plan_bytes(ghost_aei* h, Mode mode, int B) {
@@ -795,7 +828,28 @@ int64_t plan_bytes(ghost_aei* h, Mode mode, int B) {
   io.y = (void*)(fake + 0x1000000);
   plan(c, mode, B, io);
   if (!c.ok()) return (int64_t)c.rc;
-  return (int64_t)(((c.off + 255) & ~size_t(255)) + c.scratch_need + 256);
+  const size_t scr = (c.scratch_need + 255) & ~size_t(255);
+  return (int64_t)(((c.off + 255) & ~size_t(255)) + (c.dual ? 2 : 1) * scr + 256);
+}
+
+// the handle's up-path stream and events on the current device (created once); false: run on one stream
+bool ensure_up_stream(ghost_aei* h) {
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (h->s_up && h->s_up_dev == dev) return true;
+  if (h->s_up) return false;   // created on another device: this call runs on one stream
+  // the up path fills the CUs the generator's small low-resolution launches leave idle: its stream gets
+  // the lowest priority, so the generator's workgroups dispatch first when both streams have work
+  static const int low_prio = GHOST_KNOB("GHOST_UP_STREAM_LOWPRIO", 1);
+  int least = 0, greatest = 0;
+  if (!low_prio || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+  hipStream_t st;
+  if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least) != hipSuccess) return false;
+  for (auto& e : h->zev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
+  h->s_up = st;
+  h->s_up_dev = dev;
+  return true;
 }
 
 int run(ghost_aei* h, Mode mode, int B, const Io& io, void* ws, int64_t ws_bytes, void* stream) {
@@ -806,7 +860,8 @@ int run(ghost_aei* h, Mode mode, int B, const Io& io, void* ws, int64_t ws_bytes
   plan(dry, mode, B, io);
   if (!dry.ok()) return fail(dry.rc, dry.where);
   const size_t main_bytes = (dry.off + 255) & ~size_t(255);
-  const size_t need = main_bytes + dry.scratch_need + 256;
+  const size_t scr = (dry.scratch_need + 255) & ~size_t(255);
+  const size_t need = main_bytes + (dry.dual ? 2 : 1) * scr + 256;
   if (!ws || (size_t)ws_bytes < need)
     return fail(GHOST_ENOWS, "workspace too small: need " + std::to_string(need) + " bytes");
   Ctx c{};
@@ -816,6 +871,11 @@ int run(ghost_aei* h, Mode mode, int B, const Io& io, void* ws, int64_t ws_bytes
   c.scratch = c.base + main_bytes;
   c.scratch_cap = dry.scratch_need;
   c.s = (hipStream_t)stream;
+  if (dry.dual && ensure_up_stream(h)) {
+    c.s_up = h->s_up;
+    c.scratch_up = c.scratch + scr;
+  }
+  c.force_single = !c.s_up;   // no second stream on this device: the same plan on one stream
   plan(c, mode, B, io);
   if (!c.ok()) return fail(c.rc, "forward failed at " + c.where + ": " + (c.rc > 0 ? hipGetErrorString((hipError_t)c.rc) : ""));
   return 0;
@@ -849,6 +909,9 @@ extern "C" int ghost_aei_create(const char* backbone, int num_blocks, int c_id, 
 extern "C" void ghost_aei_destroy(ghost_aei* h) {
   if (!h) return;
   for (auto e : h->ev) (void)hipEventDestroy(e);
+  for (auto e : h->zev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->s_up) (void)hipStreamDestroy(h->s_up);
   delete h;
 }
 

@@ -646,6 +646,43 @@ upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, 
   store16_f(y + ((long)row * Wo + ox) * ldy + ci * VEC, o);
 }
 
+// R output rows per workgroup (same sample: 2H % R == 0), each thread's 4R source loads issued
+// before any of them is used: a 256 x 256 x 64 output is 16 K workgroups instead of 64 K
+template <typename T, int R>
+__global__ void __launch_bounds__(256)
+upsample2x_rows_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, const Up2xSrc u, int lg_nch) {
+  constexpr int VEC = Vec16<T>::N;
+  const int Wo = 2 * u.W, Ho = 2 * u.H;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= (Wo << lg_nch)) return;
+  const int row0 = blockIdx.y * R;
+  const int b = row0 / Ho, oy0 = row0 - b * Ho;
+  const int ox = i >> lg_nch, ci = i - (ox << lg_nch);
+  const T* xs = x + (long)b * u.H * u.W * ldx + ci * VEC;
+  u32x4 raw[R][4];
+  Up2xTap t[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    t[r] = up2x_tap(u, oy0 + r, ox);
+    raw[r][0] = *reinterpret_cast<const u32x4*>(xs + t[r].o00 * ldx);
+    raw[r][1] = *reinterpret_cast<const u32x4*>(xs + t[r].o01 * ldx);
+    raw[r][2] = *reinterpret_cast<const u32x4*>(xs + t[r].o10 * ldx);
+    raw[r][3] = *reinterpret_cast<const u32x4*>(xs + t[r].o11 * ldx);
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const T* e00 = reinterpret_cast<const T*>(&raw[r][0]);
+    const T* e01 = reinterpret_cast<const T*>(&raw[r][1]);
+    const T* e10 = reinterpret_cast<const T*>(&raw[r][2]);
+    const T* e11 = reinterpret_cast<const T*>(&raw[r][3]);
+    float o[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e)
+      o[e] = up2x_mix(t[r].ly0, t[r].ly1, t[r].lx0, t[r].lx1, to_f(e00[e]), to_f(e01[e]), to_f(e10[e]), to_f(e11[e]));
+    store16_f(y + ((long)(row0 + r) * Wo + ox) * ldy + ci * VEC, o);
+  }
+}
+
 int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C, hipStream_t s) {
   const int vec = dt == GHOST_F32 ? 4 : 8;
   if (C % vec || ldx % vec || ldy % vec || (uintptr_t)x % 16 || (uintptr_t)y % 16) return -1;
@@ -655,6 +692,16 @@ int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, i
   const int nch = C / vec;
   int lg = -1;
   if ((nch & (nch - 1)) == 0) for (lg = 0; (1 << lg) < nch; ++lg) {}
+  static const int rows = GHOST_KNOB("GHOST_UP_ROWS", 2);
+  if (dt == GHOST_BF16 && lg >= 0 && (rows == 2 || rows == 4) && (2 * H) % rows == 0 &&
+      (long)H * W * ldx < (1L << 31)) {
+    grid.y = (unsigned)(B * 2 * H / rows);
+    if (rows == 4)
+      hipLaunchKernelGGL((upsample2x_rows_kernel<bf16, 4>), grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, u, lg);
+    else
+      hipLaunchKernelGGL((upsample2x_rows_kernel<bf16, 2>), grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, u, lg);
+    return (int)hipGetLastError();
+  }
   if (dt == GHOST_F32)
     hipLaunchKernelGGL(upsample2x_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, u, C, lg);
   else if (dt == GHOST_BF16)

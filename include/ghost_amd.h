@@ -82,8 +82,13 @@ int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_str
  *                                    instead of reading a materialised upsample (0 materialises it)
  *   GHOST_AEI_OPT_FUSE_STATS (1):    the persistent 3x3 conv emits the InstanceNorm partials of its output
  *                                    (0: a separate statistics pass)
+ *   GHOST_AEI_OPT_TWO_STREAMS (1):   forward / swap run the attribute encoder's up path (deconv1..6 and the
+ *                                    z_attr8 upsample) on a second, handle-owned HIP stream, overlapped with
+ *                                    the generator's AADBlk k, which waits only for z_attr_k; the caller's
+ *                                    stream waits for that stream before the call's last launch, so the
+ *                                    ordering seen by the caller is unchanged (0: one stream).  Same results.
  * value is 0 or 1.  A handle is not shared across threads without external synchronisation. */
-enum { GHOST_AEI_OPT_FUSE_UPSAMPLE = 0, GHOST_AEI_OPT_FUSE_STATS = 1, GHOST_AEI_NOPT = 2 };
+enum { GHOST_AEI_OPT_FUSE_UPSAMPLE = 0, GHOST_AEI_OPT_FUSE_STATS = 1, GHOST_AEI_OPT_TWO_STREAMS = 2, GHOST_AEI_NOPT = 3 };
 int ghost_aei_set_option(ghost_aei* h, int option, int value);
 int ghost_aei_get_option(ghost_aei* h, int option, int* value);
 /* Diagnostic taps (parity bisection): while set, every forward / swap of the handle copies the stored
