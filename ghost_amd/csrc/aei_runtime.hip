@@ -597,10 +597,16 @@ bool conv3x3(Ctx& c, const std::string& wname, const void* x, int ldx, int Cin, 
   return fused;
 }
 
-void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, void* y_out, uint8_t* u8) {
+// identity projections of every AADLayer at once (idgb) and up1 (m1): they read z_id only, so the
+// two-stream plan runs them on the up-path stream while the encoder's down path runs
+struct GenIn {
+  float* idgb;
+  void* m;
+};
+
+GenIn generator_prologue(Ctx& c, int B, const float* zid32) {
   ghost_aei* h = c.h;
   const int es = h->esz;
-  const int nb = h->nb;
   // identity projections of every AADLayer at once: idgb[b] = [gamma_id | beta_id] per layer (fc1/fc2)
   float* idgb = (float*)c.alloc((size_t)B * h->id_total * sizeof(float));
   {
@@ -625,6 +631,17 @@ void generator(Ctx& c, int B, const void* const attr[8], const float* zid32, voi
     d.shift = (const float*)c.W("gen.up1.shift");
     run_conv(c, d, 7, -1, 2.0 * B * 4096 * h->c_id);
   }
+  return {idgb, m};
+}
+
+void generator(Ctx& c, int B, const void* const attr[8], GenIn gin, void* y_out, uint8_t* u8) {
+  ghost_aei* h = c.h;
+  const int es = h->esz;
+  const int nb = h->nb;
+  float* idgb = gin.idgb;
+  void* m = gin.m;
+  if (c.dual && !c.dry && c.ok())   // idgb and m1 come from the up-path stream
+    c.check((int)hipStreamWaitEvent(c.s, h->zev[1], 0), "stream wait");
   int id_off = 0;
   bool m_virtual = false;   // m is not materialised: h_in = upsample2x(m) at n x n (m is n/2 x n/2)
   const void* m_src = nullptr;   // m = upsample2x(m_src) materialised: its statistics come from the source
@@ -809,15 +826,41 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
   }
   // the resnet encoder and get_attr run on one stream; the dry run sizes a second scratch region
   c.dual = h->opt[GHOST_AEI_OPT_TWO_STREAMS] && mode != M_ATTR && !h->resnet && !c.force_single;
+  GenIn gin{};
+  float* zid32 = nullptr;
+  auto prologue = [&]() {
+    zid32 = (float*)c.alloc((size_t)B * h->c_id * sizeof(float));
+    if (!c.dry && c.ok()) c.check(rows_to_f32(io.zid_dtype, io.zid, io.zid_rs, B, h->c_id, zid32, c.s), "rows_to_f32");
+    gin = generator_prologue(c, B, zid32);
+  };
+  if (mode != M_ATTR && c.dual) {
+    // up-path stream: z_id -> idgb, m1 first (overlapping the down path), then the encoder's up path
+    hipStream_t s_main = c.s;
+    char* scr_main = c.scratch;
+    if (!c.dry) {
+      if (c.ok()) c.check((int)hipEventRecord(h->zev[1], s_main), "event record");
+      if (c.ok()) c.check((int)hipStreamWaitEvent(c.s_up, h->zev[1], 0), "stream wait");
+      c.s = c.s_up;
+      c.scratch = c.scratch_up;
+    }
+    prologue();
+    if (!c.dry) {
+      if (c.ok()) c.check((int)hipEventRecord(h->zev[1], c.s), "event record");
+      c.s = s_main;
+      c.scratch = scr_main;
+    }
+  }
   encoder(c, xin, B, attr);
   if (mode == M_ATTR) return;
-  float* zid32 = (float*)c.alloc((size_t)B * h->c_id * sizeof(float));
-  if (!c.dry && c.ok()) c.check(rows_to_f32(io.zid_dtype, io.zid, io.zid_rs, B, h->c_id, zid32, c.s), "rows_to_f32");
+  if (!c.dual) prologue();
   void* y = (mode == M_SWAP) ? c.alloc((size_t)B * 256 * 256 * 3 * es) : io.y;
-  generator(c, B, attr, zid32, y, io.u8);
+  generator(c, B, attr, gin, y, io.u8);
   // the caller's stream waits for everything the up-path stream did (also when a launch failed midway)
   if (c.dual && !c.dry) (void)hipStreamWaitEvent(c.s, h->zev[8], 0);
 }
+
+// the one-stream fallback of a two-stream plan allocates in another order: alignment padding may differ
+constexpr size_t kMainSlack = 64 * 256;
 
 int64_t plan_bytes(ghost_aei* h, Mode mode, int B) {
   Ctx c{};
@@ -829,7 +872,7 @@ int64_t plan_bytes(ghost_aei* h, Mode mode, int B) {
   plan(c, mode, B, io);
   if (!c.ok()) return (int64_t)c.rc;
   const size_t scr = (c.scratch_need + 255) & ~size_t(255);
-  return (int64_t)(((c.off + 255) & ~size_t(255)) + (c.dual ? 2 : 1) * scr + 256);
+  return (int64_t)(((c.off + 255) & ~size_t(255)) + kMainSlack + (c.dual ? 2 : 1) * scr + 256);
 }
 
 // the handle's up-path stream and events on the current device (created once); false: run on one stream
@@ -859,7 +902,7 @@ int run(ghost_aei* h, Mode mode, int B, const Io& io, void* ws, int64_t ws_bytes
   dry.h = h; dry.dry = true;
   plan(dry, mode, B, io);
   if (!dry.ok()) return fail(dry.rc, dry.where);
-  const size_t main_bytes = (dry.off + 255) & ~size_t(255);
+  const size_t main_bytes = ((dry.off + 255) & ~size_t(255)) + kMainSlack;
   const size_t scr = (dry.scratch_need + 255) & ~size_t(255);
   const size_t need = main_bytes + (dry.dual ? 2 : 1) * scr + 256;
   if (!ws || (size_t)ws_bytes < need)

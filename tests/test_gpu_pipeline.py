@@ -154,3 +154,22 @@ def test_config5_linknet3_four_identities_bf16(lib):
     tg = np.sort(d_gpu, axis=None)[-k:].mean()
     te = np.sort(d_emu, axis=None)[-k:].mean()
     assert tg <= 1.3 * te + 1.0, (float(tg), float(te))
+
+
+@pytest.mark.parametrize("backbone,nb,B", [("unet", 2, 4), ("linknet", 3, 2)])
+def test_two_stream_plan_is_bit_identical(lib, backbone, nb, B):
+    """GHOST_AEI_OPT_TWO_STREAMS: the encoder's up path and the identity projections on the handle's second
+    stream give the same bytes as the one-stream plan (forward outputs, attrs and the uint8 swap)."""
+    G, _ = model(backbone, nb, torch.bfloat16)
+    xt, z = aei_ref.make_inputs(B, 23)
+    crops = torch.from_numpy(aei_ref.make_u8_crops(B, 23)).to(DEV)
+    res = {}
+    for mode in (0, 1):
+        G.set_option("two_streams", mode)
+        Y, attr = G(xt.to(DEV), z.to(DEV))
+        u8 = G.swap_u8(crops, z.to(DEV))
+        torch.cuda.synchronize()
+        res[mode] = (Y.clone(), [a.clone() for a in attr], u8.clone())
+    assert torch.equal(res[0][0], res[1][0])
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+    assert torch.equal(res[0][2], res[1][2])
