@@ -176,6 +176,7 @@ __global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int 
   __shared__ __attribute__((aligned(1024))) unsigned char lds1[STAGE_B];
   __shared__ __attribute__((aligned(16))) float s_b[256];
   __shared__ __attribute__((aligned(16))) float s_rs[128], s_nm[128], s_gi[128], s_bi[128];
+  __shared__ __attribute__((aligned(1024))) float s_mask[256];
 
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
   const int ncp = C / 128;
@@ -244,6 +245,22 @@ __global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int 
           acc[rt][pf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rt], bfr[pf], acc[rt][pf], 0, 0, 0);
     }
   };
+  // the epilogue's inputs — the tile's h_in (256 pixels x 128 channels = 64 KB) and its 256 mask values —
+  // are DMA'd into the free stage buffer and s_mask while the last K stage computes, instead of 16
+  // dependent global loads per lane after it (chunk c of pixel P at 16-byte slot c ^ (P & 15): the 16
+  // pixels a lane group reads hit 16 bank groups)
+  auto issue_epi = [&]() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int wu = __builtin_amdgcn_readfirstlane(wid);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int q = wu + 4 * j;                  // piece: pixels 4q .. 4q+3
+      const int P = q * 4 + (lane >> 4), lc = (lane & 15) ^ (P & 15);
+      __builtin_amdgcn_global_load_lds(a.hin + (p0 + P) * a.ldh + c0 + lc * 8, lds0 + q * 1024, 16, 0, 0);
+    }
+    if (wu == 0) __builtin_amdgcn_global_load_lds(a.mask + p0 + lane * 4, (unsigned char*)s_mask, 16, 0, 0);
+#endif
+  };
   // stage pairs: even stages read lds0 and prefetch into lds1, odd ones the reverse (distinct LDS
   // objects, static waits: the compiler does not drain the in-flight DMA before the fragment reads)
   for (int st = 0; st < NST; st += 2) {
@@ -254,20 +271,29 @@ __global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (st + 2 < NST) issue(lds0, st + 2);
+    else issue_epi();
     compute(lds1);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
   // epilogue (aad_v3's register blend): lane holds, per pixel fragment pf and half sh, gamma / beta of
   // channels wr*64 + 32sh + 8lq + e (e < 8) of pixel wp*128 + 16pf + lr
 #pragma unroll
   for (int pf = 0; pf < 8; ++pf) {
-    const long p = p0 + wp * 128 + pf * 16 + lr;
-    const float Mk = a.mask[p];
+    const int P = wp * 128 + pf * 16 + lr;                  // pixel within the tile
+    const long p = p0 + P;
+    const float Mk = s_mask[P];
 #pragma unroll
     for (int sh = 0; sh < 2; ++sh) {
       const int cl = wr * 64 + sh * 32 + lq * 8;           // channel within the 128 of the tile
       float hv[8];
-      load16_f(a.hin + p * a.ldh + c0 + cl, hv);
+      {
+        const u32x4 raw = *reinterpret_cast<const u32x4*>(lds0 + P * 256 + (((cl >> 3) ^ (P & 15)) * 16));
+        const bf16* e = reinterpret_cast<const bf16*>(&raw);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hv[i] = (float)e[i];
+      }
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
