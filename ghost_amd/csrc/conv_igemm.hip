@@ -14,6 +14,7 @@
 #include "conv_igemm.h"
 #include "conv_first.h"
 #include "conv_halo.h"
+#include "conv_s2.h"
 #include "ghost_common.h"
 
 namespace ghost {
@@ -94,12 +95,6 @@ GHOST_DEV float epi_aad(const ConvArgs& a, float ga, float ba, int c, long m) {
   const float I = gi * h + bi;
   float out = (1.0f - Mk) * A + Mk * I;
   return out > 0.f ? out : out * a.slope;
-}
-
-GHOST_DEV int xcd_remap(int bid, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7;
-  const int xcd = bid & 7, idx = bid >> 3;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
 GHOST_DEV long out_pixel(const ConvArgs& a, long m, int py, int px) {
@@ -817,7 +812,9 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
 }  // namespace
 
 size_t conv_workspace_bytes(const ConvDesc& d) {
-  if (conv3x3_halo_supported(d) || convT_halo_supported(d) || conv_stem3x3_supported(d)) return 0;
+  if (conv3x3_halo_supported(d) || convT_halo_supported(d) || conv_stem3x3_supported(d) ||
+      conv4x4s2_patch_supported(d))
+    return 0;
   if (conv_first_supported(d)) return conv_first_workspace_bytes();
   Plan p = make_plan(d);
   if (!p.partial) return 0;
@@ -835,6 +832,7 @@ int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream
   if (conv_first_supported(d)) return conv_first(d, ws, ws_bytes, stream);
   if (conv_stem3x3_supported(d)) return conv_stem3x3(d, stream);
   if (convT_halo_supported(d)) return convT_halo(d, stream);
+  if (conv4x4s2_patch_supported(d)) return conv4x4s2_patch(d, stream);
   Plan p = make_plan(d);
   if (p.NT > d.Npad) return -1;  // weight rows read by the last tile must exist
   const int K = d.kind == CONV_T4S2 ? 4 * d.Cin : d.kh * d.kw * d.Cin;

@@ -72,6 +72,15 @@ GHOST_DEV f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_f
 // the two bf16 of a 32-bit word (element 0 in the low half) as fp32
 GHOST_DEV f32x2 bf16x2_f(unsigned w) { return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)}; }
 
+// workgroup id -> work index such that each XCD (the hardware deals workgroups round-robin over the
+// 8 XCDs) gets one contiguous run of work indices, so neighbours that share input lines hit the same
+// L2 (cdna_hip_programming.md T1, bijective form)
+GHOST_DEV int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
 // shuffle-xor reduction over `width` lanes (width power of two, <= 64)
 GHOST_DEV float group_sum(float v, int width) {
   for (int o = width >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

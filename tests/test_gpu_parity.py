@@ -103,6 +103,49 @@ def test_conv2d_op(lib, dt, cin, cout, k, s, p, H):
     assert float((got - ref).abs().max()) <= tol * max(1.0, float(ref.abs().max()))
 
 
+@pytest.mark.parametrize("cin,cout,H,B,xoff,yoff,bn", [(32, 64, 32, 2, 32, 64, True), (64, 128, 64, 2, 0, 0, True),
+                                                 (128, 256, 32, 3, 128, 256, True), (32, 64, 64, 1, 0, 0, False),
+                                                 (256, 64, 32, 2, 256, 0, True)])
+def test_conv4x4s2_patch_kernel(lib, cin, cout, H, B, xoff, yoff, bn):
+    """The encoder's 4x4/s2 convs with Cin % 32 == 0 (conv2..conv4) on the LDS input-patch kernel: the input read
+    from a channel slice of a 2*Cin-wide buffer (the unet concat layout) and the output written into a channel
+    slice of a wider buffer, against torch's fp32 conv of the same bf16 operands."""
+    from ghost_amd import _lib
+    from ghost_amd.network.pack import pack_conv, rup
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(cin + 3 * cout + H)
+    x = torch.randn(B, cin, H, H, generator=g)
+    w = torch.randn(cout, cin, 4, 4, generator=g) * (2.0 / (cin * 16)) ** 0.5
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh = torch.randn(cout, generator=g) * 0.1
+    Ho = H // 2
+    xr, wr = x.to(dt).float(), w.to(dt).float()
+    v = F.conv2d(xr, wr, stride=2, padding=1)
+    if bn:
+        v = v * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)
+    ref = F.leaky_relu(v, 0.1)
+    ldx, ldy = cin + xoff, cout + yoff
+    xbuf = torch.randn(B, H, H, ldx, generator=g).to(dt).to(DEV)
+    xbuf[..., xoff:] = nhwc(x).to(dt).to(DEV)
+    ybuf = torch.full((B, Ho, Ho, ldy), 7.0, dtype=dt, device=DEV)
+    wp = pack_conv(w, dt).to(DEV)
+    scp = torch.zeros(rup(cout, 128), device=DEV); scp[:cout] = sc.to(DEV)
+    shp = torch.zeros(rup(cout, 128), device=DEV); shp[:cout] = sh.to(DEV)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=DEV)
+    _lib.check(lib.ghost_conv2d_nhwc(_lib.gdtype(dt), xbuf[..., xoff:].data_ptr(), B, H, H, cin, ldx, wp.data_ptr(),
+                                     cout, wp.shape[0], wp.shape[1], 4, 4, 2, 1,
+                                     scp.data_ptr() if bn else None, shp.data_ptr() if bn else None, 0.1, None, 0, 0,
+                                     ybuf[..., yoff:].data_ptr(), ldy, ws.data_ptr(), ws.numel(), stream(lib)))
+    torch.cuda.synchronize()
+    got = ybuf[..., yoff:].float().cpu().permute(0, 3, 1, 2)
+    err = float((got - ref).abs().max())
+    assert err <= 2e-2 * max(1.0, float(ref.abs().max())), err
+    # bf16 rounding of the fp32 result: at most 1 ulp away almost everywhere
+    assert float(((got - ref).abs() > 2 ** -7 * ref.abs() + 1e-3).float().mean()) < 1e-3
+    if yoff:   # the channels before the slice are untouched
+        assert bool((ybuf[..., :yoff] == 7.0).all())
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cin,ldx,cout,k,s,p,H,mode", [
     (3, 4, 64, 7, 1, 3, 32, "relu"),          # resnet encoder conv0 on the 4-channel input layout
