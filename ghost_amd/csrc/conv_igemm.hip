@@ -415,8 +415,10 @@ GHOST_DEV void glds_issue(const ConvArgs& a, const bf16* __restrict__ x, const b
 #endif
 }
 
-template <int BM, int BN, int STAGES, int EPI>
-__global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
+// WSL = 4: warp-specialised form, 512 threads: waves 0-3 run the MFMAs and the epilogue, waves 4-7 only issue
+// the ring's LDS-DMA (same ring, same per-K-step barrier), so no compute wave pays the DMA issue cost
+template <int BM, int BN, int STAGES, int EPI, int WSL = 0>
+__global__ void __launch_bounds__(WSL ? 512 : 256) conv_glds_kernel(const ConvArgs a) {
   typedef bf16 TI;
   typedef bf16 TO;
   constexpr int WM = WaveGrid<BM, BN>::WM, WN = WaveGrid<BM, BN>::WN;
@@ -430,7 +432,10 @@ __global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
   static_assert((STAGES - 2) * LPS <= 63, "vmcnt range");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[STAGES * STAGE_B];
 
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, lr = lane & 15,
+            lq = lane >> 4;
+  const bool loads = !WSL || wid >= 4, computes = !WSL || wid < 4;
+  const int lw = WSL ? wid - 4 : wid;   // index of this wave among the DMA-issuing waves
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   // N-major order (deep ring): an XCD's run of tiles covers few channel tiles, whose weight rows
   // then stay in that XCD's 4 MB L2 while every M tile streams past them
@@ -454,7 +459,7 @@ __global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
   int a_gc[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
-    const int r = 16 * (wid * NA + j) + lrow;
+    const int r = 16 * (lw * NA + j) + lrow;
     const int m = m0 + r;
     a_gc[j] = swz(r, pc) * 8;
     a_off[j] = 0;
@@ -480,11 +485,11 @@ __global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
   const TI* b_src[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int r = 16 * (wid * NB + j) + lrow;
+    const int r = 16 * (lw * NB + j) + lrow;
     b_src[j] = w + (long)(n0 + r) * a.Kpad + swz(r, pc) * 8;
   }
 
-  const int wm = wid / WN, wn = wid % WN;
+  const int wm = (wid & 3) / WN, wn = (wid & 3) % WN;
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -492,18 +497,20 @@ __global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int n = kt1 - kt0;
+  if (loads) {
 #pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < n) glds_issue<BM, NA, NB>(a, x, b_src, a_off, a_mask, a_gc, wid, kt0 + s, lds + s * STAGE_B);
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (s < n) glds_issue<BM, NA, NB>(a, x, b_src, a_off, a_mask, a_gc, lw, kt0 + s, lds + s * STAGE_B);
+  }
   for (int it = 0; it < n; ++it) {
     // stages issued after `it` that may stay in flight
-    const int after = min(STAGES - 2, n - 1 - it);
-    wait_stages<LPS, STAGES - 2>(after);
+    if (loads) wait_stages<LPS, STAGES - 2>(min(STAGES - 2, n - 1 - it));
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (it + STAGES - 1 < n)
-      glds_issue<BM, NA, NB>(a, x, b_src, a_off, a_mask, a_gc, wid, kt0 + it + STAGES - 1,
+    if (loads && it + STAGES - 1 < n)
+      glds_issue<BM, NA, NB>(a, x, b_src, a_off, a_mask, a_gc, lw, kt0 + it + STAGES - 1,
                              lds + ((it + STAGES - 1) % STAGES) * STAGE_B);
+    if (!computes) continue;
     const unsigned char* sb = lds + (it % STAGES) * STAGE_B;
     const unsigned char* As = sb;
     const unsigned char* Bs = sb + BM * 64;
@@ -524,6 +531,7 @@ __global__ void __launch_bounds__(256) conv_glds_kernel(const ConvArgs a) {
       for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
   }
 
+  if (!computes) return;
   // ---- epilogue (as v1) ----
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -733,18 +741,31 @@ int dispatch_tile(const ConvArgs& a, const Plan& p, hipStream_t s) {
 template <int EPI>
 bool launch_glds(const ConvArgs& a, const Plan& p, hipStream_t s) {
   static const int stages_knob = GHOST_KNOB("GHOST_CONV_STAGES", 3);
+  // warp-specialised DMA waves (B = 64, same box: 4x4 3x3 1024 conv 50 -> 41 us, encoder conv5..7 49 / 47 / 32 ->
+  // 40 / 38 / 28, deconv2 82 -> 64; bench +0.4..1.8 %)
+  static const int ws = GHOST_KNOB("GHOST_CONV_WS", 1);
   const int stages = p.stages > 0 ? p.stages : stages_knob;
   dim3 grid(p.nMt * p.nNt, p.nsplit, p.npar);
   if constexpr (EPI == KEPI_AAD) {
     if (p.BM == 128 && p.BN == 128 && stages == 8) {
-      hipLaunchKernelGGL((conv_glds_kernel<128, 128, 8, EPI>), grid, dim3(256), 0, s, a);
+      if (ws)
+        hipLaunchKernelGGL((conv_glds_kernel<128, 128, 8, EPI, 4>), grid, dim3(512), 0, s, a);
+      else
+        hipLaunchKernelGGL((conv_glds_kernel<128, 128, 8, EPI>), grid, dim3(256), 0, s, a);
+      return true;
+    }
+    if (p.BM == 128 && p.BN == 128 && stages == 3 && ws) {
+      hipLaunchKernelGGL((conv_glds_kernel<128, 128, 3, EPI, 4>), grid, dim3(512), 0, s, a);
       return true;
     }
     return false;
   }
 #define GHOST_G(bm, bn, st)                                                                      \
   if (p.BM == bm && p.BN == bn && stages == st) {                                                \
-    hipLaunchKernelGGL((conv_glds_kernel<bm, bn, st, EPI>), grid, dim3(256), 0, s, a);           \
+    if (ws)                                                                                       \
+      hipLaunchKernelGGL((conv_glds_kernel<bm, bn, st, EPI, 4>), grid, dim3(512), 0, s, a);      \
+    else                                                                                          \
+      hipLaunchKernelGGL((conv_glds_kernel<bm, bn, st, EPI>), grid, dim3(256), 0, s, a);         \
     return true;                                                                                  \
   }
   GHOST_G(128, 128, 8) GHOST_G(128, 128, 6)
@@ -771,7 +792,8 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
   static const int use_v2 = GHOST_KNOB("GHOST_CONV_V2", 1);
   if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
     // measured (tools/bench_ops.py): the DMA ring wins on the 128-row tiles, loses on 256x64
-    if (use_v2 && p.fast && p.BK == 32 && (d.epi != EPI_AAD || p.stages > 0) && p.BM <= 128 &&
+    static const int aad_glds = GHOST_KNOB("GHOST_CONV_AAD_GLDS", 0);   // AAD epilogue on the 3-stage ring
+    if (use_v2 && p.fast && p.BK == 32 && (d.epi != EPI_AAD || p.stages > 0 || aad_glds) && p.BM <= 128 &&
         p.partial == (p.nsplit > 1)) {
       const bool ok = p.nsplit > 1 ? launch_glds<KEPI_SPLIT>(a, p, s)
                                    : (d.epi == EPI_AAD ? launch_glds<KEPI_AAD>(a, p, s) : launch_glds<KEPI_STD>(a, p, s));
