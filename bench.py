@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--cpu-batches", default="1,64", help="CPU baseline batch sizes ('' = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--arc-batch", type=int, default=64, help="faces per ArcFace embedding batch in its leg")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="batches in flight on the GPU (dp.GatherPipeline streams; 1 = one batch at a time)")
     ap.add_argument("--opt", action="append", default=[],
                     help="AEI_Net plan option name=value (A/B runs), e.g. --opt fuse_stats=0")
     return ap.parse_args()
@@ -362,10 +364,13 @@ def main():
     else:
         z = zs[:1]
     # swap -> all-gather of the uint8 swaps to every rank; the gather of step k overlaps step k + 1
-    # (dp.GatherPipeline; GHOST_DP_OVERLAP=0 gathers synchronously after each step)
+    # (dp.GatherPipeline; GHOST_DP_OVERLAP=0 gathers synchronously after each step).  --streams 2 (default)
+    # keeps two independent batches in flight on two HIP streams: one batch's latency-bound low-resolution
+    # stages overlap the other's HBM/MFMA-bound stages (every batch still runs its whole forward)
     from ghost_amd.inference.dp import GatherPipeline
     pipe = GatherPipeline(lambda c, o: G.swap_u8(c, z, out=o), (B, 256, 256, 3), dev,
-                          depth=2 if os.environ.get("GHOST_DP_OVERLAP", "1") != "0" else 1)
+                          depth=2 if os.environ.get("GHOST_DP_OVERLAP", "1") != "0" else 1,
+                          streams=max(1, a.streams))
 
     def step():
         slot = pipe.submit(crops)
@@ -399,16 +404,24 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    iso = {}
     if prof:
         classes["aad_dual_256"] = G.profile_read(names.index("aad_dual_256"))
-        # per-class breakdown from a separate, untimed pass (every kernel class bracketed)
+        # per-class breakdown from a separate, untimed pass with one batch at a time (every kernel class
+        # bracketed; with batches in flight a class's time would include the other batch's kernels)
+        pipe.drain()
+        pipe1 = GatherPipeline(lambda c, o: G.swap_u8(c, z, out=o), (B, 256, 256, 3), dev, depth=pipe.depth,
+                               streams=1)
         G.profile(0xFF)
         for _ in range(a.steps):
-            step()
+            pipe1.submit(crops)
+        pipe1.drain()
         torch.cuda.synchronize()
         for i, n in enumerate(names):
             if n != "aad_dual_256":
                 classes[n] = G.profile_read(i)
+            else:
+                iso = G.profile_read(i)
         G.profile(0)
 
     if rank == 0:
@@ -427,7 +440,7 @@ def main():
                                    + (", RCCL all-gather of swapped crops" if world > 1 else ""),
                        "global_batch": world * B, "per_gpu_batch": B, "backbone": a.backbone,
                        "num_blocks": a.num_blocks, "identities": max(1, a.identities),
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "batches_in_flight": pipe.nstreams},
         }
         if prof and classes["aad_dual_256"]["launches"]:
             c = classes["aad_dual_256"]
@@ -458,6 +471,18 @@ def main():
             if tr:
                 res["roofline"]["physical_gbs"] = round(tr["bytes_per_launch"] / per_launch_s / 1e9, 1)
                 res["roofline"]["physical_frac"] = round(res["roofline"]["physical_gbs"] / HBM_PEAK_GBS, 4)
+            if pipe.nstreams > 1 and iso.get("launches"):
+                # the same kernel with one batch on the GPU (untimed pass): in the timed region it shares the
+                # GPU (HBM, CUs) with the other batch in flight, so its launch there takes longer
+                iso_s = iso["ms"] / iso["launches"] / 1e3
+                res["roofline"]["timed_region_note"] = (f"{pipe.nstreams} batches in flight: the launch duration "
+                                                        "includes sharing the GPU with the other batch's kernels")
+                res["roofline"]["isolated"] = {
+                    "avg_launch_us": round(iso_s * 1e6, 2), "achieved": round(per_launch_min / iso_s / 1e9, 1),
+                    "frac": round(per_launch_min / iso_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "formula_frac": round(per_launch_formula / iso_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "physical_frac": (round(tr["bytes_per_launch"] / iso_s / 1e9 / HBM_PEAK_GBS, 4) if tr else None),
+                    "launches": iso["launches"], "note": "one batch at a time, HIP events on the launch stream"}
             cc = classes["conv3x3_all"]
             if cc["launches"]:
                 tf = cc["flops"] / (cc["ms"] / 1e3) / 1e12
@@ -471,7 +496,8 @@ def main():
                 res["aad_decoder_hbm_frac"] = round(res["aad_decoder_gbs"] / HBM_PEAK_GBS, 4)
             res["kernel_ms_per_step"] = {k: round(v["ms"] / a.steps, 3) for k, v in classes.items()}
             res["kernel_ms_per_step_note"] = ("aad_dual_256 from the timed region; the other classes from an "
-                                              "untimed pass with every class bracketed by HIP events")
+                                              "untimed one-batch-at-a-time pass with every class bracketed by "
+                                              "HIP events")
         legs = [s for s in a.legs.split(",") if s] if world == 1 else []
         if legs:
             res["legs"] = {}

@@ -101,10 +101,25 @@ class GatherPipeline:
     ``batch_shape[0]``, e.g. the last one of a shard) needs ``counts``, the valid-row count of every rank
     for this submit (known to all ranks from ``shard_bounds``); ``result`` then returns only the valid
     rows, rank by rank.  Rows past a rank's count travel as padding and are dropped.
+
+    ``streams`` > 1 keeps that many batches in flight on the GPU: submit k runs its swap (and issues its
+    all-gather) on pipeline-owned stream k % streams, after the caller's stream (where the crops were
+    produced); consecutive batches are independent, so the low-resolution, latency-bound stages of one
+    batch (encoder, 2x2..8x8 blocks) overlap the HBM- and MFMA-bound 64x64..256x256 stages of the other.
+    ``result`` and ``drain`` make the caller's stream wait for the batch's stream.  ``depth`` is rounded up
+    to a multiple of ``streams`` so a slot is always rewritten on the stream that last wrote it.
     """
 
-    def __init__(self, swap: Callable, batch_shape, device, dtype=torch.uint8, group=None, depth: int = 2):
-        self.swap, self.group, self.depth = swap, group, max(1, depth)
+    def __init__(self, swap: Callable, batch_shape, device, dtype=torch.uint8, group=None, depth: int = 2,
+                 streams: int = 1):
+        self.nstreams = max(1, int(streams))
+        depth = max(1, depth)
+        depth = (depth + self.nstreams - 1) // self.nstreams * self.nstreams
+        self.swap, self.group, self.depth = swap, group, depth
+        self.device = torch.device(device)
+        self.streams = ([torch.cuda.Stream(self.device) for _ in range(self.nstreams)]
+                        if self.nstreams > 1 else [None])
+        self.done = [None] * depth             # per slot: event after its swap + all-gather issue (streams > 1)
         dist_on = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if dist_on else 1
         self.rank = dist.get_rank(group) if dist_on else 0
@@ -137,16 +152,25 @@ class GatherPipeline:
             raise ValueError(f"GatherPipeline: counts {counts} do not fit world {self.world}, rank {self.rank} "
                              f"with {n} rows of at most {self.rows}")
         slot = self.k % self.depth
-        self._wait(slot)                      # the collective still reading this slot's buffer
-        if n:
-            self.swap(crops, self.outs[slot][:n])
-        if self.world > 1:
-            if self.nccl:
-                self.pending[slot] = dist.all_gather_into_tensor(self.gath[slot], self.outs[slot], group=self.group,
-                                                                 async_op=True)
-            else:
-                self.pending[slot] = dist.all_gather(list(self.gath[slot].chunk(self.world)), self.outs[slot],
-                                                     group=self.group, async_op=True)
+        st = self.streams[self.k % self.nstreams]
+        if st is not None:
+            st.wait_stream(torch.cuda.current_stream(self.device))   # the crops are ready on the caller's stream
+            crops.record_stream(st)
+        with torch.cuda.stream(st) if st is not None else _nullctx():
+            self._wait(slot)                      # the collective still reading this slot's buffer
+            if n:
+                self.swap(crops, self.outs[slot][:n])
+            if self.world > 1:
+                if self.nccl:
+                    self.pending[slot] = dist.all_gather_into_tensor(self.gath[slot], self.outs[slot],
+                                                                     group=self.group, async_op=True)
+                else:
+                    self.pending[slot] = dist.all_gather(list(self.gath[slot].chunk(self.world)), self.outs[slot],
+                                                         group=self.group, async_op=True)
+            if st is not None:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                self.done[slot] = ev
         self.gen[slot] += 1
         self.k += 1
         return Ticket(slot, self.gen[slot], counts)
@@ -158,6 +182,8 @@ class GatherPipeline:
             raise RuntimeError(f"GatherPipeline: the batch of this ticket was overwritten ({self.gen[ticket.slot] - ticket.gen}"
                                f" later submit(s) reused slot {ticket.slot}; depth {self.depth})")
         self._wait(ticket.slot)
+        if self.done[ticket.slot] is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.done[ticket.slot])
         g = self.gath[ticket.slot]
         if all(c == self.rows for c in ticket.counts):
             return g
@@ -166,3 +192,13 @@ class GatherPipeline:
     def drain(self):
         for s in range(self.depth):
             self._wait(s)
+            if self.done[s] is not None:
+                torch.cuda.current_stream(self.device).wait_event(self.done[s])
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False

@@ -173,3 +173,31 @@ def test_two_stream_plan_is_bit_identical(lib, backbone, nb, B):
     assert torch.equal(res[0][0], res[1][0])
     assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
     assert torch.equal(res[0][2], res[1][2])
+
+
+def test_gather_pipeline_two_batches_in_flight(lib):
+    """dp.GatherPipeline(streams=2) (bench.py's default): consecutive batches swapped on two pipeline streams
+    at once (sharing one AEI_Net handle) give the bytes of one-at-a-time swaps, batch by batch, including a
+    short last batch; results read on the caller's stream after the batch's stream."""
+    from ghost_amd.inference.dp import GatherPipeline
+    G, _ = model("unet", 2, torch.bfloat16)
+    B, nb = 4, 5
+    crops = torch.from_numpy(aei_ref.make_u8_crops(B * nb - 1, 29)).to(DEV)
+    _, z = aei_ref.make_inputs(1, 29)
+    zd = z.to(DEV)
+    ref = [G.swap_u8(crops[i:i + B], zd).clone() for i in range(0, crops.shape[0], B)]
+    pipe = GatherPipeline(lambda c, o: G.swap_u8(c, zd, out=o), (B, 256, 256, 3), DEV, depth=2, streams=2)
+    assert pipe.depth == 2 and pipe.nstreams == 2
+    got = []
+    pending = []
+    for i in range(0, crops.shape[0], B):
+        c = crops[i:i + B]
+        pending.append(pipe.submit(c, counts=[c.shape[0]] if c.shape[0] < B else None))
+        if len(pending) == 2:                  # read batch k once k + 1 is in flight
+            got.append(pipe.result(pending.pop(0)).clone())
+    got += [pipe.result(t).clone() for t in pending]
+    pipe.drain()
+    torch.cuda.synchronize()
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
