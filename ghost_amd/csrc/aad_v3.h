@@ -21,7 +21,17 @@ struct AadV3Desc {
   const float* idgb[2] = {nullptr, nullptr};
   void* out[2] = {nullptr, nullptr};
   int ldo[2] = {0, 0};
+  // tap partials (C = 64 only): a layer with zw[l] set writes, instead of its 64 channels, the 32 fp16
+  // values Z[p][t*3 + o] = sum_c zw[l][t*3 + o][c] * out_c(p) (t = ky*3 + kx, o < 3; rows >= 27 zero)
+  // of the 3x3 conv to 3 channels that is its only consumer (zw: bf16 rows of stride zwld, the narrow
+  // layout's K slice of this layer's channels); out[l] is then that [B*HW][32] fp16 buffer
+  const void* zw[2] = {nullptr, nullptr};
+  int zwld = 0;
 };
+
+// the 3x3 / pad 1 conv to 3 channels from two tap-partial buffers (AADBlk8's output conv over
+// cat(h, x'), AADLayer.py:71,79): y = tanh(sum_t (zh + zx)[p + off_t][t*3 + o]) -> bf16 y (ldy) + BGR uint8
+int tap_sum3x3(const void* zh, const void* zx, int B, int H, int W, void* y, int ldy, uint8_t* u8, hipStream_t s);
 
 bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo);
 int aad_v3(const AadV3Desc& d, hipStream_t s);

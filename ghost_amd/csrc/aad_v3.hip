@@ -36,14 +36,70 @@ struct AadV3Args {
   bf16* out[2];
   int ldo[2];
   int lda, ldh, id_ld, HW, PPW;
+  const bf16* zw[2];   // tap-partial projection rows (ZPM layers), row stride zwld
+  int zwld;
   float slope;
   Up2xSrc up;   // UP: h_in is the bilinear x2 upsample of hin (a [B, up.H, up.W] source)
 };
 
 static constexpr int kWaves = 8;
 
-template <int C, int CA, int L, bool UP, int NWV = kWaves>
+// tap partials of one 16-pixel tile: xf[sh] = the bf16 outputs (channels 32 sh + 8 lq .. +7 of pixel lr, the
+// MFMA B-operand layout), W = the layer's 32 x 64 projection rows in LDS (row stride ZLD); lane ends with
+// Z rows 16 rt + 4 lq .. +3 of pixel lr, stored as fp16 (8 bytes)
+constexpr int ZLD = 72;
+GHOST_DEV void zp_store(const bf16* __restrict__ W, const bf16x8 (&xf)[2], _Float16* __restrict__ zrow, int lr, int lq) {
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&W[(rt * 16 + lr) * ZLD + ks * 32 + lq * 8]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf[ks], acc, 0, 0, 0);
+    }
+    typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+    const f16x4 h = {(_Float16)acc[0], (_Float16)acc[1], (_Float16)acc[2], (_Float16)acc[3]};
+    *reinterpret_cast<f16x4*>(zrow + rt * 16 + lq * 4) = h;
+  }
+}
+
+// the same, one K half at a time (K step ks = the half sh just computed): keeps 8 accumulator registers live
+// instead of both halves' bf16 fragments
+GHOST_DEV void zp_mfma_half(const bf16* __restrict__ W, const bf16x8& xf, int ks, f32x4 (&acc)[2], int lr, int lq) {
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    asm volatile("" ::: "memory");   // the projection rows are re-read per use, not held across the tile loop
+    const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&W[(rt * 16 + lr) * ZLD + ks * 32 + lq * 8]);
+    acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[rt], 0, 0, 0);
+  }
+}
+GHOST_DEV void zp_store_acc(const f32x4 (&acc)[2], _Float16* __restrict__ zrow, int lq) {
+  typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const f16x4 h = {(_Float16)acc[rt][0], (_Float16)acc[rt][1], (_Float16)acc[rt][2], (_Float16)acc[rt][3]};
+    *reinterpret_cast<f16x4*>(zrow + rt * 16 + lq * 4) = h;
+  }
+}
+
+template <int L, int ZPM, int NT>
+GHOST_DEV void zp_stage_weights(const AadV3Args& a, bf16* s_wz, int tid) {
+  if constexpr (ZPM != 0) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      if (!((ZPM >> l) & 1)) continue;
+      for (int idx = tid; idx < 32 * 8; idx += NT) {
+        const int row = idx >> 3, kc = idx & 7;
+        *reinterpret_cast<u32x4*>(&s_wz[(l * 32 + row) * ZLD + kc * 8]) =
+            *reinterpret_cast<const u32x4*>(a.zw[l] + (long)row * a.zwld + kc * 8);
+      }
+    }
+  }
+}
+
+template <int C, int CA, int L, bool UP, int NWV = kWaves, int ZPM = 0>
 GHOST_DEV void aad_v3_body(const AadV3Args& a) {
+  static_assert(ZPM == 0 || C == 64, "tap partials: C = 64");
   constexpr int CT = C / 64;          // 64-channel tiles
   constexpr int KS = CA / 32;         // MFMA k-steps
   constexpr int WLD = CA + 8;         // padded LDS weight row (bf16 elements)
@@ -56,10 +112,12 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
   __shared__ float s_k[L];                                        // sum_c wh * (-mu * rstd)
   __shared__ __attribute__((aligned(16))) float s_gi[L * C];
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
+  __shared__ __attribute__((aligned(16))) bf16 s_wz[ZPM ? L * 32 * ZLD : 8];
 
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
   const long p_begin = (long)blockIdx.x * a.PPW;
   const int b = (int)(p_begin / a.HW);     // PPW divides HW: one sample per workgroup
+  zp_stage_weights<L, ZPM, NWV * 64>(a, s_wz, tid);
 
   // ---- resident weights, biases and per-channel tables ----
   for (int l = 0; l < L; ++l) {
@@ -153,6 +211,7 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       asm volatile("" ::: "memory");   // one layer's accumulators live at a time
+      bf16x8 xf[2];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         const bf16* W = s_w + (l * CT + ct) * 128 * WLD;
@@ -192,18 +251,25 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
             const float v = fmaf(Mk[l], I - A, A);
             o[e] = v > 0.f ? v : v * a.slope;
           }
-          store16_f(a.out[l] + p * a.ldo[l] + c0, o);
+          if (ZPM && ((ZPM >> l) & 1)) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xf[sh][e] = (bf16)o[e];
+          } else {
+            store16_f(a.out[l] + p * a.ldo[l] + c0, o);
+          }
         }
       }
+      if (ZPM && ((ZPM >> l) & 1))
+        zp_store(s_wz + l * 32 * ZLD, xf, reinterpret_cast<_Float16*>(a.out[l]) + p * 32, lr, lq);
     }
   }
 }
 
 // C = 64: held to 4 waves per SIMD (<= 128 VGPRs) so two 512-thread workgroups share a CU;
 // C = 128 keeps the compiler's allocation (forcing it spills)
-template <int C, int CA, int L, bool UP>
+template <int C, int CA, int L, bool UP, int ZPM = 0>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v3_kernel(const AadV3Args a) {
-  aad_v3_body<C, CA, L, UP>(a);
+  aad_v3_body<C, CA, L, UP, kWaves, ZPM>(a);
 }
 template <int C, int CA, int L, bool UP>
 __global__ void __launch_bounds__(512) aad_v3_wide_kernel(const AadV3Args a) {
@@ -238,7 +304,7 @@ struct V4Cfg {
   static constexpr int SLOT_B = ROWS * SPX * 128;  // bytes per wave per slot
 };
 
-template <int CA, int L, bool UP, bool RELU>
+template <int CA, int L, bool UP, bool RELU, int ZPM = 0>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v4_kernel(const AadV3Args a) {
   static_assert(UP, "v4 is the through-upsample form (v3's register loads win without the upsample)");
   using K = V4Cfg<CA, L, UP>;
@@ -253,6 +319,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hA[kWaves * SLOT_B];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hB[kWaves * SLOT_B];
+  __shared__ __attribute__((aligned(16))) bf16 s_wz[ZPM ? L * 32 * ZLD : 8];
 
   // wid through readfirstlane: tile indices and everything derived from them are wave-uniform (SGPRs),
   // so the per-tile address arithmetic runs on the scalar unit and the VALU keeps only lane offsets
@@ -260,6 +327,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
             lq = lane >> 4;
   const long p_begin = (long)blockIdx.x * a.PPW;
   const int b = (int)(p_begin / a.HW);
+  zp_stage_weights<L, ZPM, kWaves * 64>(a, s_wz, tid);
 
   for (int l = 0; l < L; ++l) {
     for (int idx = tid; idx < 128 * (CA / 8); idx += kWaves * 64) {
@@ -402,6 +470,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     for (int l = 0; l < L; ++l) {
       asm volatile("" ::: "memory");
       const bf16* W = s_w + l * 128 * WLD;
+      f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int sh = 0; sh < 2; ++sh) {
         asm volatile("" ::: "memory");
@@ -444,8 +513,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
             o[2 * k + 1] = v.y > 0.f ? v.y : v.y * a.slope;
           }
         }
-        store16_f(a.out[l] + p0 * a.ldo[l] + (lr * a.ldo[l] + c0), o);
+        if (ZPM && ((ZPM >> l) & 1)) {
+          bf16x8 xf;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xf[e] = (bf16)o[e];
+          zp_mfma_half(s_wz + l * 32 * ZLD, xf, sh, zacc, lr, lq);
+        } else {
+          store16_f(a.out[l] + p0 * a.ldo[l] + (lr * a.ldo[l] + c0), o);
+        }
       }
+      if (ZPM && ((ZPM >> l) & 1)) zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + (p0 + lr) * 32, lq);
     }
   };
 
@@ -498,6 +575,16 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   }
   a.lda = d.lda; a.ldh = d.ldh; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
   a.PPW = v3_ppw(d.HW, d.C);
+  int zpm = 0;
+  for (int l = 0; l < d.L; ++l)
+    if (d.zw[l]) {
+      zpm |= 1 << l;
+      a.zw[l] = (const bf16*)d.zw[l];
+    }
+  a.zwld = d.zwld;
+  if (zpm && (d.C != 64 || d.slope != 0.f || d.zwld % 8)) return -1;
+  for (int l = 0; l < d.L; ++l)
+    if (d.zw[l] && (uintptr_t)d.zw[l] % 16) return -1;
   const bool up = d.up_H > 0;
   if (up) {
     if (4 * d.up_H * d.up_W != d.HW || d.up_W * 2 < 16 || (d.C != 64 && d.C != 128)) return -1;
@@ -510,7 +597,7 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   static const unsigned dyn_lds = GHOST_KNOB("GHOST_AAD_DYNLDS", 0u);
   if (use_v4 && up && d.C == 64 && a.PPW % 256 == 0 && d.ldh % 8 == 0) {
 #define GHOST_V4(ca, l, u)                                                                       \
-    if (d.Ca == ca && d.L == l && up == u) {                                                     \
+    if (d.Ca == ca && d.L == l && up == u && !zpm) {                                             \
       if (d.slope == 0.f)                                                                        \
         hipLaunchKernelGGL((aad_v4_kernel<ca, l, u, true>), grid, dim3(kWaves * 64), dyn_lds, s, a); \
       else                                                                                       \
@@ -519,6 +606,25 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
     }
     GHOST_V4(64, 1, true) GHOST_V4(64, 2, true) GHOST_V4(32, 1, true) GHOST_V4(32, 2, true)
 #undef GHOST_V4
+    // AADBlk8's block-input pair with tap partials: layer 1 (last_add_block, nb >= 2) or both (nb = 1)
+#define GHOST_V4Z(ca, zm)                                                                        \
+    if (d.Ca == ca && d.L == 2 && zpm == zm) {                                                   \
+      hipLaunchKernelGGL((aad_v4_kernel<ca, 2, true, true, zm>), grid, dim3(kWaves * 64), 0, s, a); \
+      return (int)hipGetLastError();                                                             \
+    }
+    GHOST_V4Z(64, 1) GHOST_V4Z(64, 2) GHOST_V4Z(64, 3) GHOST_V4Z(32, 1) GHOST_V4Z(32, 2) GHOST_V4Z(32, 3)
+#undef GHOST_V4Z
+  }
+  if (zpm) {   // the non-upsampled forms with tap partials (AADBlk8's last add_block; fuse_upsample off)
+#define GHOST_V3Z(ca, l, zm)                                                                     \
+    if (d.C == 64 && d.Ca == ca && d.L == l && !up && zpm == zm) {                               \
+      hipLaunchKernelGGL((aad_v3_kernel<64, ca, l, false, zm>), grid, dim3(kWaves * 64), 0, s, a); \
+      return (int)hipGetLastError();                                                             \
+    }
+    GHOST_V3Z(64, 1, 1) GHOST_V3Z(32, 1, 1) GHOST_V3Z(64, 2, 1) GHOST_V3Z(32, 2, 1) GHOST_V3Z(64, 2, 2)
+    GHOST_V3Z(32, 2, 2) GHOST_V3Z(64, 2, 3) GHOST_V3Z(32, 2, 3)
+#undef GHOST_V3Z
+    return -1;
   }
 #define GHOST_V3(c, ca, l, u)                                                                   \
   if (d.C == c && d.Ca == ca && d.L == l && up == u) {                                          \
@@ -542,6 +648,78 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
 #undef GHOST_V3W
 #undef GHOST_V3
   return -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// AADBlk8's output conv from the tap partials: an 8 x 32 output tile per workgroup; its 10 x 34 halo of
+// zh + zx (fp16 -> fp32, summed once per halo pixel) in LDS, then one output pixel per thread gathers
+// its nine taps: the gather and epilogue of conv3x3_narrow_kernel (conv_narrow.hip), whose LDS Z the
+// producers now write (tanh; BGR uint8 of faceshifter_run.py:20-21)
+// ---------------------------------------------------------------------------------------------
+namespace {
+constexpr int TS_TH = 16, TS_TW = 32, TS_HW = TS_TW + 2, TS_HP = (TS_TH + 2) * TS_HW, TS_LD = 29;
+constexpr int TS_ITEMS = TS_HP * 4, TS_PER = (TS_ITEMS + 511) / 512;   // (halo pixel, 16-byte chunk) per thread
+}
+
+__global__ void __launch_bounds__(512) tap_sum3x3_kernel(const _Float16* __restrict__ zh, const _Float16* __restrict__ zx,
+                                                         int H, int W, bf16* __restrict__ y, int ldy,
+                                                         uint8_t* __restrict__ u8) {
+  __shared__ float Z[TS_HP * TS_LD];
+  const int tid = threadIdx.x;
+  const int tiles_x = W / TS_TW, tiles_y = H / TS_TH;
+  const int b = blockIdx.x / (tiles_x * tiles_y);
+  const int r = blockIdx.x - b * tiles_x * tiles_y;
+  const int y0 = (r / tiles_x) * TS_TH, x0 = (r % tiles_x) * TS_TW;
+  const long img = (long)b * H * W;
+  typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+  // halo pixel p, 16-byte chunk j (Z values 8j .. 8j+7; chunk 3 holds 24..31, of which 24..26 are used):
+  // every load of the thread issued before the first is used
+  f16x8 va[TS_PER], vc[TS_PER];
+#pragma unroll
+  for (int u = 0; u < TS_PER; ++u) {
+    const int i = tid + u * 512;
+    const int p = i >> 2, j = i & 3;
+    const int hy = p / TS_HW, hx = p - hy * TS_HW;
+    const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+    const bool ok = i < TS_ITEMS && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    const long q = (img + (long)(ok ? iy : 0) * W + (ok ? ix : 0)) * 32 + j * 8;
+    va[u] = ok ? *reinterpret_cast<const f16x8*>(zh + q) : f16x8{};
+    vc[u] = ok ? *reinterpret_cast<const f16x8*>(zx + q) : f16x8{};
+  }
+#pragma unroll
+  for (int u = 0; u < TS_PER; ++u) {
+    const int i = tid + u * 512;
+    if (i >= TS_ITEMS) break;
+    const int p = i >> 2, j = i & 3;
+    const int ne = j == 3 ? 3 : 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (e < ne) Z[p * TS_LD + j * 8 + e] = (float)va[u][e] + (float)vc[u][e];
+  }
+  __syncthreads();
+  const int oy = tid / TS_TW, ox = tid - oy * TS_TW;
+  const long q = img + (long)(y0 + oy) * W + (x0 + ox);
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    float s = 0.f;
+#pragma unroll
+    for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx) s += Z[((oy + ty) * TS_HW + ox + tx) * TS_LD + (ty * 3 + tx) * 3 + o];
+    s = tanhf(s);
+    y[q * ldy + o] = (bf16)s;
+    if (u8) {
+      const float t = (s * 0.5f + 0.5f) * 255.0f;   // faceshifter_run.py:20-21
+      u8[q * 3 + (2 - o)] = (uint8_t)(int)t;
+    }
+  }
+}
+
+int tap_sum3x3(const void* zh, const void* zx, int B, int H, int W, void* y, int ldy, uint8_t* u8, hipStream_t s) {
+  if (H % TS_TH || W % TS_TW || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16) return -1;
+  hipLaunchKernelGGL(tap_sum3x3_kernel, dim3((unsigned)(B * (H / TS_TH) * (W / TS_TW))), dim3(512), 0, s,
+                     (const _Float16*)zh, (const _Float16*)zx, H, W, (bf16*)y, ldy, u8);
+  return (int)hipGetLastError();
 }
 
 }  // namespace ghost

@@ -69,7 +69,7 @@ struct ghost_aei {
   std::map<std::string, const void*> slots;   // name -> device pointer (nullptr = unbound)
   int id_total = 0;                            // sum over AAD layers of 2*c_x
   // per-handle plan options (ghost_aei_set_option); defaults are the measured choices
-  int opt[GHOST_AEI_NOPT] = {1, 1, 1};
+  int opt[GHOST_AEI_NOPT] = {1, 1, 1, GHOST_KNOB("GHOST_AAD_ZP", 2)};
   // GHOST_AEI_OPT_TWO_STREAMS: the encoder up path's stream and its events (created on first use, on the
   // device current then): zev[k] = z_attr_k written (k = 2..8), zev[0] = the down path done
   hipStream_t s_up = nullptr;
@@ -462,6 +462,8 @@ struct AadOut {
   int id_off;
   void* out;
   int ldo;
+  const void* zw = nullptr;   // tap partials (aad_v3.h): out is then the [P][32] fp16 partial buffer
+  int zwld = 0;
 };
 
 // AADLayers that read the same h_in / z_attr: the register-epilogue kernel takes up to two at
@@ -543,6 +545,8 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
       d.idgb[l] = idgb ? idgb + o.id_off : nullptr;
       d.out[l] = o.out;
       d.ldo[l] = o.ldo;
+      d.zw[l] = o.zw;
+      if (o.zw) d.zwld = o.zwld;
     }
     if (!c.ok() || c.dry) continue;
     const double Pn = (double)B * n * n;
@@ -678,19 +682,44 @@ void generator(Ctx& c, int B, const void* const attr[8], GenIn gin, void* y_out,
       run_stats(c, m, cin, B, n * n, cin, stat_m);
     void* y = last_k ? y_out : c.alloc(P * cout * es);
     // x-branch and h'-branch share the output conv: conv(cat(a_x, a_h), [W_x | W_h]) = x + h'
-    void* cat = split ? c.alloc(P * 2 * cin * es) : nullptr;
+    // AADBlk8 (cout = 3) with tap partials (GHOST_AEI_OPT_TAP_PARTIALS): the AADLayers feeding that conv write
+    // its per-tap partial sums instead of their channels (zh: the h path, zx: last_add_block's x')
+    const int zp = (last_k && split && cin == 64 && cout == 3 && h->dt == GHOST_BF16)
+                       ? h->opt[GHOST_AEI_OPT_TAP_PARTIALS] : 0;
+    const bf16* wn = zp ? (const bf16*)c.W(blk + ".conv" + std::to_string(nb - 1) + ".wn") : nullptr;
+    const int wnld = rup(2 * cin, 32);
+    void* zh = zp ? c.alloc(P * 32 * 2) : nullptr;
+    void* zx = zp == 2 ? c.alloc(P * 32 * 2) : nullptr;
+    void* xq = zp == 1 ? c.alloc(P * cin * es) : nullptr;   // x' alone (the narrow conv contracts it)
+    void* cat = (split && !zp) ? c.alloc(P * 2 * cin * es) : nullptr;
     const void* x = m;
     const float* stat_x = stat_m;
     for (int i = 0; i < nb; ++i) {
       const bool last = i == nb - 1;
       const std::string cn = blk + ".conv" + std::to_string(i) + ".w";
       std::vector<AadOut> group;
-      void* a = (last && split) ? cat : c.alloc(P * cin * es);
-      const int lda_out = (last && split) ? 2 * cin : cin;
-      group.push_back({blk + ".aad" + std::to_string(i), base + 2 * cin * i, a, lda_out});
-      if (i == 0 && split)   // last_add_block's AADLayer reads the block input m as well
-        group.push_back({blk + ".aadlast", base + 2 * cin * nb, (char*)cat + (size_t)cin * es, 2 * cin});
+      if (zp && last) {
+        AadOut o{blk + ".aad" + std::to_string(i), base + 2 * cin * i, zh, 32};
+        o.zw = wn; o.zwld = wnld;
+        group.push_back(o);
+      } else {
+        void* a = (last && split) ? cat : c.alloc(P * cin * es);
+        const int lda_out = (last && split) ? 2 * cin : cin;
+        group.push_back({blk + ".aad" + std::to_string(i), base + 2 * cin * i, a, lda_out});
+      }
+      if (i == 0 && split) {   // last_add_block's AADLayer reads the block input m as well
+        if (zp == 2) {
+          AadOut o{blk + ".aadlast", base + 2 * cin * nb, zx, 32};
+          o.zw = wn + cin; o.zwld = wnld;
+          group.push_back(o);
+        } else if (zp == 1) {
+          group.push_back({blk + ".aadlast", base + 2 * cin * nb, xq, cin});
+        } else {
+          group.push_back({blk + ".aadlast", base + 2 * cin * nb, (char*)cat + (size_t)cin * es, 2 * cin});
+        }
+      }
       aad_group(c, group, x, cin, stat_x, za, Ca, Ca, B, n, cin, idgb, i == 0 && m_virtual, small ? gmask : nullptr);
+      void* a = group[0].out;
       if (!last) {
         void* xn = c.alloc(P * cin * es);
         float* st = (float*)c.alloc((size_t)B * cin * 2 * sizeof(float));
@@ -706,6 +735,20 @@ void generator(Ctx& c, int B, const void* const attr[8], GenIn gin, void* y_out,
         stat_x = st;
       } else if (!split) {
         conv3x3(c, cn, a, cin, cin, B, n, cout, y, cout, m, cin, last_k, last_k ? u8 : nullptr);
+      } else if (zp == 2) {
+        if (c.ok() && !c.dry) {
+          int e_all = c.prof_begin(2);
+          c.check(tap_sum3x3(zh, zx, B, n, n, y, cout, u8, c.s), "tap_sum3x3");
+          c.prof_end(2, e_all, 0, 0);
+        }
+      } else if (zp == 1) {
+        if (c.ok() && !c.dry) {
+          int e_all = c.prof_begin(2);
+          c.check(conv3x3_narrow(h->dt, xq, B, n, n, cin, cin, wn + cin, wnld, cout, nullptr, 0, 1, y, cout, u8, c.s,
+                                 zh),
+                  "conv3x3_narrow + tap partials");
+          c.prof_end(2, e_all, 0, 2.0 * P * cout * 9.0 * cin);
+        }
       } else {
         conv3x3(c, cn, cat, 2 * cin, 2 * cin, B, n, cout, y, cout, nullptr, 0, last_k, last_k ? u8 : nullptr);
       }
@@ -1078,7 +1121,8 @@ extern "C" int ghost_aei_profile_read(ghost_aei* h, int cls, double* ms, int64_t
 extern "C" int ghost_aei_set_option(ghost_aei* h, int option, int value) {
   if (!h) return fail(GHOST_EINVAL, "null handle");
   if (option < 0 || option >= GHOST_AEI_NOPT) return fail(GHOST_EINVAL, "unknown option");
-  if (value != 0 && value != 1) return fail(GHOST_EINVAL, "option value must be 0 or 1");
+  const int vmax = option == GHOST_AEI_OPT_TAP_PARTIALS ? 2 : 1;
+  if (value < 0 || value > vmax) return fail(GHOST_EINVAL, "option value out of range");
   h->opt[option] = value;
   return 0;
 }

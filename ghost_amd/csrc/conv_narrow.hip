@@ -26,6 +26,7 @@ struct NarrowArgs {
   const void* res;
   void* y;
   uint8_t* u8;
+  const _Float16* zadd;   // optional [B*H*W][32] fp16 tap partials of other input channels, added to Z
   int H, W, Cin, ldx, Kpad, ldy, ldres, NO, tanh_out;
 };
 
@@ -127,6 +128,19 @@ __global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const NarrowArgs a)
     }
   }
   __syncthreads();
+  if (a.zadd) {   // tap partials of the channels a producer already contracted (AADBlk8's h path, aad_v3.h)
+    for (int i = tid; i < HP * 4; i += 256) {
+      const int p = i >> 2, j = i & 3;
+      const int hy = p / HW_, hx = p - hy * HW_;
+      const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
+      if (iy < 0 || iy >= a.H || ix < 0 || ix >= a.W) continue;
+      typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+      const f16x8 z = *reinterpret_cast<const f16x8*>(a.zadd + (img + (long)iy * a.W + ix) * 32 + j * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Z[p * ZLD + j * 8 + e] += (float)z[e];
+    }
+    __syncthreads();
+  }
 
   // gather: one output pixel per thread
   const int oy = tid / TW, ox = tid - oy * TW;
@@ -153,9 +167,11 @@ bool conv3x3_narrow_supported(int dt, int H, int W, int Cin, int ldx, int NO) {
 }
 
 int conv3x3_narrow(int dt, const void* x, int B, int H, int W, int Cin, int ldx, const void* w_narrow, int Kpad, int NO,
-                   const void* res, int ldres, int tanh_out, void* y, int ldy, uint8_t* u8, hipStream_t s) {
+                   const void* res, int ldres, int tanh_out, void* y, int ldy, uint8_t* u8, hipStream_t s,
+                   const void* zadd) {
   if (!conv3x3_narrow_supported(dt, H, W, Cin, ldx, NO) || (uintptr_t)x % 16 || (uintptr_t)w_narrow % 16) return -1;
-  NarrowArgs a{x, w_narrow, res, y, u8, H, W, Cin, ldx, Kpad, ldy, ldres, NO, tanh_out};
+  if (zadd && (uintptr_t)zadd % 16) return -1;
+  NarrowArgs a{x, w_narrow, res, y, u8, (const _Float16*)zadd, H, W, Cin, ldx, Kpad, ldy, ldres, NO, tanh_out};
   dim3 grid((unsigned)(B * (H / TH) * (W / TW)));
   if (dt == GHOST_BF16 && Cin == 128)
     hipLaunchKernelGGL((conv3x3_narrow_kernel<bf16, 128>), grid, dim3(256), 0, s, a);

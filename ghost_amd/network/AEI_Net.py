@@ -128,7 +128,7 @@ class AADGenerator(nn.Module):
 
 
 # per-handle plan options (include/ghost_amd.h GHOST_AEI_OPT_*)
-OPTIONS = {"fuse_upsample": 0, "fuse_stats": 1, "two_streams": 2}
+OPTIONS = {"fuse_upsample": 0, "fuse_stats": 1, "two_streams": 2, "tap_partials": 3}
 
 
 class _Runtime:
@@ -197,7 +197,8 @@ class AEI_Net(nn.Module):
         return rt.dtype
 
     def set_option(self, name: str, value: int) -> None:
-        """Per-model plan option (include/ghost_amd.h): fuse_upsample, fuse_stats, two_streams (0 / 1)."""
+        """Per-model plan option (include/ghost_amd.h): fuse_upsample, fuse_stats, two_streams (0 / 1),
+        tap_partials (0 / 1 / 2)."""
         if name not in OPTIONS:
             raise ValueError(f"ghost_amd: unknown option {name!r} (known: {sorted(OPTIONS)})")
         self._options[name] = int(value)

@@ -87,8 +87,23 @@ int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_str
  *                                    the generator's AADBlk k, which waits only for z_attr_k; the caller's
  *                                    stream waits for that stream before the call's last launch, so the
  *                                    ordering seen by the caller is unchanged (0: one stream).  Same results.
- * value is 0 or 1.  A handle is not shared across threads without external synchronisation. */
-enum { GHOST_AEI_OPT_FUSE_UPSAMPLE = 0, GHOST_AEI_OPT_FUSE_STATS = 1, GHOST_AEI_OPT_TWO_STREAMS = 2, GHOST_AEI_NOPT = 3 };
+ *   GHOST_AEI_OPT_TAP_PARTIALS (2):  bf16, C = 64 output block (AADBlk8): the 3x3 conv to 3 channels is
+ *                                    contracted in its producers: each AADLayer that feeds it writes the 27
+ *                                    per-tap partial sums of its channels (fp16, 32 per pixel) instead of its
+ *                                    64 bf16 channels, and a gather kernel sums the nine taps (+ tanh, uint8).
+ *                                    2: both the h path and last_add_block's x'; 1: the h path only (x' is
+ *                                    written and the narrow conv contracts it); 0: neither.  The partials
+ *                                    are rounded to fp16 once (the extra rounding the bf16-storage
+ *                                    emulation of oracle/aei_ref.py models).
+ * value is 0 or 1 (TAP_PARTIALS: 0..2).  A handle is not shared across threads without external
+ * synchronisation. */
+enum {
+  GHOST_AEI_OPT_FUSE_UPSAMPLE = 0,
+  GHOST_AEI_OPT_FUSE_STATS = 1,
+  GHOST_AEI_OPT_TWO_STREAMS = 2,
+  GHOST_AEI_OPT_TAP_PARTIALS = 3,
+  GHOST_AEI_NOPT = 4
+};
 int ghost_aei_set_option(ghost_aei* h, int option, int value);
 int ghost_aei_get_option(ghost_aei* h, int option, int* value);
 /* Diagnostic taps (parity bisection): while set, every forward / swap of the handle copies the stored

@@ -325,6 +325,10 @@ def aei_forward(p, xt, z_id, backbone="unet", num_blocks=2, dtype=torch.float32)
 # statistics of an upsample in closed form over its source (source side >= 32, C % 64 == 0:
 # ops.hip in_stats_up2x_closed_form), which are the statistics of the fp32 upsample.
 _STORE = [torch.bfloat16]     # storage dtype of the emulation (float32: rounding off, for self-checks)
+# GHOST_AEI_OPT_TAP_PARTIALS of the runtime being emulated (include/ghost_amd.h): AADBlk8's 3x3 conv to 3
+# channels contracted per tap in its producers, each tap's partial sum stored in fp16 (2: the h path and
+# last_add_block's x', 1: the h path only, 0: neither)
+_TAP_PARTIALS = [2]
 
 
 def _q(t: torch.Tensor) -> torch.Tensor:
@@ -413,6 +417,21 @@ def up1_bf16_storage(z_id, p):
                                  p["generator.up1.bias"].float()))
 
 
+def _tap_conv3x3(a, w, round16):
+    """conv2d(a, w, padding=1) for 3 output channels as the runtime's tap-partial path computes it: per tap
+    (ky, kx) the partial sum Z_t = sum_c w[:, c, ky, kx] * a_c at every source pixel (fp32 over bf16
+    operands), stored in fp16 when round16, then out[q] = sum_t Z_t[q + (ky - 1, kx - 1)] (zero outside)."""
+    H, W = a.shape[-2:]
+    out = torch.zeros(a.shape[0], w.shape[0], H, W)
+    for ky in range(3):
+        for kx in range(3):
+            zt = torch.einsum("bchw,oc->bohw", a, w[:, :, ky, kx])
+            if round16:
+                zt = zt.half().float()
+            out = out + F.pad(zt, (1, 1, 1, 1))[:, :, ky:ky + H, kx:kx + W]
+    return out
+
+
 def gen_block_bf16_storage(y_prev, za, z_id, p, backbone, num_blocks, k):
     """AADBlk_k (AAD_ResBlk.forward, AADLayer.py:74-80) from the *stored* previous block output
     (k = 1: m1 from up1_bf16_storage), including the x2 upsample in front of it (AEI_Net.py:125-137).
@@ -429,15 +448,19 @@ def gen_block_bf16_storage(y_prev, za, z_id, p, backbone, num_blocks, k):
         m_stats = _in_stats(u) if (y_prev.shape[-1] >= 32 and cin % 64 == 0) else None
     pre = f"generator.AADBlk{k}"
     x, st = m, m_stats
+    zp = _TAP_PARTIALS[0] if (k == 8 and cin != cout and cin == 64 and cout == 3
+                              and _STORE[0] == torch.bfloat16) else 0
     for i in range(num_blocks):
         a = aad_layer_bf16_storage(x, za, z_id, p, f"{pre}.add_blocks.{3 * i}", st)
-        x = F.conv2d(a, _wq(p, f"{pre}.add_blocks.{3 * i + 2}.weight"), None, padding=1)
+        wc = _wq(p, f"{pre}.add_blocks.{3 * i + 2}.weight")
+        x = _tap_conv3x3(a, wc, True) if (zp and i == num_blocks - 1) else F.conv2d(a, wc, None, padding=1)
         st = None
         if i < num_blocks - 1:
             x = _q(x)
     if cin != cout:
         a = aad_layer_bf16_storage(m, za, z_id, p, f"{pre}.last_add_block.0", m_stats)
-        y = x + F.conv2d(a, _wq(p, f"{pre}.last_add_block.2.weight"), None, padding=1)
+        wl = _wq(p, f"{pre}.last_add_block.2.weight")
+        y = x + (_tap_conv3x3(a, wl, zp == 2) if zp else F.conv2d(a, wl, None, padding=1))
     else:
         y = x + m
     return y if k == 8 else _q(y)
@@ -455,12 +478,14 @@ def generator_bf16_storage(z_attr, z_id, p, backbone="unet", num_blocks=2):
 
 
 @torch.no_grad()
-def aei_forward_bf16_storage(p, xt, z_id, backbone="unet", num_blocks=2, store=torch.bfloat16):
+def aei_forward_bf16_storage(p, xt, z_id, backbone="unet", num_blocks=2, store=torch.bfloat16, tap_partials=2):
     """AEI_Net.forward (AEI_Net.py:153-156) as the bf16 runtime stores it -> (Y, attr, blocks, y_u8_src).
 
     Y is the bf16-rounded tanh output, attr the stored encoder maps, blocks the stored AADBlk1..7
-    outputs (+ AADBlk8's pre-tanh sum), and y_u8_src the fp32 tanh the uint8 frame is made from."""
+    outputs (+ AADBlk8's pre-tanh sum), and y_u8_src the fp32 tanh the uint8 frame is made from.
+    tap_partials: the runtime's GHOST_AEI_OPT_TAP_PARTIALS (fp16 per-tap partials of AADBlk8's output conv)."""
     prev, _STORE[0] = _STORE[0], store
+    prev_tp, _TAP_PARTIALS[0] = _TAP_PARTIALS[0], tap_partials
     try:
         xt = _q(xt.float())
         attr = encoder_bf16_storage(xt, p, backbone)
@@ -468,6 +493,7 @@ def aei_forward_bf16_storage(p, xt, z_id, backbone="unet", num_blocks=2, store=t
         return _q(t), attr, blocks, t
     finally:
         _STORE[0] = prev
+        _TAP_PARTIALS[0] = prev_tp
 
 
 def fp16_reference_forward(p, xt, z_id, backbone="unet", num_blocks=2):
