@@ -483,11 +483,19 @@ def main():
             ca8 = 32 if a.backbone == "linknet" else 64     # z_attr8 channels (AEI_Net.py:110,118)
             # layers in the kernel: the formula bytes per launch are L * B*256^2*(2*64 + Ca)*2
             nl = max(1, round(per_launch_formula / (B * 65536 * (2 * 64 + ca8) * 2)))
-            # minimum bytes of the fused kernel: h_in's 128x128 source once, z_attr8 once, nl outputs
-            per_launch_min = B * (128 * 128 * 64 + 65536 * ca8 + nl * 65536 * 64) * 2.0
+            # minimum bytes of the fused kernel: h_in's 128x128 source once, z_attr8 once, nl outputs; an output
+            # whose layer feeds AADBlk8's conv to 3 channels through tap partials (GHOST_AEI_OPT_TAP_PARTIALS) is
+            # 32 fp16 partial sums per pixel instead of 64 bf16 channels: nb >= 2 -> last_add_block's layer (mode
+            # 2); nb = 1 -> the h path's layer (modes 1, 2) and last_add_block's (mode 2)
+            zp = G.get_option("tap_partials") if a.dtype == "bf16" else 0
+            n_part = min(nl, (1 if zp == 2 else 0) if a.num_blocks >= 2 else zp)
+            per_launch_min = B * (128 * 128 * 64 + 65536 * ca8 + (nl - n_part) * 65536 * 64
+                                  + n_part * 65536 * 32) * 2.0
             ach = per_launch_min / per_launch_s / 1e9
-            kname = f"aad_v4_kernel<{ca8}, {nl}, true>"
-            kmatch = f"aad_v4_kernel<{ca8}, {nl}, true"   # the PMC summary's names carry the ReLU flag too
+            kname = f"aad_v4_kernel<{ca8}, {nl}, true>" + (f" ({n_part} layer(s) writing tap partials)" if n_part else "")
+            # the PMC summary's names carry the ReLU flag and the tap-partial layer mask (ZPM) too
+            zpm = (2 if zp == 2 else 0) if a.num_blocks >= 2 else {0: 0, 1: 1, 2: 3}.get(zp, 0)
+            kmatch = f"aad_v4_kernel<{ca8}, {nl}, true, true, {zpm}>"
             res["roofline"] = {"kernel": f"{kname}: AADBlk8's block-input AAD kernel at 256x256, {nl} AADLayer(s) "
                                          "sharing h_in/z_attr, h_in = bilinear x2 of the 128x128 block output "
                                          "sampled in-kernel (IN-normalise, sigmoid mask, MFMA gamma/beta, blend, "
@@ -496,7 +504,8 @@ def main():
                                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kmatch),
                                "bytes_per_launch": per_launch_min,
                                "bytes_note": "achieved = minimum bytes of the fused kernel (128x128 h_in source + "
-                                             "z_attr8 + outputs) / launch time; formula_* = SURVEY.md 8d's per-layer "
+                                             "z_attr8 + outputs as stored: 64 bf16 channels, or 32 fp16 tap partials "
+                                             "per pixel) / launch time; formula_* = SURVEY.md 8d's per-layer "
                                              "|h_in|+|z_attr|+|out| with h_in counted at 256x256 per layer",
                                "formula_bytes_per_launch": per_launch_formula,
                                "formula_gbs": round(per_launch_formula / per_launch_s / 1e9, 1),

@@ -45,16 +45,32 @@ struct AadV3Args {
 static constexpr int kWaves = 8;
 
 // tap partials of one 16-pixel tile: xf[sh] = the bf16 outputs (channels 32 sh + 8 lq .. +7 of pixel lr, the
-// MFMA B-operand layout), W = the layer's 32 x 64 projection rows in LDS (row stride ZLD); lane ends with
-// Z rows 16 rt + 4 lq .. +3 of pixel lr, stored as fp16 (8 bytes)
-constexpr int ZLD = 72;
+// MFMA B-operand layout), W = the layer's 32 x 64 projection rows in LDS (64-element rows, see zw_idx); lane
+// ends with Z rows 16 rt + 4 lq .. +3 of pixel lr, stored as fp16 (8 bytes)
+constexpr int ZLD = 64;
+// element offset of (row, k) in an unpadded image of 64-element (128-byte) rows with the 16-byte chunks XOR-
+// swizzled by row & 7: the ds_read_b128 of rows 16 rt + lr, chunk 4 ks + lq is conflict-free in every 16-lane
+// group (the +8-element padding it replaces was 2-way in half the groups and cost 1 KB per 64 rows)
+GHOST_DEV int sw64(int row, int k) { return row * 64 + ((((k >> 3) ^ (row & 7)) << 3) | (k & 7)); }
+// the same for 32-element (64-byte) rows: chunks XOR-swizzled by (row >> 1) & 3
+GHOST_DEV int sw32(int row, int k) { return row * 32 + ((((k >> 3) ^ ((row >> 1) & 3)) << 3) | (k & 7)); }
+template <int CA>
+GHOST_DEV int swca(int row, int k) {
+  if constexpr (CA == 64) return sw64(row, k);
+  else return sw32(row, k);
+}
+// LDS slot of layer l's projection rows: only the layers in ZPM are staged
+template <int ZPM>
+GHOST_DEV constexpr int zp_slot(int l) { return l == 0 ? 0 : (ZPM & 1); }
+template <int ZPM>
+constexpr int zp_nlayers() { return (ZPM & 1) + ((ZPM >> 1) & 1); }
 GHOST_DEV void zp_store(const bf16* __restrict__ W, const bf16x8 (&xf)[2], _Float16* __restrict__ zrow, int lr, int lq) {
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&W[(rt * 16 + lr) * ZLD + ks * 32 + lq * 8]);
+      const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&W[sw64(rt * 16 + lr, ks * 32 + lq * 8)]);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf[ks], acc, 0, 0, 0);
     }
     typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
@@ -69,7 +85,7 @@ GHOST_DEV void zp_mfma_half(const bf16* __restrict__ W, const bf16x8& xf, int ks
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     asm volatile("" ::: "memory");   // the projection rows are re-read per use, not held across the tile loop
-    const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&W[(rt * 16 + lr) * ZLD + ks * 32 + lq * 8]);
+    const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&W[sw64(rt * 16 + lr, ks * 32 + lq * 8)]);
     acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[rt], 0, 0, 0);
   }
 }
@@ -90,7 +106,7 @@ GHOST_DEV void zp_stage_weights(const AadV3Args& a, bf16* s_wz, int tid) {
       if (!((ZPM >> l) & 1)) continue;
       for (int idx = tid; idx < 32 * 8; idx += NT) {
         const int row = idx >> 3, kc = idx & 7;
-        *reinterpret_cast<u32x4*>(&s_wz[(l * 32 + row) * ZLD + kc * 8]) =
+        *reinterpret_cast<u32x4*>(&s_wz[sw64(zp_slot<ZPM>(l) * 32 + row, kc * 8)]) =
             *reinterpret_cast<const u32x4*>(a.zw[l] + (long)row * a.zwld + kc * 8);
       }
     }
@@ -112,7 +128,7 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
   __shared__ float s_k[L];                                        // sum_c wh * (-mu * rstd)
   __shared__ __attribute__((aligned(16))) float s_gi[L * C];
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
-  __shared__ __attribute__((aligned(16))) bf16 s_wz[ZPM ? L * 32 * ZLD : 8];
+  __shared__ __attribute__((aligned(16))) bf16 s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
 
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
   const long p_begin = (long)blockIdx.x * a.PPW;
@@ -260,7 +276,7 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
         }
       }
       if (ZPM && ((ZPM >> l) & 1))
-        zp_store(s_wz + l * 32 * ZLD, xf, reinterpret_cast<_Float16*>(a.out[l]) + p * 32, lr, lq);
+        zp_store(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, reinterpret_cast<_Float16*>(a.out[l]) + p * 32, lr, lq);
     }
   }
 }
@@ -298,7 +314,7 @@ __global__ void __launch_bounds__(512) aad_v3_wide_kernel(const AadV3Args a) {
 // ---------------------------------------------------------------------------------------------
 template <int CA, int L, bool UP>
 struct V4Cfg {
-  static constexpr int C = 64, KS = CA / 32, WLD = CA + 8, NH = 2;
+  static constexpr int C = 64, KS = CA / 32, NH = 2;
   static constexpr int SPX = UP ? 10 : 16;        // h pixels per row held in a slot
   static constexpr int ROWS = UP ? 2 : 1;
   static constexpr int SLOT_B = ROWS * SPX * 128;  // bytes per wave per slot
@@ -308,7 +324,12 @@ template <int CA, int L, bool UP, bool RELU, int ZPM = 0>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v4_kernel(const AadV3Args a) {
   static_assert(UP, "v4 is the through-upsample form (v3's register loads win without the upsample)");
   using K = V4Cfg<CA, L, UP>;
-  constexpr int C = 64, KS = K::KS, WLD = K::WLD, SPX = K::SPX, SLOT_B = K::SLOT_B;
+  constexpr int C = 64, KS = K::KS, SPX = K::SPX, SLOT_B = K::SLOT_B;
+  // weight rows: with tap partials unpadded + XOR-swizzled (swca; keeps the kernel within 80 KB of LDS, two
+  // workgroups per CU, next to the projection rows), without them padded by 8 elements (the swizzle's address
+  // arithmetic spills the ZPM = 0 form at 128 VGPRs)
+  constexpr int WLD = ZPM ? CA : CA + 8;
+  auto widx = [](int row, int k) { return ZPM ? swca<CA>(row, k) : row * (CA + 8) + k; };
   __shared__ __attribute__((aligned(16))) bf16 s_w[L * 128 * WLD];
   __shared__ __attribute__((aligned(16))) float s_b[L * 128];
   __shared__ __attribute__((aligned(16))) float s_rs[C];
@@ -319,7 +340,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hA[kWaves * SLOT_B];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hB[kWaves * SLOT_B];
-  __shared__ __attribute__((aligned(16))) bf16 s_wz[ZPM ? L * 32 * ZLD : 8];
+  __shared__ __attribute__((aligned(16))) bf16 s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
 
   // wid through readfirstlane: tile indices and everything derived from them are wave-uniform (SGPRs),
   // so the per-tile address arithmetic runs on the scalar unit and the VALU keeps only lane offsets
@@ -332,7 +353,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   for (int l = 0; l < L; ++l) {
     for (int idx = tid; idx < 128 * (CA / 8); idx += kWaves * 64) {
       const int row = idx / (CA / 8), kc = idx - row * (CA / 8);
-      *reinterpret_cast<u32x4*>(&s_w[(l * 128 + row) * WLD + kc * 8]) =
+      *reinterpret_cast<u32x4*>(&s_w[widx(l * 128 + row, kc * 8)]) =
           *reinterpret_cast<const u32x4*>(a.w3[l] + (long)row * CA + kc * 8);
     }
     for (int idx = tid; idx < 128; idx += kWaves * 64) s_b[l * 128 + idx] = a.b3[l][idx];
@@ -487,7 +508,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
-            const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&W[(rt * 16 + lr) * WLD + ks * 32 + lq * 8]);
+            const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&W[widx(rt * 16 + lr, ks * 32 + lq * 8)]);
             acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i], 0, 0, 0);
           }
         }
@@ -517,7 +538,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
           bf16x8 xf;
 #pragma unroll
           for (int e = 0; e < 8; ++e) xf[e] = (bf16)o[e];
-          zp_mfma_half(s_wz + l * 32 * ZLD, xf, sh, zacc, lr, lq);
+          zp_mfma_half(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, sh, zacc, lr, lq);
         } else {
           store16_f(a.out[l] + p0 * a.ldo[l] + (lr * a.ldo[l] + c0), o);
         }

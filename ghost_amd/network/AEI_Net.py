@@ -205,6 +205,18 @@ class AEI_Net(nn.Module):
         if self._rt is not None:
             _lib.check(self._rt.lib.ghost_aei_set_option(self._rt.h, OPTIONS[name], int(value)), f"option {name}")
 
+    def get_option(self, name: str) -> int:
+        """The plan option's value in effect (the handle's, once a forward has created it)."""
+        if name not in OPTIONS:
+            raise ValueError(f"ghost_amd: unknown option {name!r} (known: {sorted(OPTIONS)})")
+        if self._rt is not None:
+            v = C.c_int()
+            _lib.check(self._rt.lib.ghost_aei_get_option(self._rt.h, OPTIONS[name], C.byref(v)), f"option {name}")
+            return int(v.value)
+        if name in self._options:
+            return self._options[name]
+        raise RuntimeError("ghost_amd: option defaults live in the native handle; run a forward first")
+
     def _runtime(self, device) -> _Runtime:
         dt = self._dtype()
         sig = (device, dt) + tuple((t.data_ptr(), t._version) for t in self.state_dict().values())

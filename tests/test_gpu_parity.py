@@ -738,3 +738,18 @@ def test_boundary_rejects_bad_out_and_host_embeddings(lib):
             G.swap_u8(crops, z[:1].to(DEV), out=bad)
     with pytest.raises(RuntimeError, match="z_id"):
         G(torch.zeros(2, 3, 256, 256, device=DEV), z)
+
+
+def test_plan_options_read_back_from_the_handle(lib):
+    """get_option reads the native handle: the measured defaults (include/ghost_amd.h) after the first
+    forward, and what set_option wrote afterwards (bench.py sizes the roofline kernel's bytes from it)."""
+    G = model("unet", 2, compute_dtype=torch.bfloat16)
+    xt, z = aei_ref.make_inputs(1, 3)
+    G(xt.to(DEV), z.to(DEV))
+    assert {n: G.get_option(n) for n in ("fuse_upsample", "fuse_stats", "two_streams", "tap_partials")} == \
+        {"fuse_upsample": 1, "fuse_stats": 1, "two_streams": 1, "tap_partials": 2}
+    G.set_option("tap_partials", 1)
+    assert G.get_option("tap_partials") == 1
+    G.set_option("tap_partials", 2)
+    with pytest.raises(ValueError):
+        G.get_option("no_such_option")
