@@ -117,10 +117,11 @@ __global__ void up2x_weights_kernel(const Up2xSrc u, float* __restrict__ wt, int
 
 // a workgroup: RB source rows x CPB = 512 / RB source columns of one sample (CPB = min(W, 128)),
 // 64 channels; lane (cc, q): channel chunk cc, source row r0 + q % RB, columns c0 + 16 (q / RB) ..
-// +15 walked left to right, the next four columns of both rows loaded as one batch (eight 16-byte
-// loads in flight per lane)
+// +15 walked left to right, the next NB columns of both rows loaded as one batch
+// (held to <= 128 VGPRs: left alone the compiler hoisted every column's loads into 256 VGPRs + 55 AGPRs, one
+// wave per SIMD, and the kernel ran at 1.9 TB/s)
 template <typename T>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
 in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, float* __restrict__ part, const Up2xSrc u,
                         const float* __restrict__ wt, int ld) {
   __shared__ float red[2][32][65];
@@ -150,16 +151,19 @@ in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, flo
     RT0[e] = 0.f;
     RT1[e] = 0.f;
   }
-  for (int k0 = 0; k0 < 16; k0 += 4) {
-    u32x4 nr0[4], nr1[4];   // raw columns sx0 + k0 + 1 .. +4 of both rows
+  // NB columns of both rows per batch; the batches unrolled, so the compiler may issue a batch's loads
+  // ahead of the previous batch's arithmetic within the 128-VGPR cap (NB = 4 or 8 spill under it)
+  constexpr int NB = 2;
+  for (int k0 = 0; k0 < 16; k0 += NB) {
+    u32x4 nr0[NB], nr1[NB];   // raw columns sx0 + k0 + 1 .. +NB of both rows
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NB; ++j) {
       const int sxn = min(sx0 + k0 + 1 + j, u.W - 1);   // g1x = 0 on the last column
       nr0[j] = *reinterpret_cast<const u32x4*>(r0 + (long)sxn * ldx);
       nr1[j] = *reinterpret_cast<const u32x4*>(r1 + (long)sxn * ldx);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NB; ++j) {
       const int sx = sx0 + k0 + j;
       const float wx = wxt[sx], g0x = wxt[ld + sx], g1x = wxt[2 * ld + sx], g1x2 = 2.f * g1x;
       const bf16* e0 = reinterpret_cast<const bf16*>(&nr0[j]);
