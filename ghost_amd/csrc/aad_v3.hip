@@ -587,7 +587,7 @@ bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, in
 int aad_v3(const AadV3Desc& d, hipStream_t s) {
   if (!aad_v3_supported(GHOST_BF16, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo[0])) return -1;
   if (d.L == 2 && d.ldo[1] % 8) return -1;
-  if (d.L < 1 || d.L > 2 || (d.L == 2 && d.C != 64 && !(d.C == 128 && d.Ca == 64 && d.up_H == 0))) return -1;
+  if (d.L < 1 || d.L > 2 || (d.L == 2 && d.C != 64 && !(d.C == 128 && d.Ca == 64))) return -1;
   AadV3Args a{};
   a.za = (const bf16*)d.za; a.hin = (const bf16*)d.hin; a.stat = d.stat;
   for (int l = 0; l < d.L; ++l) {
@@ -661,8 +661,9 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   // through-upsample forms: the block-input AADLayers of AADBlk8 (first add_block + last_add_block)
   GHOST_V3(64, 64, 2, true) GHOST_V3(64, 32, 2, true) GHOST_V3(64, 64, 1, true) GHOST_V3(64, 32, 1, true)
   GHOST_V3W(128, 128, 1, false) GHOST_V3W(128, 64, 1, false) GHOST_V3W(128, 32, 1, false)
-  // the AADBlk7 block-input pair (C = 128, Ca = 64): one pass over h_in / z_attr for both layers
-  GHOST_V3W(128, 64, 2, false)
+  // the AADBlk7 block-input pair (C = 128, Ca = 64): one pass over h_in / z_attr for both layers, h_in
+  // materialised or (UP) sampled from the 64x64 AADBlk6 output on the fly
+  GHOST_V3W(128, 64, 2, false) GHOST_V3W(128, 64, 2, true)
   // AADBlk7's block-input AADLayers read upsample2x(AADBlk6 output) on the fly (C = 128)
   GHOST_V3W(128, 128, 1, true) GHOST_V3W(128, 64, 1, true) GHOST_V3W(128, 32, 1, true)
   GHOST_V3W(256, 128, 1, false) GHOST_V3W(256, 64, 1, false)

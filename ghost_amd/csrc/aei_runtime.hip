@@ -526,10 +526,10 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     }
     return;
   }
-  // AADBlk7's block-input pair (C = 128, Ca = 64, materialised h_in) in one kernel: measured B = 64,
-  // 258 vs 2 x 141 us (GHOST_AAD_PAIR128=0: one layer per kernel)
+  // AADBlk7's block-input pair (C = 128, Ca = 64; h_in materialised or sampled through the upsample) in one
+  // kernel: measured B = 64, 258 vs 2 x 141 us materialised (GHOST_AAD_PAIR128=0: one layer per kernel)
   static const int pair128 = GHOST_KNOB("GHOST_AAD_PAIR128", 1);
-  const size_t lmax = (C == 64 || (pair128 && C == 128 && Ca == 64 && !up_src)) ? 2 : 1;
+  const size_t lmax = (C == 64 || (pair128 && C == 128 && Ca == 64)) ? 2 : 1;
   for (size_t i0 = 0; i0 < ls.size(); i0 += lmax) {
     AadV3Desc d;
     d.za = za; d.lda = lda; d.Ca = Ca; d.hin = hin; d.ldh = ldh; d.stat = stat;
@@ -762,9 +762,12 @@ void generator(Ctx& c, int B, const void* const attr[8], GenIn gin, void* y_out,
       int Ca_n, n_n;
       h->attr_geom(k + 1, Ca_n, n_n);
       const int cout_n = h->gen()[k][1];
-      // C = 64 only: at C = 128 (AADBlk7) the two single-layer kernels re-reading the upsample
-      // cost more (+110 us) than the materialised upsample they replace (-85 us), measured B = 64
-      const bool fuse = h->opt[GHOST_AEI_OPT_FUSE_UPSAMPLE] && cout != cout_n && cout == 64 && Ca_n % 32 == 0 &&
+      // C = 64 (AADBlk8), and C = 128 (AADBlk7) where its pair runs as one dual-layer kernel (Ca = 64): two
+      // single-layer kernels re-reading the upsample cost more (+110 us) than the materialised upsample they
+      // replace (-85 us), measured B = 64
+      static const int up128 = GHOST_KNOB("GHOST_FUSE_UP128", 1);
+      const bool fuse = h->opt[GHOST_AEI_OPT_FUSE_UPSAMPLE] && cout != cout_n && Ca_n % 32 == 0 &&
+                        (cout == 64 || (up128 && cout == 128 && Ca_n == 64)) &&
                         aad_v3_supported(h->dt, B, n_n * n_n, cout, Ca_n, Ca_n, cout, 8);
       if (fuse) {
         m = y;
