@@ -96,6 +96,20 @@ def pmc_traffic(kernel_substr):
     return None
 
 
+def aad_v4_min_bytes(B, ca8, nl, num_blocks, tap_partials):
+    """Minimum HBM bytes of one aad_v4 launch (AADBlk8's block-input AADLayer pair at 256x256, bf16): the
+    128x128x64 h_in source once, z_attr8 (ca8 channels) once, and each of the nl outputs as stored — 64 bf16
+    channels, or 32 fp16 tap partials for a layer that feeds the 3x3 conv to RGB through them
+    (GHOST_AEI_OPT_TAP_PARTIALS: nb >= 2 -> last_add_block's layer in mode 2; nb = 1 -> the h path's layer in
+    modes 1 and 2, last_add_block's in mode 2).  Returns (bytes, layers writing partials, the kernel's ZPM mask)."""
+    if num_blocks >= 2:
+        zpm = 2 if tap_partials == 2 else 0
+    else:
+        zpm = {0: 0, 1: 1, 2: 3}.get(tap_partials, 0)
+    n_part = min(nl, bin(zpm).count("1"))
+    return B * (128 * 128 * 64 + 65536 * ca8 + (nl - n_part) * 65536 * 64 + n_part * 65536 * 32) * 2.0, n_part, zpm
+
+
 def arcface_flops_per_face(layers=(3, 13, 30, 3)):
     """2*MAC of IResNet at 112x112: stem, per block conv1 (s1) + conv2 (stride) + downsample, fc."""
     fl = 2.0 * 112 * 112 * 64 * 27
@@ -488,13 +502,10 @@ def main():
             # 32 fp16 partial sums per pixel instead of 64 bf16 channels: nb >= 2 -> last_add_block's layer (mode
             # 2); nb = 1 -> the h path's layer (modes 1, 2) and last_add_block's (mode 2)
             zp = G.get_option("tap_partials") if a.dtype == "bf16" else 0
-            n_part = min(nl, (1 if zp == 2 else 0) if a.num_blocks >= 2 else zp)
-            per_launch_min = B * (128 * 128 * 64 + 65536 * ca8 + (nl - n_part) * 65536 * 64
-                                  + n_part * 65536 * 32) * 2.0
+            per_launch_min, n_part, zpm = aad_v4_min_bytes(B, ca8, nl, a.num_blocks, zp)
             ach = per_launch_min / per_launch_s / 1e9
             kname = f"aad_v4_kernel<{ca8}, {nl}, true>" + (f" ({n_part} layer(s) writing tap partials)" if n_part else "")
             # the PMC summary's names carry the ReLU flag and the tap-partial layer mask (ZPM) too
-            zpm = (2 if zp == 2 else 0) if a.num_blocks >= 2 else {0: 0, 1: 1, 2: 3}.get(zp, 0)
             kmatch = f"aad_v4_kernel<{ca8}, {nl}, true, true, {zpm}>"
             res["roofline"] = {"kernel": f"{kname}: AADBlk8's block-input AAD kernel at 256x256, {nl} AADLayer(s) "
                                          "sharing h_in/z_attr, h_in = bilinear x2 of the 128x128 block output "
