@@ -62,6 +62,16 @@ template <typename T> GHOST_DEV void store16_f(T* p, const float* in) {
   *reinterpret_cast<u32x4*>(p) = raw;
 }
 
+// the same with a non-temporal (streaming) store: for a large output that is not read again before it
+// has left the caches
+template <typename T> GHOST_DEV void store16_f_nt(T* p, const float* in) {
+  u32x4 raw;
+  T* e = reinterpret_cast<T*>(&raw);
+#pragma unroll
+  for (int i = 0; i < Vec16<T>::N; ++i) e[i] = from_f<T>(in[i]);
+  __builtin_nontemporal_store(raw, reinterpret_cast<u32x4*>(p));
+}
+
 GHOST_DEV float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
 // v_exp_f32 + v_rcp_f32 (a few ulp from sigmoidf_ref): for masks blended into bf16 outputs
 GHOST_DEV float sigmoid_fast(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }

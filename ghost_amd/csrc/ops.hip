@@ -652,7 +652,7 @@ upsample2x_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, 
 
 // R output rows per workgroup (same sample: 2H % R == 0), each thread's 4R source loads issued
 // before any of them is used: a 256 x 256 x 64 output is 16 K workgroups instead of 64 K
-template <typename T, int R>
+template <typename T, int R, bool NT = false>
 __global__ void __launch_bounds__(256)
 upsample2x_rows_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, const Up2xSrc u, int lg_nch) {
   constexpr int VEC = Vec16<T>::N;
@@ -683,7 +683,10 @@ upsample2x_rows_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int 
 #pragma unroll
     for (int e = 0; e < VEC; ++e)
       o[e] = up2x_mix(t[r].ly0, t[r].ly1, t[r].lx0, t[r].lx1, to_f(e00[e]), to_f(e01[e]), to_f(e10[e]), to_f(e11[e]));
-    store16_f(y + ((long)(row0 + r) * Wo + ox) * ldy + ci * VEC, o);
+    if constexpr (NT)
+      store16_f_nt(y + ((long)(row0 + r) * Wo + ox) * ldy + ci * VEC, o);
+    else
+      store16_f(y + ((long)(row0 + r) * Wo + ox) * ldy + ci * VEC, o);
   }
 }
 
@@ -700,8 +703,14 @@ int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, i
   if (dt == GHOST_BF16 && lg >= 0 && (rows == 2 || rows == 4) && (2 * H) % rows == 0 &&
       (long)H * W * ldx < (1L << 31)) {
     grid.y = (unsigned)(B * 2 * H / rows);
+    // outputs of >= 64 MB (the encoder's z_attr8: 537 MB at B = 64, read again only by AADBlk8, long after it
+    // has left L2 and the Infinity Cache) are written with non-temporal stores
+    static const int nt_knob = GHOST_KNOB("GHOST_UP_NT", 1);
+    const bool nt = nt_knob && (long)B * 4 * H * W * C * 2 >= (64L << 20);
     if (rows == 4)
       hipLaunchKernelGGL((upsample2x_rows_kernel<bf16, 4>), grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, u, lg);
+    else if (nt)
+      hipLaunchKernelGGL((upsample2x_rows_kernel<bf16, 2, true>), grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, u, lg);
     else
       hipLaunchKernelGGL((upsample2x_rows_kernel<bf16, 2>), grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, u, lg);
     return (int)hipGetLastError();
