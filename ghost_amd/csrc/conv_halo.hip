@@ -387,7 +387,10 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   // the wave's youngest VM ops (VM ops retire in issue order), so the wait covers this stage's DMA
   // without waiting for the stores to reach memory; the later stages wait vmcnt(0).
   // (EPX: overhang-masked stores may be skipped by a whole wave, so the count is not static: wait for 0)
-  constexpr int NST = ((DBG & 16) || EPX) ? 0 : 16 + (STATS ? 1 : 0);
+  // W16: the epilogue writes 16-byte pieces (8 stores per wave; see there) — the two-block (Cin = 64) tiles of
+  // the 256 x 256 stage only: with more blocks per tile the exchange's registers push the kernel into spills
+  constexpr bool W16 = !EPX && NCB == 2 && IMG == 1 && !(DBG & 16);
+  constexpr int NST = ((DBG & 16) || EPX) ? 0 : (W16 ? 8 : 16) + (STATS ? 1 : 0);
   if (nmine == 0) return;
   Tile cur = tile_of(0);
   set_dma_tile(cur);
@@ -464,6 +467,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       const int q = i * 16 + lr;
       const int oy = cur.y0 + G::hrow0(wid) + q / TW, ox = cur.x0 + q % TW;
       const long pix = cur.base + (IMG > 1 ? (long)wid * a.H * a.W : 0L) + (long)oy * a.W + ox;
+      uint2 ov[4];   // W16: the 4 channel fragments' bf16 outputs, stored 16 bytes at a time below
       if constexpr (EPX) {
         if (oy >= a.H || ox >= a.W) {
 #pragma unroll
@@ -518,9 +522,27 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
           oe[r] = (bf16)v;
           acc[j][i][r] = STATS ? (float)oe[r] : 0.f;   // the stored (rounded) value, for the statistics
         }
-        if constexpr (!(DBG & 16)) *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+        if constexpr (W16) ov[j] = o;
+        else if constexpr (!(DBG & 16)) *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
         else if ((o.x ^ o.y) == 0x7fc00001u) *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
         }
+      }
+      if constexpr (W16) {
+        // lanes lq and lq ^ 1 (lane ^ 16) hold channels 16 j + 4 lq .. +3 and the next four: each sends the
+        // fragment its partner completes (even lanes keep j = 0, 2, odd lanes j = 1, 3), so every lane writes
+        // two 16-byte pieces of 8 channels (8 stores per wave per tile instead of 16 of 8 bytes)
+        const bool odd = (lq & 1) != 0;
+        const uint2 sa = odd ? ov[0] : ov[1], sb = odd ? ov[2] : ov[3];
+        uint2 ga, gb;
+        ga.x = (unsigned)__shfl_xor((int)sa.x, 16, 64);
+        ga.y = (unsigned)__shfl_xor((int)sa.y, 16, 64);
+        gb.x = (unsigned)__shfl_xor((int)sb.x, 16, 64);
+        gb.y = (unsigned)__shfl_xor((int)sb.y, 16, 64);
+        const uint2 a0 = odd ? ga : ov[0], a1 = odd ? ov[1] : ga;
+        const uint2 b0 = odd ? gb : ov[2], b1 = odd ? ov[3] : gb;
+        bf16* yp = a.y + pix * a.ldy + cur.n0 + (lq & 2) * 4;
+        *reinterpret_cast<u32x4*>(yp + (odd ? 16 : 0)) = u32x4{a0.x, a0.y, a1.x, a1.y};
+        *reinterpret_cast<u32x4*>(yp + (odd ? 48 : 32)) = u32x4{b0.x, b0.y, b1.x, b1.y};
       }
     }
     if constexpr (STATS) {
@@ -931,6 +953,7 @@ bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
   static const int pp = GHOST_KNOB("GHOST_HALO_PP", 1);
   if (!conv3x3_halo_supported(d)) return false;
   if (d.prelu || d.y2 || d.res_first) return false;   // epilogue variants of the non-persistent kernel only
+  if (d.ldy % 8 || (uintptr_t)d.y % 16) return false;   // the 16-byte epilogue stores (W16)
   if (halo_img8(d)) {
     const int ncb = d.Cin / 32;
     const bool ok8 = ncb == 2 || ncb == 4 || ncb == 8 || ncb == 16 || ncb == 32;
