@@ -63,8 +63,8 @@ def parse():
     ap.add_argument("--num-blocks", type=int, default=2)
     ap.add_argument("--identities", type=int, default=1, help="source identities mixed in every batch (config 5: 4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--legs", default="d2h,config5,video,arcface",
-                    help="side measurements at N=1 (comma list of d2h, config5, video, arcface; '' = none)")
+    ap.add_argument("--legs", default="d2h,config5,video,latency,arcface",
+                    help="side measurements at N=1 (comma list of d2h, config5, video, latency, arcface; '' = none)")
     ap.add_argument("--video", type=int, default=900, help="frames of the config-3 video leg")
     ap.add_argument("--cpu-batches", default="1,64", help="CPU baseline batch sizes ('' = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
@@ -94,6 +94,36 @@ def pmc_traffic(kernel_substr):
             return {"bytes_per_launch": k["hbm_bytes"], "read": k["read_bytes"], "write": k["write_bytes"],
                     "source": rel + " (" + data.get("source", "rocprofv3 --pmc") + ")"}
     return None
+
+
+def rocprof_avg_us(kname):
+    """The kernel's average duration in the newest committed rocprofv3 --stats summaries: the timed
+    configuration (profiles/rNN_kernel_stats.csv: bench.py's two batches in flight) and one batch at a time
+    (profiles/rNN_kernel_stats_1stream.csv).  kname: the demangled 'aad_v5_kernel<64, 2, true, 2>'."""
+    import csv
+    import glob
+    import re
+    m = re.match(r"(\w+)<(.*)>", kname)
+    if not m:
+        return None
+    base, targs = m.group(1), [t.strip() for t in m.group(2).split(",")]
+    mangled = base + "I" + "".join(("Lb1E" if t == "true" else "Lb0E" if t == "false" else f"Li{t}E") for t in targs) + "E"
+    out = {}
+    for key, pat in (("timed", "r[0-9][0-9]_kernel_stats.csv"), ("isolated", "r[0-9][0-9]_kernel_stats_1stream.csv")):
+        files = sorted(glob.glob(os.path.join(REPO, "profiles", pat)))
+        if not files:
+            continue
+        try:
+            for r in csv.DictReader(open(files[-1])):
+                nm = r.get("Name") or r.get("KernelName") or ""
+                if mangled in nm or kname in nm.replace("ghost::", ""):
+                    out[key + "_avg_us"] = round(float(r["AverageNs"]) / 1e3, 2)
+                    out[key + "_calls"] = int(r["Calls"])
+                    out[key + "_source"] = os.path.relpath(files[-1], REPO)
+                    break
+        except (OSError, ValueError, KeyError):
+            continue
+    return out or None
 
 
 def aad_v4_min_bytes(B, ca8, nl, num_blocks, tap_partials):
@@ -346,6 +376,38 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
             "host_bytes_moved": int(n_face * 196608 * 2 + 2 * n_frames * H * W * 3)}
 
 
+def latency_leg(dev, n=20):
+    """BASELINE config 1 on the GPU: one 256x256 image-to-image swap (B = 1, unet/2), fp32 and bf16.
+    latency_ms = wall time of one synchronous swap_u8 call (median of n, after warm-up); host_ms = the
+    host time of the call alone (the Python wrapper + the native plan's launches onto an idle stream,
+    median of n)."""
+    out = {"workload": "config 1 on 1 GPU: B=1 unet/2 swap_u8 (u8 crop in -> u8 swap out, device-resident), "
+                       "one call at a time, synchronised after each"}
+    crop = torch.from_numpy(np.random.Generator(np.random.PCG64(21)).integers(0, 256, (1, 256, 256, 3),
+                                                                           dtype=np.uint8)).to(dev)
+    z = identity_rows(1, dev)
+    for name, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+        G = make_model("unet", 2, dt, dev)
+        y = torch.empty(1, 256, 256, 3, dtype=torch.uint8, device=dev)
+        for _ in range(5):
+            G.swap_u8(crop, z, out=y)
+        torch.cuda.synchronize()
+        lat, host = [], []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            G.swap_u8(crop, z, out=y)
+            t1 = time.perf_counter()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            host.append(t1 - t0)
+            lat.append(t2 - t0)
+        out[name] = {"latency_ms": round(float(np.median(lat)) * 1e3, 3),
+                     "host_ms": round(float(np.median(host)) * 1e3, 3)}
+        del G
+        torch.cuda.empty_cache()
+    return out
+
+
 def host_cpu_budget():
     """CPUs this process may use: the cgroup quota when one is set (the GPU box gives a job a share
     of a large host, whose os.cpu_count() is many times that share), else the affinity mask."""
@@ -384,6 +446,60 @@ def cpu_baseline(backbone, nb, batches):
             "os_cpu_count": os.cpu_count(), "by_batch": per_b,
             "sample": f"{backbone}/{nb} fp32 (oracle/aei_ref.py) at B in {list(batches)}: 1 warm-up + 3 timed "
                       f"iterations each on {threads} threads (the process's CPU quota); value = B={best}"}
+
+
+def device_sync(dev: torch.device) -> None:
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def timed_region(step, drain, steps, warmup, world, dev, before_timed=None) -> float:
+    """W untimed warm-up steps, then EXACTLY K timed steps bracketed by a barrier + device synchronize on
+    both sides (every step's collective drained inside the region); returns the max over ranks of the
+    K steps' wall time (an all-reduce MAX over the group: RCCL on the GPU, gloo in the CPU test)."""
+    for _ in range(warmup):
+        step()
+    drain()
+    device_sync(dev)
+    if before_timed is not None:
+        before_timed()
+    if world > 1:
+        dist.barrier()
+    device_sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    drain()
+    device_sync(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def headline_record(world, B, steps, warmup, el, backbone, num_blocks, identities, dtype, nstreams) -> dict:
+    """The JSON line's headline fields: value = frames of ALL ranks / max-over-ranks time (weak scaling,
+    B frames per GPU per step)."""
+    frames = world * B * steps
+    cfg = "config 5 (mixed identities)" if identities > 1 else ("config 4" if world > 1 else "config 2")
+    return {
+        "metric": BASELINE_METRIC,
+        "value": round(frames / el, 2), "unit": "frames/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(el / steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": dtype if dtype == "fp32" else "bf16", "data": "synthetic",
+        "config": {"workload": f"BASELINE {cfg}: batch={B} synthetic 256x256 aligned faces per GPU"
+                               + (f" mixing {identities} identities" if identities > 1 else "")
+                               + f", AEI_Net {backbone} num_blocks={num_blocks}, faceshifter_batch "
+                                 "(u8 in -> u8 out, device-resident; D2H in legs.d2h)"
+                               + (", RCCL all-gather of swapped crops" if world > 1 else ""),
+                   "global_batch": world * B, "per_gpu_batch": B, "backbone": backbone,
+                   "num_blocks": num_blocks, "identities": max(1, identities),
+                   "parallelism": f"dp{world}", "batches_in_flight": nstreams},
+    }
 
 
 def main():
@@ -425,36 +541,23 @@ def main():
         if pipe.depth == 1:
             pipe.result(slot)
 
-    for _ in range(a.warmup):
-        step()
-    pipe.drain()
-    torch.cuda.synchronize()
     prof = not a.no_profile
     names = ["aad_all", "aad_dual_256", "conv3x3_all", "conv3x3_256", "in_stats_mask", "encoder", "upsample",
              "id_proj"]
     classes = {}
-    if prof:
-        # inside the timed region only the roofline kernel is bracketed (one HIP event pair per step,
-        # recorded on the launch stream around each of its launches)
-        G.profile(1 << names.index("aad_dual_256"))
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    pipe.drain()                  # every step's all-gather is inside the timed region
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+
+    def before_timed():
+        if prof:
+            # inside the timed region only the roofline kernel is bracketed (one HIP event pair per step,
+            # recorded on the launch stream around each of its launches)
+            G.profile(1 << names.index("aad_dual_256"))
+
+    el = timed_region(step, pipe.drain, a.steps, a.warmup, world, dev, before_timed)
     iso = {}
+    clock = {"timed": (0.0, 0), "isolated": (0.0, 0)}
     if prof:
         classes["aad_dual_256"] = G.profile_read(names.index("aad_dual_256"))
+        clock["timed"] = G.profile_clock()
         # per-class breakdown from a separate, untimed pass with one batch at a time (every kernel class
         # bracketed; with batches in flight a class's time would include the other batch's kernels)
         pipe.drain()
@@ -470,30 +573,17 @@ def main():
                 classes[n] = G.profile_read(i)
             else:
                 iso = G.profile_read(i)
+        clock["isolated"] = G.profile_clock()
         G.profile(0)
 
     if rank == 0:
-        frames = world * B * a.steps
-        value = frames / el
-        cfg = "config 5 (mixed identities)" if a.identities > 1 else ("config 4" if world > 1 else "config 2")
-        res = {
-            "metric": BASELINE_METRIC,
-            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": a.dtype if a.dtype == "fp32" else "bf16", "data": "synthetic",
-            "config": {"workload": f"BASELINE {cfg}: batch={B} synthetic 256x256 aligned faces per GPU"
-                                   + (f" mixing {a.identities} identities" if a.identities > 1 else "")
-                                   + f", AEI_Net {a.backbone} num_blocks={a.num_blocks}, faceshifter_batch "
-                                     "(u8 in -> u8 out, device-resident; D2H in legs.d2h)"
-                                   + (", RCCL all-gather of swapped crops" if world > 1 else ""),
-                       "global_batch": world * B, "per_gpu_batch": B, "backbone": a.backbone,
-                       "num_blocks": a.num_blocks, "identities": max(1, a.identities),
-                       "parallelism": f"dp{world}", "batches_in_flight": pipe.nstreams},
-        }
+        res = headline_record(world, B, a.steps, a.warmup, el, a.backbone, a.num_blocks, a.identities, a.dtype,
+                              pipe.nstreams)
         if prof and classes["aad_dual_256"]["launches"]:
             c = classes["aad_dual_256"]
             per_launch_formula = c["bytes"] / c["launches"]
-            per_launch_s = c["ms"] / c["launches"] / 1e3
+            ev_s = c["ms"] / c["launches"] / 1e3                 # HIP-event bracket (includes queueing)
+            clk_us, clk_n = clock["timed"]
             ca8 = 32 if a.backbone == "linknet" else 64     # z_attr8 channels (AEI_Net.py:110,118)
             # layers in the kernel: the formula bytes per launch are L * B*256^2*(2*64 + Ca)*2
             nl = max(1, round(per_launch_formula / (B * 65536 * (2 * 64 + ca8) * 2)))
@@ -503,41 +593,59 @@ def main():
             # 2); nb = 1 -> the h path's layer (modes 1, 2) and last_add_block's (mode 2)
             zp = G.get_option("tap_partials") if a.dtype == "bf16" else 0
             per_launch_min, n_part, zpm = aad_v4_min_bytes(B, ca8, nl, a.num_blocks, zp)
+            v5 = G.kernel_variant("aad_dual_256") == "v5"
+            kname = (f"aad_v5_kernel<{ca8}, {nl}, true, {zpm}>" if v5 else f"aad_v4_kernel<{ca8}, {nl}, true, true, {zpm}>")
+            # the kernel's own execution span (first workgroup start -> last wave end, its wall-clock stamps),
+            # live in the timed region; the event bracket only if the clock recorded nothing
+            clocked = clk_n > 0
+            per_launch_s = clk_us / clk_n / 1e6 if clocked else ev_s
             ach = per_launch_min / per_launch_s / 1e9
-            kname = f"aad_v4_kernel<{ca8}, {nl}, true>" + (f" ({n_part} layer(s) writing tap partials)" if n_part else "")
-            # the PMC summary's names carry the ReLU flag and the tap-partial layer mask (ZPM) too
-            kmatch = f"aad_v4_kernel<{ca8}, {nl}, true, true, {zpm}>"
-            res["roofline"] = {"kernel": f"{kname}: AADBlk8's block-input AAD kernel at 256x256, {nl} AADLayer(s) "
-                                         "sharing h_in/z_attr, h_in = bilinear x2 of the 128x128 block output "
-                                         "sampled in-kernel (IN-normalise, sigmoid mask, MFMA gamma/beta, blend, "
-                                         "ReLU)",
-                               "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(kmatch),
-                               "bytes_per_launch": per_launch_min,
-                               "bytes_note": "achieved = minimum bytes of the fused kernel (128x128 h_in source + "
-                                             "z_attr8 + outputs as stored: 64 bf16 channels, or 32 fp16 tap partials "
-                                             "per pixel) / launch time; formula_* = SURVEY.md 8d's per-layer "
-                                             "|h_in|+|z_attr|+|out| with h_in counted at 256x256 per layer",
-                               "formula_bytes_per_launch": per_launch_formula,
-                               "formula_gbs": round(per_launch_formula / per_launch_s / 1e9, 1),
-                               "formula_frac": round(per_launch_formula / per_launch_s / 1e9 / HBM_PEAK_GBS, 4),
-                               "avg_launch_us": round(per_launch_s * 1e6, 2), "launches_timed": c["launches"]}
-            tr = res["roofline"]["traffic"]
+            tr = pmc_traffic(kname)
+            rp = rocprof_avg_us(kname)
+            res["roofline"] = {
+                "kernel": f"{kname}: AADBlk8's block-input AAD kernel at 256x256, {nl} AADLayer(s) sharing h_in/"
+                          "z_attr, h_in = bilinear x2 of the 128x128 block output sampled in-kernel (IN-normalise, "
+                          "sigmoid mask, MFMA gamma/beta, blend, ReLU)"
+                          + (f"; {n_part} layer(s) writing tap partials" if n_part else ""),
+                "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": tr["bytes_per_launch"] if tr else None,
+                "avg_launch_us": round(per_launch_s * 1e6, 2), "launches_timed": clk_n if clocked else c["launches"],
+                "duration_source": ("in-kernel wall clock (earliest workgroup start to latest wave end, "
+                                    "s_memrealtime stamps) of every launch in the timed region" if clocked else
+                                    "HIP events on the launch stream around each launch in the timed region"),
+                "bytes_per_launch": per_launch_min,
+                "bytes_note": "achieved = minimum bytes of the fused kernel (128x128 h_in source + z_attr8 + outputs "
+                              "as stored: 64 bf16 channels, or 32 fp16 tap partials per pixel) / launch duration",
+                "fractions": {
+                    "minimum_bytes": round(ach / HBM_PEAK_GBS, 4),
+                    "physical_pmc": (round(tr["bytes_per_launch"] / per_launch_s / 1e9 / HBM_PEAK_GBS, 4)
+                                     if tr else None),
+                    "survey_8d_formula": round(per_launch_formula / per_launch_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "formula_bytes_per_launch": per_launch_formula,
+                    "pmc_source": tr["source"] if tr else None},
+                "timed_region_latency": {
+                    "avg_launch_us": round(ev_s * 1e6, 2), "launches": c["launches"],
+                    "note": (f"HIP events on the launch stream; with {pipe.nstreams} batches in flight the bracket "
+                             "includes queueing behind the other stream's kernels")},
+                "rocprof": rp,
+            }
             if tr:
-                res["roofline"]["physical_gbs"] = round(tr["bytes_per_launch"] / per_launch_s / 1e9, 1)
-                res["roofline"]["physical_frac"] = round(res["roofline"]["physical_gbs"] / HBM_PEAK_GBS, 4)
-            if pipe.nstreams > 1 and iso.get("launches"):
-                # the same kernel with one batch on the GPU (untimed pass): in the timed region it shares the
-                # GPU (HBM, CUs) with the other batch in flight, so its launch there takes longer
-                iso_s = iso["ms"] / iso["launches"] / 1e3
-                res["roofline"]["timed_region_note"] = (f"{pipe.nstreams} batches in flight: the launch duration "
-                                                        "includes sharing the GPU with the other batch's kernels")
+                res["roofline"]["traffic_detail"] = tr
+            if rp and rp.get("timed_avg_us"):
+                res["roofline"]["rocprof_agreement"] = round(per_launch_s * 1e6 / rp["timed_avg_us"], 3)
+            if iso.get("launches"):
+                # the same kernel with one batch on the GPU (untimed pass)
+                iso_us, iso_n = clock["isolated"]
+                iso_s = iso_us / iso_n / 1e6 if iso_n else iso["ms"] / iso["launches"] / 1e3
                 res["roofline"]["isolated"] = {
                     "avg_launch_us": round(iso_s * 1e6, 2), "achieved": round(per_launch_min / iso_s / 1e9, 1),
                     "frac": round(per_launch_min / iso_s / 1e9 / HBM_PEAK_GBS, 4),
                     "formula_frac": round(per_launch_formula / iso_s / 1e9 / HBM_PEAK_GBS, 4),
                     "physical_frac": (round(tr["bytes_per_launch"] / iso_s / 1e9 / HBM_PEAK_GBS, 4) if tr else None),
-                    "launches": iso["launches"], "note": "one batch at a time, HIP events on the launch stream"}
+                    "event_avg_launch_us": round(iso["ms"] / iso["launches"] * 1e3, 2),
+                    "launches": iso["launches"],
+                    "note": "one batch at a time (untimed pass); rocprof.isolated_avg_us is the one-stream trace row"}
             cc = classes["conv3x3_all"]
             if cc["launches"]:
                 tf = cc["flops"] / (cc["ms"] / 1e3) / 1e12
@@ -562,6 +670,8 @@ def main():
             res["legs"]["config3_video"] = video_leg(G, dev, a.video)
         if "config5" in legs:
             res["legs"]["config5"] = config5_leg(dev, B, a.steps, 3, nstreams=pipe.nstreams)
+        if "latency" in legs:
+            res["legs"]["config1_latency"] = latency_leg(dev)
         if "arcface" in legs and a.arc_batch > 0:
             # one batch at a time: two in flight measured neutral (the persistent 3x3 convs hold every CU)
             res["legs"]["arcface"] = arcface_leg(dev, a.arc_batch, max(3, a.steps // 2), 1)

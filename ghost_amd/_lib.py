@@ -47,6 +47,7 @@ _SIGS = {
     "ghost_aei_profile": (i32, [vp, i32]),
     "ghost_aei_profile_read": (i32, [vp, i32, C.POINTER(C.c_double), C.POINTER(i64), C.POINTER(C.c_double),
                                      C.POINTER(C.c_double)]),
+    "ghost_aei_profile_clock": (i32, [vp, C.POINTER(C.c_double), C.POINTER(i64), C.POINTER(i32)]),
     "ghost_conv2d_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
                                 f32, vp, i32, i32, vp, i32, vp, i64, vp]),
     "ghost_arc_create": (i32, [C.POINTER(i32), i32, i32, C.POINTER(vp)]),

@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 
 from .. import _lib
+from .._packed import PackedModule, WorkspaceCache
 
 WIDTHS = (64, 128, 256, 512)
 
@@ -67,6 +68,7 @@ class _Runtime:
         _lib.check(self.lib.ghost_arc_create(arr, nf, _lib.gdtype(dtype), C.byref(h)), "ghost_arc_create")
         self.h = h
         self.slots = slots
+        self.ws = WorkspaceCache()   # (N, stream) -> workspace
         for name, t in slots.items():
             _lib.check(self.lib.ghost_arc_bind(h, name.encode(), t.data_ptr(), t.numel()), f"bind {name}")
         if self.lib.ghost_arc_missing(h) != 0:
@@ -80,7 +82,7 @@ class _Runtime:
             pass
 
 
-class IResNet(nn.Module):
+class IResNet(PackedModule):
     fc_scale = 7 * 7
 
     def __init__(self, block, layers, dropout=0, num_features=512, zero_init_residual=False, groups=1,
@@ -117,8 +119,7 @@ class IResNet(nn.Module):
             for m in self.modules():
                 if isinstance(m, IBasicBlock):
                     nn.init.constant_(m.bn2.weight, 0)
-        self._rt = None
-        self._rt_sig = None
+        self._init_packed()
 
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None
@@ -139,17 +140,16 @@ class IResNet(nn.Module):
     def _runtime(self, device):
         from .pack import pack_iresnet
         dt = self._dtype()
-        sig = (device, dt) + tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
-        if self._rt is None or self._rt_sig != sig:
-            sd = {k: v.detach() for k, v in self.state_dict().items()}
-            for k, v in sd.items():
-                if v.is_floating_point() and v.device != device:
-                    raise RuntimeError(f"ghost_amd: parameter {k} is on {v.device}, input on {device}")
-            with torch.no_grad():
-                slots = pack_iresnet(sd, self.layers_cfg, dt)
-            self._rt = _Runtime(self.layers_cfg, self.num_features, dt, slots)
-            self._rt_sig = sig
-        return self._rt
+        return self._cached_runtime(device, dt, lambda sd: _Runtime(self.layers_cfg, self.num_features, dt,
+                                                                     pack_iresnet(sd, self.layers_cfg, dt)))
+
+    def _workspace(self, rt, N, dev):
+        def nbytes():
+            n = rt.lib.ghost_arc_workspace_bytes(rt.h, N)
+            if n < 0:
+                _lib.check(int(n), "ArcFace workspace sizing")
+            return n
+        return rt.ws.get((N, _lib.stream_ptr(dev)), nbytes, dev)
 
     # -- execution -------------------------------------------------------------------
     @torch.no_grad()
@@ -163,10 +163,7 @@ class IResNet(nn.Module):
         rt = self._runtime(x.device)
         N = x.shape[0]
         emb = torch.empty(N, self.num_features, dtype=torch.float32, device=x.device)
-        nbytes = rt.lib.ghost_arc_workspace_bytes(rt.h, N)
-        if nbytes < 0:
-            _lib.check(int(nbytes), "ArcFace workspace sizing")
-        ws = torch.empty(int(nbytes), dtype=torch.uint8, device=x.device)
+        ws = self._workspace(rt, N, x.device)
         st = (C.c_int64 * 4)(*x.stride())
         _lib.check(rt.lib.ghost_arc_forward(rt.h, x.data_ptr(), _lib.gdtype(x.dtype), st, N, emb.data_ptr(),
                                             ws.data_ptr(), ws.numel(), _lib.stream_ptr(x.device)), "IResNet.forward")
@@ -184,7 +181,7 @@ class IResNet(nn.Module):
         rt = self._runtime(crops.device)
         N, H, W = crops.shape[:3]
         emb = torch.empty(N, self.num_features, dtype=torch.float32, device=crops.device)
-        ws = torch.empty(int(rt.lib.ghost_arc_workspace_bytes(rt.h, N)), dtype=torch.uint8, device=crops.device)
+        ws = self._workspace(rt, N, crops.device)
         _lib.check(rt.lib.ghost_arc_embed_u8(rt.h, crops.data_ptr(), crops.stride(0), N, H, W, emb.data_ptr(),
                                              ws.data_ptr(), ws.numel(), _lib.stream_ptr(crops.device)),
                    "IResNet.embed_u8")

@@ -27,6 +27,9 @@ struct AadV3Desc {
   // layout's K slice of this layer's channels); out[l] is then that [B*HW][32] fp16 buffer
   const void* zw[2] = {nullptr, nullptr};
   int zwld = 0;
+  // in-kernel clock of the launch (profiling; the v5 kernel): [0] earliest start, [1] latest end
+  unsigned long long* tclk = nullptr;
+  int* version_out = nullptr;   // set to the kernel generation that ran (3, 4 or 5)
 };
 
 // the 3x3 / pad 1 conv to 3 channels from two tap-partial buffers (AADBlk8's output conv over

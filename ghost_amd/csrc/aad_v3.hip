@@ -40,6 +40,10 @@ struct AadV3Args {
   int zwld;
   float slope;
   Up2xSrc up;   // UP: h_in is the bilinear x2 upsample of hin (a [B, up.H, up.W] source)
+  // in-kernel clock (v5; nullptr = off): [0] = earliest workgroup start, [1] = latest wave end, in
+  // wall-clock ticks (hipDeviceAttributeWallClockRate); atomicMin / atomicMax by one lane each
+  unsigned long long* tclk;
+  int v5_xcd;   // v5: blocks in XCD-contiguous order
 };
 
 static constexpr int kWaves = 8;
@@ -346,6 +350,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   // so the per-tile address arithmetic runs on the scalar unit and the VALU keeps only lane offsets
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, lr = lane & 15,
             lq = lane >> 4;
+  if (a.tclk && tid == 0) atomicMin(&a.tclk[0], (unsigned long long)wall_clock64());
   const long p_begin = (long)blockIdx.x * a.PPW;
   const int b = (int)(p_begin / a.HW);
   zp_stage_weights<L, ZPM, kWaves * 64>(a, s_wz, tid);
@@ -566,6 +571,288 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) zc[ks] = zn[ks];
   }
+  if (a.tclk && lane == 0) atomicMax(&a.tclk[1], (unsigned long long)wall_clock64());
+}
+
+// ---------------------------------------------------------------------------------------------
+// v5: v4 with each wave tile = 2 output rows x 8 columns that read the SAME two source rows.
+//
+// In v4 a tile is 16 pixels of one output row: it DMAs 10 source pixels of each of its 2 source rows,
+// and every source row is fetched again for each of the ~4 output rows that sample it (the h_in source
+// came from HBM ~3.6x per launch: PMC 1.025 GB read against 0.671 GB minimum).  With align_corners and
+// an exact x2 scale, output rows 2k-1 and 2k sample the same source rows (k-1, k) for k = 1 .. H-1, and
+// rows 0 and 2H-1 sample source rows 0 and H-1 alone (interpolation weight exactly 0 on the other row;
+// the host checks both facts in fp32, v5_pairing_ok).  So the image's output rows form H "row tiles":
+// q = 0 -> rows {0, 2H-1}, q >= 1 -> rows {2q-1, 2q}, each reading 2 source rows.  A wave tile is one row
+// tile x 8 columns = 16 pixels (lanes lr 0-7 the first row, 8-15 the second: the MFMA's 16-pixel B
+// operand): 2 rows x 6 source pixels = 1.5 KB of DMA per 16 pixels instead of 2.5 KB.  A workgroup
+// (1024 pixels) covers RT = 64 / (OW / 8) row tiles; its waves walk them side by side (wave w: row tile
+// w % RT, columns 8 (w / RT + (8 / RT) i)), so the source row two neighbouring row tiles share is fetched
+// by both at nearly the same time (one L2 miss), and blocks go to XCDs in contiguous runs
+// (xcd_remap) so the row a block shares with the next is read on the same L2.
+// ---------------------------------------------------------------------------------------------
+template <int CA, int L, bool RELU, int ZPM = 0>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v5_kernel(const AadV3Args a) {
+  constexpr int C = 64, KS = CA / 32, SPX = 6, SLOT_B = 2 * SPX * 128;
+  constexpr int WLD = ZPM ? CA : CA + 8;
+  auto widx = [](int row, int k) { return ZPM ? swca<CA>(row, k) : row * (CA + 8) + k; };
+  __shared__ __attribute__((aligned(16))) bf16 s_w[L * 128 * WLD];
+  __shared__ __attribute__((aligned(16))) float s_b[L * 128];
+  __shared__ __attribute__((aligned(16))) float s_rs[C];
+  __shared__ __attribute__((aligned(16))) float s_nm[C];
+  __shared__ __attribute__((aligned(16))) float s_cf[L * C];
+  __shared__ float s_k[L];
+  __shared__ __attribute__((aligned(16))) float s_gi[L * C];
+  __shared__ __attribute__((aligned(16))) float s_bi[L * C];
+  __shared__ __attribute__((aligned(1024))) unsigned char s_hA[kWaves * SLOT_B];
+  __shared__ __attribute__((aligned(1024))) unsigned char s_hB[kWaves * SLOT_B];
+  __shared__ __attribute__((aligned(16))) bf16 s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
+
+  const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, lr = lane & 15,
+            lq = lane >> 4;
+  if (a.tclk && tid == 0) atomicMin(&a.tclk[0], (unsigned long long)wall_clock64());
+  const int H = a.up.H, W = a.up.W, OW = 2 * W;
+  const int NCT = OW / 8;                      // 8-column tiles per row tile
+  const int RT = 64 / NCT;                     // row tiles per workgroup (host: 1, 2, 4 or 8)
+  const int wpi = H / RT;                      // workgroups per image
+  const int wi = a.v5_xcd ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const int b = wi / wpi, g = wi - b * wpi;
+  zp_stage_weights<L, ZPM, kWaves * 64>(a, s_wz, tid);
+
+  for (int l = 0; l < L; ++l) {
+    for (int idx = tid; idx < 128 * (CA / 8); idx += kWaves * 64) {
+      const int row = idx / (CA / 8), kc = idx - row * (CA / 8);
+      *reinterpret_cast<u32x4*>(&s_w[widx(l * 128 + row, kc * 8)]) =
+          *reinterpret_cast<const u32x4*>(a.w3[l] + (long)row * CA + kc * 8);
+    }
+    for (int idx = tid; idx < 128; idx += kWaves * 64) s_b[l * 128 + idx] = a.b3[l][idx];
+    for (int c = tid; c < C; c += kWaves * 64) {
+      const float rs = a.stat[((long)b * C + c) * 2 + 1];
+      s_cf[l * C + c] = a.wh[l][c] * rs;
+      s_gi[l * C + c] = a.idgb[l][(long)b * a.id_ld + c];
+      s_bi[l * C + c] = a.idgb[l][(long)b * a.id_ld + C + c];
+    }
+  }
+  for (int c = tid; c < C; c += kWaves * 64) {
+    const float mu = a.stat[((long)b * C + c) * 2], rs = a.stat[((long)b * C + c) * 2 + 1];
+    s_rs[c] = rs;
+    s_nm[c] = -mu * rs;
+  }
+  __syncthreads();
+  if (wid < L) {
+    float k = 0.f;
+    for (int c = lane; c < C; c += 64) k = fmaf(a.wh[wid][c], s_nm[c], k);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) k += __shfl_xor(k, o, 64);
+    if (lane == 0) s_k[wid] = k;
+  }
+  __syncthreads();
+  float bh[L];
+#pragma unroll
+  for (int l = 0; l < L; ++l) bh[l] = a.bh[l][0] + s_k[l];
+
+  const bf16* src = a.hin + (long)b * H * W * a.ldh;
+  const long pimg = (long)b * a.HW;
+  const int ri = lr >> 3, col = lr & 7;        // this lane's pixel: row ri of the row tile, column col
+  const int rtl = wid % RT;                    // this wave's row tile inside the workgroup
+  const int q = g * RT + rtl;                  // ... inside the image
+  const int oyA = q == 0 ? 0 : 2 * q - 1, oyB = q == 0 ? 2 * H - 1 : 2 * q;
+  // source rows of the row tile (scalar): sA = y0(oyA); sB = y1(oyA) for a pair, y0(oyB) for the edge tile
+  int sA, sB;
+  {
+    float rA = a.up.sh * (float)oyA, rB = a.up.sh * (float)oyB;
+    asm volatile("" : "+v"(rA), "+v"(rB));
+    const int y0A = __builtin_amdgcn_readfirstlane((int)rA), y0B = __builtin_amdgcn_readfirstlane((int)rB);
+    sA = y0A;
+    sB = q == 0 ? y0B : y0A + (y0A < H - 1 ? 1 : 0);
+  }
+  // this lane's row: its y taps as slot rows (top / bottom) and weight
+  const int oy = ri ? oyB : oyA;
+  float fly1;
+  int top, bot;
+  {
+    float ry = a.up.sh * (float)oy;
+    asm volatile("" : "+v"(ry));
+    const int y0 = (int)ry, y1 = y0 + (y0 < H - 1 ? 1 : 0);
+    fly1 = ry - (float)y0;
+    top = y0 == sA ? 0 : 1;
+    bot = y1 == sA ? 0 : (y1 == sB ? 1 : top);
+  }
+  const f32x2 ly0 = {1.f - fly1, 1.f - fly1}, ly1 = {fly1, fly1};
+  const long prow = pimg + (long)oy * OW;      // this lane's output row
+  const int nw = 64 / kWaves;                  // tiles per wave
+  const int ox_w = 8 * (wid / RT), ox_step = 64 / RT;   // wave's first column, column step between its tiles
+
+  // z fragments of tile i (registers) + its 2 x 6 source pixels (DMA into slot `slot` of this wave)
+  auto issue = [&](int i, u32x4 (&zc)[KS], unsigned char* slot) {
+    const int ox0 = ox_w + ox_step * i;
+    const bf16* zt = a.za + (prow + ox0 + col) * a.lda + lq * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(zt + ks * 32);
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned char* dst = slot + wid * SLOT_B;
+    float rx = a.up.sw * (float)ox0;
+    asm volatile("" : "+v"(rx));
+    const int x_lo = __builtin_amdgcn_readfirstlane((int)rx);
+    const bf16* rowA = src + (long)sA * W * a.ldh;
+    const bf16* rowB = src + (long)sB * W * a.ldh;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k == 1 && lane >= 32) continue;                    // 12 slot pixels x 8 chunks = 96 pieces
+      const int qs = k * 8 + (lane >> 3), cl = lane & 7;     // slot pixel / chunk position this lane fills
+      const int sr = qs >= SPX, px = qs - (sr ? SPX : 0);
+      const int sx = min(x_lo + px, W - 1);
+      __builtin_amdgcn_global_load_lds((sr ? rowB : rowA) + sx * a.ldh + ((cl ^ (qs & 7)) * 8), dst + k * 1024, 16,
+                                       0, 0);
+    }
+#endif
+  };
+  // tile i's h_in chunks out of its LDS slot through the bilinear x2
+  auto hload = [&](int i, const unsigned char* slot, u32x4 (&hc)[2]) {
+    const unsigned char* hs = slot + wid * SLOT_B;
+    const int ox0 = ox_w + ox_step * i;
+    float rx0 = a.up.sw * (float)ox0;
+    asm volatile("" : "+v"(rx0));
+    const int x_lo = __builtin_amdgcn_readfirstlane((int)rx0);
+    float rx = a.up.sw * (float)(ox0 + col);
+    asm volatile("" : "+v"(rx));
+    const int x0 = (int)rx;
+    const int x1 = x0 + (x0 < W - 1 ? 1 : 0);
+    const float flx1 = rx - (float)x0;
+    const int q00 = top * SPX + x0 - x_lo, q01 = top * SPX + x1 - x_lo;
+    const int q10 = bot * SPX + x0 - x_lo, q11 = bot * SPX + x1 - x_lo;
+    const f32x2 lx0 = {1.f - flx1, 1.f - flx1}, lx1 = {flx1, flx1};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ch = j * 4 + lq;
+      auto ld = [&](int qq) { return *reinterpret_cast<const u32x4*>(hs + qq * 128 + ((ch ^ (qq & 7)) * 16)); };
+      const u32x4 r00 = ld(q00), r01 = ld(q01), r10 = ld(q10), r11 = ld(q11);
+      bf16* hv = reinterpret_cast<bf16*>(&hc[j]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f32x2 tp = fma2(lx0, bf16x2_f(r00[k]), lx1 * bf16x2_f(r01[k]));
+        const f32x2 bt = fma2(lx0, bf16x2_f(r10[k]), lx1 * bf16x2_f(r11[k]));
+        const f32x2 v = fma2(ly0, tp, ly1 * bt);
+        hv[2 * k] = (bf16)v.x;
+        hv[2 * k + 1] = (bf16)v.y;
+      }
+    }
+  };
+  auto compute = [&](int i, const u32x4 (&zc)[KS], const u32x4 (&hc)[2]) {
+    const long p = prow + (ox_w + ox_step * i) + col;   // this lane's output pixel
+    f32x2 ms[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) ms[l] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c0 = j * 32 + lq * 8;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f32x2 h2 = bf16x2_f(hc[j][k]);
+#pragma unroll
+        for (int l = 0; l < L; ++l) ms[l] = fma2(*reinterpret_cast<const f32x2*>(&s_cf[l * C + c0 + 2 * k]), h2, ms[l]);
+      }
+    }
+    float Mk[L];
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      float sm = ms[l].x + ms[l].y;
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      Mk[l] = sigmoid_fast(sm + bh[l]);
+    }
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      asm volatile("" ::: "memory");
+      const bf16* Wt = s_w + l * 128 * WLD;
+      f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int sh = 0; sh < 2; ++sh) {
+        asm volatile("" ::: "memory");
+        f32x4 acc[4];
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) {
+          const int rt = (i4 & 1) + 2 * sh + 4 * (i4 >> 1);
+          acc[i4] = *reinterpret_cast<const f32x4*>(&s_b[l * 128 + rt * 16 + lq * 4]);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          bf16x8 bfrag;
+          __builtin_memcpy(&bfrag, &zc[ks], 16);
+#pragma unroll
+          for (int i4 = 0; i4 < 4; ++i4) {
+            const int rt = (i4 & 1) + 2 * sh + 4 * (i4 >> 1);
+            const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&Wt[widx(rt * 16 + lr, ks * 32 + lq * 8)]);
+            acc[i4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i4], 0, 0, 0);
+          }
+        }
+        const int c0 = sh * 32 + lq * 8;
+        const f32x2 M2 = {Mk[l], Mk[l]};
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int c = c0 + 2 * k;
+          const f32x2 hh = fma2(bf16x2_f(hc[sh][k]), *reinterpret_cast<const f32x2*>(&s_rs[c]),
+                                *reinterpret_cast<const f32x2*>(&s_nm[c]));
+          const f32x2 gg = {acc[k >> 1][(2 * k) & 3], acc[k >> 1][(2 * k + 1) & 3]};
+          const f32x2 be = {acc[2 + (k >> 1)][(2 * k) & 3], acc[2 + (k >> 1)][(2 * k + 1) & 3]};
+          const f32x2 A = fma2(gg, hh, be);
+          const f32x2 I = fma2(*reinterpret_cast<const f32x2*>(&s_gi[l * C + c]), hh,
+                               *reinterpret_cast<const f32x2*>(&s_bi[l * C + c]));
+          const f32x2 v = fma2(M2, I - A, A);
+          if constexpr (RELU) {
+            o[2 * k] = fmaxf(v.x, 0.f);
+            o[2 * k + 1] = fmaxf(v.y, 0.f);
+          } else {
+            o[2 * k] = v.x > 0.f ? v.x : v.x * a.slope;
+            o[2 * k + 1] = v.y > 0.f ? v.y : v.y * a.slope;
+          }
+        }
+        if (ZPM && ((ZPM >> l) & 1)) {
+          bf16x8 xf;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xf[e] = (bf16)o[e];
+          zp_mfma_half(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, sh, zacc, lr, lq);
+        } else {
+          store16_f(a.out[l] + p * a.ldo[l] + c0, o);
+        }
+      }
+      if (ZPM && ((ZPM >> l) & 1)) zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + p * 32, lq);
+    }
+  };
+
+  u32x4 zc[KS], zn[KS];
+  issue(0, zc, s_hA);
+  for (int i = 0; i < nw; ++i) {
+    unsigned char* cur = (i & 1) ? s_hB : s_hA;
+    unsigned char* nxt = (i & 1) ? s_hA : s_hB;
+    asm volatile("" ::: "memory");
+    u32x4 hc[2];
+    hload(i, cur, hc);
+    asm volatile("" ::: "memory");
+    if (i + 1 < nw) issue(i + 1, zn, nxt);
+    asm volatile("" ::: "memory");
+    compute(i, zc, hc);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) zc[ks] = zn[ks];
+  }
+  if (a.tclk && lane == 0) atomicMax(&a.tclk[1], (unsigned long long)wall_clock64());
+}
+
+// v5's row pairing holds for this source height in fp32 (PyTorch's index arithmetic, as up2x_tap): output
+// rows 2k-1, 2k share y0 = k-1 (k = 1 .. H-1); rows 0 and 2H-1 land exactly on source rows 0 and H-1
+static bool v5_pairing_ok(const Up2xSrc& u) {
+  auto y0f = [&](int oy, float* fr) {
+    volatile float r = u.sh * (float)oy;   // one fp32 multiply, as the kernel (no contraction)
+    const int y = (int)r;
+    if (fr) *fr = r - (float)y;
+    return y;
+  };
+  float f0, f1;
+  if (y0f(0, &f0) != 0 || f0 != 0.f || y0f(2 * u.H - 1, &f1) != u.H - 1 || f1 != 0.f) return false;
+  for (int k = 1; k < u.H; ++k)
+    if (y0f(2 * k - 1, nullptr) != k - 1 || y0f(2 * k, nullptr) != k - 1) return false;
+  return true;
 }
 
 // pixels per workgroup: one sample's block; C = 256 stages its weights once per 1024 pixels
@@ -612,10 +899,39 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
     a.up = up2x_src(d.up_H, d.up_W);
   }
   dim3 grid((unsigned)((long)d.B * d.HW / a.PPW));
+  if (d.version_out) *d.version_out = 3;
   static const int use_v4 = GHOST_KNOB("GHOST_AAD_V4", 1);
   // v4 (prefetching) only for the through-upsample form: measured B = 64, 256x256 L = 2: 724 vs 734 us
   // with the upsample, 604 vs 550 us without it (there v3's register loads win)
   static const unsigned dyn_lds = GHOST_KNOB("GHOST_AAD_DYNLDS", 0u);
+  a.tclk = d.tclk;
+  a.v5_xcd = GHOST_KNOB("GHOST_V5_XCD", 1);
+  static const int use_v5 = GHOST_KNOB("GHOST_AAD_V5", 0);
+  // v5: OW / 8 column tiles must divide the 64 tiles of a 1024-pixel workgroup (OW in {64 .. 512}) and the
+  // workgroups of an image must cover its H row tiles
+  const int v5_nct = 2 * d.up_W / 8, v5_rt = v5_nct > 0 && 64 % v5_nct == 0 ? 64 / v5_nct : 0;
+  if (use_v5 && up && d.C == 64 && a.PPW == 1024 && d.ldh % 8 == 0 && d.up_W % 4 == 0 && v5_rt >= 1 &&
+      v5_rt <= 8 && d.up_H % v5_rt == 0 && d.up_H >= 2 && v5_pairing_ok(a.up)) {
+#define GHOST_V5(ca, l)                                                                          \
+    if (d.Ca == ca && d.L == l && !zpm) {                                                        \
+      if (d.slope == 0.f)                                                                        \
+        hipLaunchKernelGGL((aad_v5_kernel<ca, l, true>), grid, dim3(kWaves * 64), 0, s, a);      \
+      else                                                                                       \
+        hipLaunchKernelGGL((aad_v5_kernel<ca, l, false>), grid, dim3(kWaves * 64), 0, s, a);     \
+      if (d.version_out) *d.version_out = 5;                                                     \
+      return (int)hipGetLastError();                                                             \
+    }
+    GHOST_V5(64, 1) GHOST_V5(64, 2) GHOST_V5(32, 1) GHOST_V5(32, 2)
+#undef GHOST_V5
+#define GHOST_V5Z(ca, zm)                                                                        \
+    if (d.Ca == ca && d.L == 2 && zpm == zm) {                                                   \
+      hipLaunchKernelGGL((aad_v5_kernel<ca, 2, true, zm>), grid, dim3(kWaves * 64), 0, s, a);    \
+      if (d.version_out) *d.version_out = 5;                                                     \
+      return (int)hipGetLastError();                                                             \
+    }
+    GHOST_V5Z(64, 1) GHOST_V5Z(64, 2) GHOST_V5Z(64, 3) GHOST_V5Z(32, 1) GHOST_V5Z(32, 2) GHOST_V5Z(32, 3)
+#undef GHOST_V5Z
+  }
   if (use_v4 && up && d.C == 64 && a.PPW % 256 == 0 && d.ldh % 8 == 0) {
 #define GHOST_V4(ca, l, u)                                                                       \
     if (d.Ca == ca && d.L == l && up == u && !zpm) {                                             \
@@ -623,6 +939,7 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
         hipLaunchKernelGGL((aad_v4_kernel<ca, l, u, true>), grid, dim3(kWaves * 64), dyn_lds, s, a); \
       else                                                                                       \
         hipLaunchKernelGGL((aad_v4_kernel<ca, l, u, false>), grid, dim3(kWaves * 64), dyn_lds, s, a); \
+      if (d.version_out) *d.version_out = 4;                                                     \
       return (int)hipGetLastError();                                                             \
     }
     GHOST_V4(64, 1, true) GHOST_V4(64, 2, true) GHOST_V4(32, 1, true) GHOST_V4(32, 2, true)
@@ -631,6 +948,7 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
 #define GHOST_V4Z(ca, zm)                                                                        \
     if (d.Ca == ca && d.L == 2 && zpm == zm) {                                                   \
       hipLaunchKernelGGL((aad_v4_kernel<ca, 2, true, true, zm>), grid, dim3(kWaves * 64), 0, s, a); \
+      if (d.version_out) *d.version_out = 4;                                                     \
       return (int)hipGetLastError();                                                             \
     }
     GHOST_V4Z(64, 1) GHOST_V4Z(64, 2) GHOST_V4Z(64, 3) GHOST_V4Z(32, 1) GHOST_V4Z(32, 2) GHOST_V4Z(32, 3)

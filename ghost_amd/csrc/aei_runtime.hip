@@ -70,11 +70,16 @@ struct ghost_aei {
   int id_total = 0;                            // sum over AAD layers of 2*c_x
   // per-handle plan options (ghost_aei_set_option); defaults are the measured choices
   int opt[GHOST_AEI_NOPT] = {1, 1, 1, GHOST_KNOB("GHOST_AAD_ZP", 2)};
-  // GHOST_AEI_OPT_TWO_STREAMS: the encoder up path's stream and its events (created on first use, on the
-  // device current then): zev[k] = z_attr_k written (k = 2..8), zev[0] = the down path done
-  hipStream_t s_up = nullptr;
-  int s_up_dev = -1;
-  hipEvent_t zev[9] = {nullptr};
+  // GHOST_AEI_OPT_TWO_STREAMS: the encoder up path's stream and its events, one set per device (created
+  // on first use on the device of the caller's stream): zev[k] = z_attr_k written (k = 2..8), zev[0] = the
+  // down path done, zev[1] = idgb / m1 ready; zend = everything this call queued on the up stream
+  struct UpPath {
+    hipStream_t s = nullptr;
+    hipEvent_t zev[9] = {nullptr};
+    hipEvent_t zend = nullptr;
+  };
+  std::map<int, UpPath> up_path;
+  hipEvent_t* zev = nullptr;                   // the events of the device of the running call
   void* taps[8] = {nullptr};                   // ghost_aei_set_taps: AADBlk1..7 outputs copied here
   // profiling
   int prof_mask = 0;
@@ -83,6 +88,12 @@ struct ghost_aei {
   std::vector<Pending> pend;
   int ev_used = 0;
   ProfClass prof[8];
+  // in-kernel clock of the roofline kernel's launches (profiling class 1, the v5 AAD kernel): per launch
+  // [earliest workgroup start, latest wave end] in wall-clock ticks; device buffer of clk_cap pairs
+  unsigned long long* clk = nullptr;
+  int clk_cap = 0, clk_n = 0, clk_dev = -1;
+  int roof_version = 0;                        // kernel generation of class 1's last launch (aad_v3.h)
+  unsigned long long* next_clk() { return (clk && clk_n < clk_cap) ? clk + 2 * clk_n++ : nullptr; }
 
   typedef int Pair[2];
   typedef int Triple[3];
@@ -114,6 +125,7 @@ struct Ctx {
   // two-stream plan: the up path's stream and its own scratch region (the launches of the two streams
   // overlap, so they cannot share the split-K / statistics partials)
   bool dual = false, force_single = false;
+  int dev = 0;
   hipStream_t s_up = nullptr;
   char* scratch_up = nullptr;
   int rc = 0;
@@ -559,6 +571,8 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     int e_all = c.prof_begin(0);
     // class 1: the block-input AAD kernel at 256x256 (reads h_in through the x2 upsample; one or two layers)
     int e_big = (n == 256 && up_src) ? c.prof_begin(1) : -1;
+    if (e_big >= 0 && h->clk_dev == c.dev) d.tclk = h->next_clk();
+    if (e_big >= 0) d.version_out = &h->roof_version;
     c.check(aad_v3(d, c.s), "aad_v3");
     if (e_big >= 0) c.prof_end(1, e_big, bytes, flops);
     if (e_all >= 0) c.prof_end(0, e_all, bytes, flops);
@@ -901,8 +915,13 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
   if (!c.dual) prologue();
   void* y = (mode == M_SWAP) ? c.alloc((size_t)B * 256 * 256 * 3 * es) : io.y;
   generator(c, B, attr, gin, y, io.u8);
-  // the caller's stream waits for everything the up-path stream did (also when a launch failed midway)
-  if (c.dual && !c.dry) (void)hipStreamWaitEvent(c.s, h->zev[8], 0);
+  // the caller's stream waits for everything this call queued on the up-path stream, also when a launch
+  // failed midway (a fresh record: zev[8] may still hold the previous call's record then)
+  if (c.dual && !c.dry) {
+    const bool rec = hipEventRecord(h->up_path[c.dev].zend, c.s_up) == hipSuccess;
+    if (rec) (void)hipStreamWaitEvent(c.s, h->up_path[c.dev].zend, 0);
+    else (void)hipStreamSynchronize(c.s_up);
+  }
 }
 
 // the one-stream fallback of a two-stream plan allocates in another order: alignment padding may differ
@@ -921,25 +940,51 @@ int64_t plan_bytes(ghost_aei* h, Mode mode, int B) {
   return (int64_t)(((c.off + 255) & ~size_t(255)) + kMainSlack + (c.dual ? 2 : 1) * scr + 256);
 }
 
-// the handle's up-path stream and events on the current device (created once); false: run on one stream
-bool ensure_up_stream(ghost_aei* h) {
-  int dev = -1;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (h->s_up && h->s_up_dev == dev) return true;
-  if (h->s_up) return false;   // created on another device: this call runs on one stream
+// the handle's up-path stream and events on device `dev` (the current device; created once per device);
+// false: this call runs on one stream
+bool ensure_up_stream(ghost_aei* h, int dev) {
+  auto it = h->up_path.find(dev);
+  if (it != h->up_path.end()) return it->second.s != nullptr;
+  ghost_aei::UpPath& u = h->up_path[dev];   // a failed creation leaves a null stream: one stream from then on
   // the up path fills the CUs the generator's small low-resolution launches leave idle: its stream gets
   // the lowest priority, so the generator's workgroups dispatch first when both streams have work
   static const int low_prio = GHOST_KNOB("GHOST_UP_STREAM_LOWPRIO", 1);
   int least = 0, greatest = 0;
   if (!low_prio || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
-  hipStream_t st;
-  if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least) != hipSuccess) return false;
-  for (auto& e : h->zev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return false;
-  h->s_up = st;
-  h->s_up_dev = dev;
+  ghost_aei::UpPath tmp;
+  bool ok = hipStreamCreateWithPriority(&tmp.s, hipStreamNonBlocking, least) == hipSuccess;
+  for (auto& e : tmp.zev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&tmp.zend, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    for (auto e : tmp.zev)
+      if (e) (void)hipEventDestroy(e);
+    if (tmp.zend) (void)hipEventDestroy(tmp.zend);
+    if (tmp.s) (void)hipStreamDestroy(tmp.s);
+    return false;
+  }
+  u = tmp;
   return true;
 }
+
+// makes the device of the caller's stream current for the duration of a call (every launch, the up-path
+// stream and its events then live on the stream's device, whatever device the caller had current)
+struct DeviceGuard {
+  int prev = -1, dev = -1;
+  bool ok = false;
+  explicit DeviceGuard(hipStream_t s) {
+    if (hipGetDevice(&prev) != hipSuccess) return;
+    dev = prev;
+    if (s) {
+      hipDevice_t d;
+      if (hipStreamGetDevice(s, &d) != hipSuccess) return;
+      dev = (int)d;
+    }
+    ok = dev == prev || hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (ok && dev != prev) (void)hipSetDevice(prev);
+  }
+};
 
 int run(ghost_aei* h, Mode mode, int B, const Io& io, void* ws, int64_t ws_bytes, void* stream) {
   if (int rc = check_handle(h)) return rc;
@@ -960,8 +1005,12 @@ int run(ghost_aei* h, Mode mode, int B, const Io& io, void* ws, int64_t ws_bytes
   c.scratch = c.base + main_bytes;
   c.scratch_cap = dry.scratch_need;
   c.s = (hipStream_t)stream;
-  if (dry.dual && ensure_up_stream(h)) {
-    c.s_up = h->s_up;
+  DeviceGuard guard(c.s);
+  if (!guard.ok) return fail(GHOST_EINVAL, "cannot make the device of the caller's stream current");
+  c.dev = guard.dev;
+  if (dry.dual && ensure_up_stream(h, c.dev)) {
+    c.s_up = h->up_path[c.dev].s;
+    h->zev = h->up_path[c.dev].zev;
     c.scratch_up = c.scratch + scr;
   }
   c.force_single = !c.s_up;   // no second stream on this device: the same plan on one stream
@@ -998,9 +1047,13 @@ extern "C" int ghost_aei_create(const char* backbone, int num_blocks, int c_id, 
 extern "C" void ghost_aei_destroy(ghost_aei* h) {
   if (!h) return;
   for (auto e : h->ev) (void)hipEventDestroy(e);
-  for (auto e : h->zev)
-    if (e) (void)hipEventDestroy(e);
-  if (h->s_up) (void)hipStreamDestroy(h->s_up);
+  if (h->clk) (void)hipFree(h->clk);
+  for (auto& kv : h->up_path) {
+    for (auto e : kv.second.zev)
+      if (e) (void)hipEventDestroy(e);
+    if (kv.second.zend) (void)hipEventDestroy(kv.second.zend);
+    if (kv.second.s) (void)hipStreamDestroy(kv.second.s);
+  }
   delete h;
 }
 
@@ -1092,6 +1145,54 @@ extern "C" int ghost_aei_profile(ghost_aei* h, int class_mask) {
   h->pend.clear();
   h->ev_used = 0;
   for (auto& p : h->prof) p = ProfClass{};
+  h->clk_n = 0;
+  if (class_mask & 2) {   // class 1: arm the in-kernel clock (buffer on the current device)
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(GHOST_EINVAL, "hipGetDevice failed");
+    if (h->clk && h->clk_dev != dev) {
+      (void)hipFree(h->clk);
+      h->clk = nullptr;
+    }
+    if (!h->clk) {
+      h->clk_cap = 4096;
+      if (hipMalloc(&h->clk, sizeof(unsigned long long) * 2 * h->clk_cap) != hipSuccess) {
+        h->clk = nullptr;
+        return fail(GHOST_EINVAL, "clock buffer allocation failed");
+      }
+      h->clk_dev = dev;
+    }
+    std::vector<unsigned long long> init(2 * h->clk_cap);
+    for (int i = 0; i < h->clk_cap; ++i) {
+      init[2 * i] = ~0ull;
+      init[2 * i + 1] = 0;
+    }
+    if (hipMemcpy(h->clk, init.data(), init.size() * sizeof(init[0]), hipMemcpyHostToDevice) != hipSuccess)
+      return fail(GHOST_EINVAL, "clock buffer reset failed");
+  }
+  return 0;
+}
+
+extern "C" int ghost_aei_profile_clock(ghost_aei* h, double* us_total, int64_t* launches, int* kernel_version) {
+  if (!h || !us_total || !launches) return fail(GHOST_EINVAL, "null argument");
+  *us_total = 0;
+  *launches = 0;
+  if (kernel_version) *kernel_version = h->roof_version;
+  if (!h->clk || h->clk_n == 0) return 0;
+  std::vector<unsigned long long> v(2 * h->clk_n);
+  if (hipMemcpy(v.data(), h->clk, v.size() * sizeof(v[0]), hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(GHOST_EINVAL, "clock buffer read failed");
+  int rate_khz = 0;
+  if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, h->clk_dev) != hipSuccess || rate_khz <= 0)
+    return fail(GHOST_EINVAL, "wall clock rate unavailable");
+  double ticks = 0;
+  int64_t n = 0;
+  for (int i = 0; i < h->clk_n; ++i) {
+    if (v[2 * i] == ~0ull || v[2 * i + 1] < v[2 * i]) continue;   // a launch that did not run the clocked kernel
+    ticks += (double)(v[2 * i + 1] - v[2 * i]);
+    ++n;
+  }
+  *us_total = ticks / (rate_khz * 1e-3);
+  *launches = n;
   return 0;
 }
 

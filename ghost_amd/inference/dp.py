@@ -7,12 +7,14 @@ per-sample InstanceNorm), so the build shards them:
 * rank r of W swaps the contiguous block of present crops ``[r*S, min(N, (r+1)*S))`` with
   ``S = ceil(N / W)`` (the last block padded to S so every rank contributes equal bytes);
 * one all-gather over the process group (RCCL over xGMI on MI355X, gloo in the CPU tests)
-  returns every rank's uint8 swaps; because blocks are contiguous and gathered in rank
-  order, trimming the padding restores frame order exactly;
+  returns every rank's uint8 swaps — or, for the video mux, one gather to rank 0 only (the
+  reference writes the video from one process, core.py:72-88; the other ranks then copy nothing
+  to the host); because blocks are contiguous and gathered in rank order, trimming the padding
+  restores frame order exactly;
 * the ``present`` bookkeeping of core.py:79-88 then re-inserts ``[]`` for frames without
   a face, bit-exactly as the single-GPU path.
 
-No collective other than that all-gather is on the data path.
+No collective other than that all-gather (or gather) is on the data path.
 """
 from __future__ import annotations
 
@@ -32,11 +34,21 @@ def shard_bounds(n: int, world: int, rank: int):
     return start, min(n, start + per), per
 
 
-def gather_frames(local: torch.Tensor, per: int, n: int, group=None) -> torch.Tensor:
-    """All-gather each rank's [<=per, ...] uint8 block (padded to per) and return the first n rows in order."""
+def gather_frames(local: torch.Tensor, per: int, n: int, group=None, dst: Optional[int] = None):
+    """Collect each rank's [<=per, ...] uint8 block (padded to per) and return the first n rows in frame
+    order.  ``dst=None``: an all-gather, every rank returns the n rows.  ``dst=r``: a gather to rank r
+    only (the video mux rank, core.py:72-88 writes the frames on one process), which returns the n rows
+    there and ``None`` on every other rank."""
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[:local.shape[0]] = local
+    if dst is not None:
+        out = (torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+               if rank == dst else None)
+        dist.gather(pad, list(out.chunk(world)) if out is not None else None, dst=_global_rank(group, dst),
+                    group=group)
+        return out[:n] if out is not None else None
     if dist.get_backend(group) == "nccl":
         out = torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(out, pad, group=group)
@@ -47,26 +59,38 @@ def gather_frames(local: torch.Tensor, per: int, n: int, group=None) -> torch.Te
     return out[:n]
 
 
+def _global_rank(group, r: int) -> int:
+    return r if group is None else dist.get_global_rank(group, r)
+
+
 def swap_frames_dp(crops: torch.Tensor, swap: Callable[[torch.Tensor], torch.Tensor], BS: int = 64,
-                   group=None) -> torch.Tensor:
+                   group=None, dst: Optional[int] = None):
     """Shard N crops [N,256,256,3] (uint8, identical on every rank) over the group, swap this
-    rank's block in batches of BS with ``swap`` (crops -> uint8 swaps), all-gather; every rank
-    returns the N swapped crops in frame order."""
+    rank's block in batches of BS with ``swap`` (crops -> uint8 swaps), then collect: every rank
+    returns the N swapped crops in frame order (``dst=None``, all-gather), or only rank ``dst`` does
+    and the others return ``None`` (gather)."""
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     n = crops.shape[0]
     start, end, per = shard_bounds(n, world, rank)
     outs = [swap(crops[i:min(end, i + BS)]) for i in range(start, end, BS)]
     local = torch.cat(outs, 0) if outs else crops[:0].clone()
-    return gather_frames(local, per, n, group)
+    return gather_frames(local, per, n, group, dst)
 
 
 def model_inference_dp(resized_frs: np.ndarray, present: Sequence[int], source_embed: torch.Tensor, G,
-                       BS: int = 64, device=None, group=None) -> List:
-    """core.py:57-88 for one identity, data-parallel over the group: returns the per-frame list
-    (swapped crop or ``[]``) on every rank."""
+                       BS: int = 64, device=None, group=None, collect: str = "rank0") -> Optional[List]:
+    """core.py:57-88 for one identity, data-parallel over the group.  ``collect="rank0"`` (default): the
+    swapped crops are gathered to rank 0 only, which copies them to the host and returns the per-frame
+    list (swapped crop or ``[]``) for the video mux; every other rank returns ``None`` and copies nothing
+    to the host.  ``collect="all"``: all-gather, every rank returns the list."""
+    if collect not in ("rank0", "all"):
+        raise ValueError(f"ghost_amd: collect must be 'rank0' or 'all', got {collect!r}")
     device = torch.device(device or "cuda")
     crops = torch.from_numpy(np.ascontiguousarray(resized_frs)).to(device)
-    gathered = swap_frames_dp(crops, lambda c: G.swap_u8(c, source_embed), BS, group)
+    gathered = swap_frames_dp(crops, lambda c: G.swap_u8(c, source_embed), BS, group,
+                              dst=0 if collect == "rank0" else None)
+    if gathered is None:
+        return None
     return reinsert_present(gathered.cpu().numpy(), present)
 
 
@@ -111,7 +135,7 @@ class GatherPipeline:
     """
 
     def __init__(self, swap: Callable, batch_shape, device, dtype=torch.uint8, group=None, depth: int = 2,
-                 streams: int = 1):
+                 streams: int = 1, dst: Optional[int] = None):
         self.nstreams = max(1, int(streams))
         depth = max(1, depth)
         depth = (depth + self.nstreams - 1) // self.nstreams * self.nstreams
@@ -127,8 +151,12 @@ class GatherPipeline:
         shape = tuple(batch_shape)
         self.rows = shape[0]
         self.outs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(self.depth)]
+        # dst: gather to that rank only (the video mux rank); the other ranks keep no gather buffers and
+        # their ``result`` is None
+        self.dst = dst
+        self.receiver = dst is None or self.rank == dst
         self.gath = ([torch.empty((self.world * shape[0],) + shape[1:], dtype=dtype, device=device)
-                      for _ in range(self.depth)] if self.world > 1 else self.outs)
+                      if self.receiver else None for _ in range(self.depth)] if self.world > 1 else self.outs)
         self.pending: List[Optional[object]] = [None] * self.depth
         self.gen = [0] * self.depth
         self.k = 0
@@ -160,7 +188,12 @@ class GatherPipeline:
             self._wait(slot)                      # the collective still reading this slot's buffer
             if n:
                 self.swap(crops, self.outs[slot][:n])
-            if self.world > 1:
+            if self.world > 1 and self.dst is not None:
+                g = self.gath[slot]
+                self.pending[slot] = dist.gather(self.outs[slot], list(g.chunk(self.world)) if g is not None else None,
+                                                 dst=_global_rank(self.group, self.dst), group=self.group,
+                                                 async_op=True)
+            elif self.world > 1:
                 if self.nccl:
                     self.pending[slot] = dist.all_gather_into_tensor(self.gath[slot], self.outs[slot],
                                                                      group=self.group, async_op=True)
@@ -185,6 +218,8 @@ class GatherPipeline:
         if self.done[ticket.slot] is not None:
             torch.cuda.current_stream(self.device).wait_event(self.done[ticket.slot])
         g = self.gath[ticket.slot]
+        if g is None:         # gather to another rank
+            return None
         if all(c == self.rows for c in ticket.counts):
             return g
         return torch.cat([g[r * self.rows:r * self.rows + c] for r, c in enumerate(ticket.counts)])

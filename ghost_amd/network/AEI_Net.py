@@ -29,6 +29,7 @@ import torch
 import torch.nn as nn
 
 from .. import _lib
+from .._packed import PackedModule, WorkspaceCache
 from .AADLayer import AAD_ResBlk, AADLayer, AddBlocksSequential  # noqa: F401  (reference re-exports)
 from .pack import pack_all
 from .resnet import MLAttrEncoderResnet
@@ -148,11 +149,22 @@ class _Runtime:
             _lib.check(-2, "weights incomplete")
         for name, v in (options or {}).items():
             _lib.check(self.lib.ghost_aei_set_option(h, OPTIONS[name], int(v)), f"option {name}")
+        self.ws = WorkspaceCache()   # (mode, B, stream) -> workspace (stream-ordered reuse)
         self.geom = []
         for k in range(1, 9):
             c_, h_, w_ = C.c_int(), C.c_int(), C.c_int()
             _lib.check(self.lib.ghost_aei_attr_geometry(h, k, C.byref(c_), C.byref(h_), C.byref(w_)))
             self.geom.append((c_.value, h_.value, w_.value))
+
+    def workspace(self, mode: str, B: int, dev: torch.device, stream: int) -> torch.Tensor:
+        fn = self.lib.ghost_aei_swap_workspace_bytes if mode == "swap" else self.lib.ghost_aei_workspace_bytes
+
+        def nbytes():
+            n = fn(self.h, B)
+            if n < 0:
+                _lib.check(int(n), "workspace sizing")
+            return n
+        return self.ws.get((mode, B, stream), nbytes, dev)
 
     def __del__(self):
         try:
@@ -162,7 +174,7 @@ class _Runtime:
             pass
 
 
-class AEI_Net(nn.Module):
+class AEI_Net(PackedModule):
     """AEI_Net(backbone, num_blocks=2, c_id=256)  (AEI_Net.py:143-159)."""
 
     def __init__(self, backbone, num_blocks=2, c_id=256, *, compute_dtype: Optional[torch.dtype] = None):
@@ -178,11 +190,10 @@ class AEI_Net(nn.Module):
         else:
             raise ValueError(f"unknown backbone {backbone!r}")
         self.generator = AADGenerator(backbone, c_id, num_blocks)
-        self._rt = None
-        self._rt_sig = None
         self._options = {}
         import weakref
         self.encoder._owner = weakref.ref(self)
+        self._init_packed()
 
     # -- weights -------------------------------------------------------------------
     def _dtype(self) -> torch.dtype:
@@ -204,6 +215,7 @@ class AEI_Net(nn.Module):
         self._options[name] = int(value)
         if self._rt is not None:
             _lib.check(self._rt.lib.ghost_aei_set_option(self._rt.h, OPTIONS[name], int(value)), f"option {name}")
+            self._rt.ws.clear()   # the plan (and so its workspace size) depends on the options
 
     def get_option(self, name: str) -> int:
         """The plan option's value in effect (the handle's, once a forward has created it)."""
@@ -218,18 +230,12 @@ class AEI_Net(nn.Module):
         raise RuntimeError("ghost_amd: option defaults live in the native handle; run a forward first")
 
     def _runtime(self, device) -> _Runtime:
+        """The packed runtime for (device, dtype) (_packed.PackedModule: re-packed after load_state_dict,
+        .to/.half, or an in-place change of any parameter or buffer)."""
         dt = self._dtype()
-        sig = (device, dt) + tuple((t.data_ptr(), t._version) for t in self.state_dict().values())
-        if self._rt is None or self._rt_sig != sig:
-            sd = {k: v.detach() for k, v in self.state_dict().items()}
-            for k, v in sd.items():
-                if v.is_floating_point() and v.device != device:
-                    raise RuntimeError(f"ghost_amd: parameter {k} is on {v.device}, input on {device}")
-            with torch.no_grad():
-                slots = pack_all(sd, self.backbone, self.num_blocks, self.c_id, dt)
-            self._rt = _Runtime(self.backbone, self.num_blocks, self.c_id, dt, slots, self._options)
-            self._rt_sig = sig
-        return self._rt
+        return self._cached_runtime(device, dt, lambda sd: _Runtime(
+            self.backbone, self.num_blocks, self.c_id, dt, pack_all(sd, self.backbone, self.num_blocks, self.c_id, dt),
+            self._options))
 
     # -- execution -----------------------------------------------------------------
     def _prep(self, Xt, what):
@@ -269,10 +275,8 @@ class AEI_Net(nn.Module):
                                    or not out_u8.is_contiguous() or out_u8.device != dev):
             raise RuntimeError("ghost_amd: out_u8 must be a contiguous uint8 [B,256,256,3] tensor on the input device")
         lib = rt.lib
-        nbytes = lib.ghost_aei_workspace_bytes(rt.h, B)
-        if nbytes < 0:
-            _lib.check(int(nbytes), "workspace sizing")
-        ws = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
+        stream = _lib.stream_ptr(dev)
+        ws = rt.workspace("forward", B, dev, stream)
         ap = (C.c_void_p * 8)(*[a.data_ptr() for a in attrs])
         blocks = []
         if taps:
@@ -283,7 +287,7 @@ class AEI_Net(nn.Module):
             _lib.check(lib.ghost_aei_forward(rt.h, Xt.data_ptr(), _lib.gdtype(Xt.dtype), st, B, z.data_ptr(),
                                              _lib.gdtype(z.dtype), z.stride(0), Y.data_ptr(),
                                              out_u8.data_ptr() if out_u8 is not None else None, ap, ws.data_ptr(),
-                                             ws.numel(), _lib.stream_ptr(dev)), "AEI_Net.forward")
+                                             ws.numel(), stream), "AEI_Net.forward")
         finally:
             if taps:
                 lib.ghost_aei_set_taps(rt.h, None)
@@ -298,13 +302,11 @@ class AEI_Net(nn.Module):
     def get_attr(self, X):
         rt, B, attrs, st = self._prep(X, "AEI_Net.get_attr")
         lib = rt.lib
-        nbytes = lib.ghost_aei_workspace_bytes(rt.h, B)
-        if nbytes < 0:
-            _lib.check(int(nbytes), "workspace sizing")
-        ws = torch.empty(int(nbytes), dtype=torch.uint8, device=X.device)
+        stream = _lib.stream_ptr(X.device)
+        ws = rt.workspace("forward", B, X.device, stream)
         ap = (C.c_void_p * 8)(*[a.data_ptr() for a in attrs])
         _lib.check(lib.ghost_aei_get_attr(rt.h, X.data_ptr(), _lib.gdtype(X.dtype), st, B, ap, ws.data_ptr(),
-                                          ws.numel(), _lib.stream_ptr(X.device)), "AEI_Net.get_attr")
+                                          ws.numel(), stream), "AEI_Net.get_attr")
         od = self._out_dtype(rt)
         return tuple(a.permute(0, 3, 1, 2).to(od) for a in attrs)
 
@@ -335,13 +337,11 @@ class AEI_Net(nn.Module):
             raise RuntimeError(f"ghost_amd: out must be a contiguous uint8 [{B},256,256,3] tensor on {dev}, got "
                                f"{out.dtype} {tuple(out.shape)} on {out.device}")
         lib = rt.lib
-        nbytes = lib.ghost_aei_swap_workspace_bytes(rt.h, B)
-        if nbytes < 0:
-            _lib.check(int(nbytes), "workspace sizing")
-        ws = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
+        stream = _lib.stream_ptr(dev)
+        ws = rt.workspace("swap", B, dev, stream)
         _lib.check(lib.ghost_aei_swap_u8(rt.h, crops_u8.data_ptr(), crops_u8.stride(0), B, z.data_ptr(),
                                          _lib.gdtype(z.dtype), zrs, out.data_ptr(), ws.data_ptr(), ws.numel(),
-                                         _lib.stream_ptr(dev)), "AEI_Net.swap_u8")
+                                         stream), "AEI_Net.swap_u8")
         return out
 
     def profile(self, class_mask: int):
@@ -350,6 +350,20 @@ class AEI_Net(nn.Module):
         if rt is None:
             raise RuntimeError("ghost_amd: run one forward before enabling profiling")
         _lib.check(rt.lib.ghost_aei_profile(rt.h, class_mask))
+
+    def profile_clock(self):
+        """Class 1's in-kernel clock: (total microseconds of kernel execution span, launches)."""
+        rt = self._rt
+        us, n = C.c_double(), C.c_int64()
+        _lib.check(rt.lib.ghost_aei_profile_clock(rt.h, C.byref(us), C.byref(n), None))
+        return us.value, n.value
+
+    def kernel_variant(self, what: str = "aad_dual_256") -> str:
+        """Which generation of the profiled roofline AAD kernel ran last ('v4' / 'v5')."""
+        rt = self._rt
+        us, n, v = C.c_double(), C.c_int64(), C.c_int()
+        _lib.check(rt.lib.ghost_aei_profile_clock(rt.h, C.byref(us), C.byref(n), C.byref(v)))
+        return f"v{v.value}"
 
     def profile_read(self, cls: int):
         rt = self._rt

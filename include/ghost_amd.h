@@ -119,6 +119,12 @@ int ghost_aei_set_taps(ghost_aei* h, void* const taps[8]);
 int ghost_aei_profile(ghost_aei* h, int class_mask);
 /* after the stream is synchronised: total ms, launches, algorithmic bytes and flops of class i */
 int ghost_aei_profile_read(ghost_aei* h, int cls, double* ms, int64_t* launches, double* bytes, double* flops);
+/* class 1's in-kernel clock (armed by ghost_aei_profile with bit 1 set, on the current device): the sum over
+ * its launches since then of (latest wave end - earliest workgroup start), in microseconds, read from the
+ * kernel's own wall-clock stamps (hipDeviceAttributeWallClockRate) — the kernel's execution span, which
+ * unlike a HIP-event bracket does not include queueing behind other streams' kernels.  After a sync.
+ * kernel_version (may be NULL): generation of the class-1 AAD kernel that ran last (4: aad_v4, 5: aad_v5). */
+int ghost_aei_profile_clock(ghost_aei* h, double* us_total, int64_t* launches, int* kernel_version);
 
 /* ---- single operators (NHWC, per-op parity tests and callers of single layers) ------ */
 /* Conv2d kh x kw / stride / pad (+ per-channel scale/shift, leaky slope, residual, tanh).

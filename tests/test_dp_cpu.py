@@ -156,3 +156,170 @@ def test_reinsert_present_matches_reference_bookkeeping():
     present = [1, 0, 0, 1, 1, 0]
     frames = reinsert_present(out, present)
     assert [f if isinstance(f, list) else f.tolist() for f in frames] == [[0, 1], [], [], [2, 3], [4, 5], []]
+
+
+class _FakeG:
+    """Stand-in for AEI_Net.swap_u8 on CPU tensors (the GPU swap is covered by the -m gpu tests)."""
+
+    def swap_u8(self, crops, z, out=None):
+        y = fake_swap(crops)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+
+def _mux_worker(rank, world, port, collect, q):
+    from ghost_amd.inference import dp
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    host_copies = []
+    orig_cpu = torch.Tensor.cpu
+
+    def spy_cpu(self, *a, **k):   # every device->host copy model_inference_dp makes on this rank
+        host_copies.append(tuple(self.shape))
+        return orig_cpu(self, *a, **k)
+    try:
+        g = np.random.Generator(np.random.PCG64(11))
+        present = [1, 0, 1, 1, 0, 1, 1, 1, 0]
+        frs = g.integers(0, 256, size=(sum(present), 4, 4, 3), dtype=np.uint8)
+        torch.Tensor.cpu = spy_cpu
+        try:
+            out = dp.model_inference_dp(frs, present, torch.zeros(1, 512), _FakeG(), BS=2, device="cpu",
+                                        collect=collect)
+        finally:
+            torch.Tensor.cpu = orig_cpu
+        q.put((rank, None if out is None else [f if isinstance(f, list) else f.tolist() for f in out], host_copies))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("collect", ["rank0", "all"])
+def test_model_inference_dp_rank0_mux_gloo(collect):
+    """core.py:72-88 data-parallel: with collect='rank0' only rank 0 receives the swapped crops and
+    copies them to the host (the video mux rank), in frame order with [] re-inserted; rank 1 returns
+    None and makes no host copy.  collect='all' gives every rank the list."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mux_worker, args=(r, world, port, collect, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {r: (out, cp) for r, out, cp in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = np.random.Generator(np.random.PCG64(11))
+    present = [1, 0, 1, 1, 0, 1, 1, 1, 0]
+    frs = g.integers(0, 256, size=(sum(present), 4, 4, 3), dtype=np.uint8)
+    sw = fake_swap(torch.from_numpy(frs)).numpy()
+    expect = [f if isinstance(f, list) else f.tolist() for f in reinsert_present(sw, present)]
+    assert results[0][0] == expect
+    assert len(results[0][1]) == 1           # one D2H of the gathered crops
+    if collect == "rank0":
+        assert results[1] == (None, [])
+    else:
+        assert results[1][0] == expect
+
+
+def _bench_worker(rank, world, port, q):
+    import time as _t
+    import bench
+    from ghost_amd.inference.dp import GatherPipeline
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B, steps, warmup = 3, 4, 2
+        calls = []
+
+        def swap(c, o):       # rank 1 is slower: the reported time must be rank 1's (max over ranks)
+            calls.append(1)
+            _t.sleep(0.02 * (rank + 1))
+            o.copy_(fake_swap(c))
+        pipe = GatherPipeline(swap, (B, 4, 4, 3), torch.device("cpu"), depth=2)
+        crops = torch.full((B, 4, 4, 3), rank, dtype=torch.uint8)
+        marks = []
+        t0 = _t.perf_counter()
+        el = bench.timed_region(lambda: pipe.submit(crops), pipe.drain, steps, warmup, world, torch.device("cpu"),
+                                lambda: marks.append(len(calls)))
+        total = _t.perf_counter() - t0
+        rec = bench.headline_record(world, B, steps, warmup, el, "unet", 2, 1, "bf16", 1)
+        q.put((rank, el, total, len(calls), marks, rec))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_multi_rank_reporting_gloo():
+    """bench.py's N > 1 path with a stand-in swap (gloo world 2): W warm-up steps before the timed region,
+    exactly K inside, the reported time is the max over ranks (identical on every rank, >= the slow rank's
+    K steps), value = all ranks' frames / that time, global_batch = N*B, parallelism dpN."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (el0, tot0, n0, m0, rec0), (el1, tot1, n1, m1, rec1) = res[0], res[1]
+    assert el0 == el1                         # all-reduce MAX: one time for the job
+    assert el1 >= 4 * 0.04 * 0.9              # rank 1's four timed steps at 40 ms each
+    assert n0 == n1 == 6 and m0 == m1 == [2]  # 2 warm-up steps, then exactly 4 timed
+    assert rec0 == rec1
+    assert rec0["n_gpus"] == 2 and rec0["config"]["global_batch"] == 6 and rec0["config"]["parallelism"] == "dp2"
+    assert rec0["scaling"] == "weak" and rec0["steps"] == 4 and rec0["warmup"] == 2
+    assert abs(rec0["value"] - 2 * 3 * 4 / el0) < 0.01 * rec0["value"]
+    assert "all-gather" in rec0["config"]["workload"]
+
+
+def _pipe_dst_worker(rank, world, port, q):
+    from ghost_amd.inference.dp import GatherPipeline
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B = 2
+        pipe = GatherPipeline(lambda c, o: o.copy_(fake_swap(c)), (B, 4, 4, 3), torch.device("cpu"), depth=2, dst=0)
+        outs = []
+        prev = None
+        for k in range(4):
+            t = pipe.submit(torch.full((B, 4, 4, 3), 10 * k + rank, dtype=torch.uint8))
+            if prev is not None:
+                r = pipe.result(prev)
+                outs.append(None if r is None else r.clone().numpy())
+            prev = t
+        r = pipe.result(prev)
+        outs.append(None if r is None else r.clone().numpy())
+        pipe.drain()
+        q.put((rank, outs, pipe.gath[0] is None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_pipeline_dst_rank0_gloo():
+    """GatherPipeline(dst=0): batches stream to rank 0 only, in rank order; the other rank holds no
+    gather buffers and reads None."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_dst_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (o, nob) for r, o, nob in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    outs0, nobuf0 = res[0]
+    outs1, nobuf1 = res[1]
+    assert not nobuf0 and nobuf1
+    assert outs1 == [None] * 4
+    for k in range(4):
+        expect = torch.cat([fake_swap(torch.full((2, 4, 4, 3), 10 * k + rr, dtype=torch.uint8)) for rr in range(world)])
+        assert np.array_equal(outs0[k], expect.numpy()), k
