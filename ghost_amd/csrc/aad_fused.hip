@@ -141,16 +141,16 @@ __global__ void __launch_bounds__(256) aad_fused_kernel(const AadArgs a) {
       const T* Ab = As + (wm * (BM / 2) + lr) * LDR;
       const T* Bb = Bs + (wn * (BN / 2) + lr) * LDR;
       if constexpr (sizeof(T) == 2) {
-        bf16x8 af[TM], bfv[TN];
+        v8_t<T> af[TM], bfv[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * LDR + lq * 8);
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const v8_t<T>*>(Ab + i * 16 * LDR + lq * 8);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * LDR + lq * 8);
+        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const v8_t<T>*>(Bb + j * 16 * LDR + lq * 8);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16x16x32<T>(af[i], bfv[j], acc[i][j]);
       } else {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -256,6 +256,9 @@ int aad_fused(int dt, const void* za, int lda, int Ca, const void* w, int Kpad, 
   if (dt == GHOST_BF16) {
     const size_t lds = lds_bytes<bf16, BM>(C);
     hipLaunchKernelGGL((aad_fused_kernel<bf16, BM>), grid, dim3(256), lds, s, a);
+  } else if (dt == GHOST_F16) {
+    const size_t lds = lds_bytes<_Float16, BM>(C);
+    hipLaunchKernelGGL((aad_fused_kernel<_Float16, BM>), grid, dim3(256), lds, s, a);
   } else if (dt == GHOST_F32) {
     const size_t lds = lds_bytes<float, BM>(C);
     hipLaunchKernelGGL((aad_fused_kernel<float, BM>), grid, dim3(256), lds, s, a);

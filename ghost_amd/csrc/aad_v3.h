@@ -5,6 +5,7 @@
 namespace ghost {
 
 struct AadV3Desc {
+  int dt = 1;                                        // storage type: GHOST_BF16 (1) or GHOST_F16 (2)
   const void* za = nullptr;  int lda = 0, Ca = 0;   // z_attr NHWC
   const void* hin = nullptr; int ldh = 0;           // h_in NHWC (shared by the L layers)
   // up_H > 0: h_in = upsample2x(hin) (bilinear x2, align_corners) with hin the [B, up_H, up_W]
@@ -27,15 +28,18 @@ struct AadV3Desc {
   // layout's K slice of this layer's channels); out[l] is then that [B*HW][32] fp16 buffer
   const void* zw[2] = {nullptr, nullptr};
   int zwld = 0;
-  // in-kernel clock of the launch (profiling; the v5 kernel): [0] earliest start, [1] latest end
+  // in-kernel clock of the launch (profiling; v4 / v5): aad_v3_clock_words(d) words of per-workgroup start
+  // and per-wave end stamps
   unsigned long long* tclk = nullptr;
   int* version_out = nullptr;   // set to the kernel generation that ran (3, 4 or 5)
 };
 
 // the 3x3 / pad 1 conv to 3 channels from two tap-partial buffers (AADBlk8's output conv over
 // cat(h, x'), AADLayer.py:71,79): y = tanh(sum_t (zh + zx)[p + off_t][t*3 + o]) -> bf16 y (ldy) + BGR uint8
-int tap_sum3x3(const void* zh, const void* zx, int B, int H, int W, void* y, int ldy, uint8_t* u8, hipStream_t s);
+int tap_sum3x3(int dt, const void* zh, const void* zx, int B, int H, int W, void* y, int ldy, uint8_t* u8,
+               hipStream_t s);
 
+int aad_v3_clock_words(const AadV3Desc& d);
 bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo);
 int aad_v3(const AadV3Desc& d, hipStream_t s);
 

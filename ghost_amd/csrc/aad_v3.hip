@@ -17,6 +17,7 @@
 // round trip and every global access is a 16-byte vector along channels.
 // HBM bytes per launch = |h_in| + |z_attr| + L * |out|  (the algorithmic minimum).
 #include <cstdlib>
+#include <type_traits>
 
 #include "aad_v3.h"
 #include "ghost_common.h"
@@ -24,26 +25,29 @@
 
 namespace ghost {
 
-struct AadV3Args {
-  const bf16* za;
-  const bf16* hin;
+template <typename T>   // T: the 16-bit storage type (bf16, or fp16 for a .half() module)
+struct AadV3ArgsT {
+  const T* za;
+  const T* hin;
   const float* stat;
-  const bf16* w3[2];
+  const T* w3[2];
   const float* b3[2];
   const float* wh[2];
   const float* bh[2];
   const float* idgb[2];
-  bf16* out[2];
+  T* out[2];
   int ldo[2];
   int lda, ldh, id_ld, HW, PPW;
-  const bf16* zw[2];   // tap-partial projection rows (ZPM layers), row stride zwld
+  const T* zw[2];   // tap-partial projection rows (ZPM layers), row stride zwld
   int zwld;
   float slope;
   Up2xSrc up;   // UP: h_in is the bilinear x2 upsample of hin (a [B, up.H, up.W] source)
-  // in-kernel clock (v5; nullptr = off): [0] = earliest workgroup start, [1] = latest wave end, in
-  // wall-clock ticks (hipDeviceAttributeWallClockRate); atomicMin / atomicMax by one lane each
+  // in-kernel clock (nullptr = off): per workgroup its start stamp tclk[blockIdx.x], per wave its end stamp
+  // tclk[grid + blockIdx.x * 8 + wave], wall-clock ticks (hipDeviceAttributeWallClockRate); plain stores to
+  // distinct words, so the clock does not perturb the kernel (one contended atomic per wave did: +100 us)
   unsigned long long* tclk;
   int v5_xcd;   // v5: blocks in XCD-contiguous order
+  int v5_ipw;   // v5: 1024-pixel work items per workgroup
 };
 
 static constexpr int kWaves = 8;
@@ -68,14 +72,15 @@ template <int ZPM>
 GHOST_DEV constexpr int zp_slot(int l) { return l == 0 ? 0 : (ZPM & 1); }
 template <int ZPM>
 constexpr int zp_nlayers() { return (ZPM & 1) + ((ZPM >> 1) & 1); }
-GHOST_DEV void zp_store(const bf16* __restrict__ W, const bf16x8 (&xf)[2], _Float16* __restrict__ zrow, int lr, int lq) {
+template <typename T>
+GHOST_DEV void zp_store(const T* __restrict__ W, const v8_t<T> (&xf)[2], _Float16* __restrict__ zrow, int lr, int lq) {
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&W[sw64(rt * 16 + lr, ks * 32 + lq * 8)]);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf[ks], acc, 0, 0, 0);
+      const v8_t<T> wf = *reinterpret_cast<const v8_t<T>*>(&W[sw64(rt * 16 + lr, ks * 32 + lq * 8)]);
+      acc = mfma16x16x32<T>(wf, xf[ks], acc);
     }
     typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
     const f16x4 h = {(_Float16)acc[0], (_Float16)acc[1], (_Float16)acc[2], (_Float16)acc[3]};
@@ -84,13 +89,14 @@ GHOST_DEV void zp_store(const bf16* __restrict__ W, const bf16x8 (&xf)[2], _Floa
 }
 
 // the same, one K half at a time (K step ks = the half sh just computed): keeps 8 accumulator registers live
-// instead of both halves' bf16 fragments
-GHOST_DEV void zp_mfma_half(const bf16* __restrict__ W, const bf16x8& xf, int ks, f32x4 (&acc)[2], int lr, int lq) {
+// instead of both halves' T fragments
+template <typename T>
+GHOST_DEV void zp_mfma_half(const T* __restrict__ W, const v8_t<T>& xf, int ks, f32x4 (&acc)[2], int lr, int lq) {
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     asm volatile("" ::: "memory");   // the projection rows are re-read per use, not held across the tile loop
-    const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&W[sw64(rt * 16 + lr, ks * 32 + lq * 8)]);
-    acc[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[rt], 0, 0, 0);
+    const v8_t<T> wf = *reinterpret_cast<const v8_t<T>*>(&W[sw64(rt * 16 + lr, ks * 32 + lq * 8)]);
+    acc[rt] = mfma16x16x32<T>(wf, xf, acc[rt]);
   }
 }
 GHOST_DEV void zp_store_acc(const f32x4 (&acc)[2], _Float16* __restrict__ zrow, int lq) {
@@ -102,8 +108,8 @@ GHOST_DEV void zp_store_acc(const f32x4 (&acc)[2], _Float16* __restrict__ zrow, 
   }
 }
 
-template <int L, int ZPM, int NT>
-GHOST_DEV void zp_stage_weights(const AadV3Args& a, bf16* s_wz, int tid) {
+template <typename T, int L, int ZPM, int NT>
+GHOST_DEV void zp_stage_weights(const AadV3ArgsT<T>& a, T* s_wz, int tid) {
   if constexpr (ZPM != 0) {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
@@ -117,14 +123,14 @@ GHOST_DEV void zp_stage_weights(const AadV3Args& a, bf16* s_wz, int tid) {
   }
 }
 
-template <int C, int CA, int L, bool UP, int NWV = kWaves, int ZPM = 0>
-GHOST_DEV void aad_v3_body(const AadV3Args& a) {
+template <typename T, int C, int CA, int L, bool UP, int NWV = kWaves, int ZPM = 0>
+GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
   static_assert(ZPM == 0 || C == 64, "tap partials: C = 64");
   constexpr int CT = C / 64;          // 64-channel tiles
   constexpr int KS = CA / 32;         // MFMA k-steps
-  constexpr int WLD = CA + 8;         // padded LDS weight row (bf16 elements)
+  constexpr int WLD = CA + 8;         // padded LDS weight row (T elements)
   constexpr int NH = CT * 2;          // 16-byte h_in chunks per lane (8 channels each)
-  __shared__ __attribute__((aligned(16))) bf16 s_w[L * CT * 128 * WLD];
+  __shared__ __attribute__((aligned(16))) T s_w[L * CT * 128 * WLD];
   __shared__ __attribute__((aligned(16))) float s_b[L * CT * 128];
   __shared__ __attribute__((aligned(16))) float s_rs[C];
   __shared__ __attribute__((aligned(16))) float s_nm[C];
@@ -132,12 +138,12 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
   __shared__ float s_k[L];                                        // sum_c wh * (-mu * rstd)
   __shared__ __attribute__((aligned(16))) float s_gi[L * C];
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
-  __shared__ __attribute__((aligned(16))) bf16 s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
+  __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
 
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
   const long p_begin = (long)blockIdx.x * a.PPW;
   const int b = (int)(p_begin / a.HW);     // PPW divides HW: one sample per workgroup
-  zp_stage_weights<L, ZPM, NWV * 64>(a, s_wz, tid);
+  zp_stage_weights<T, L, ZPM, NWV * 64>(a, s_wz, tid);
 
   // ---- resident weights, biases and per-channel tables ----
   for (int l = 0; l < L; ++l) {
@@ -187,18 +193,18 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
     for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + ks * 32 + lq * 8);
     if constexpr (UP) {
       // the tile's 16 pixels lie on one output row; each chunk is interpolated from the four
-      // source pixels (L1/L2 hits: a source pixel feeds ~4 outputs) and rounded to bf16
+      // source pixels (L1/L2 hits: a source pixel feeds ~4 outputs) and rounded to T
       const int r = (int)(p - (long)b * a.HW);
       const int oy = r / (2 * a.up.W), ox = r - oy * (2 * a.up.W);
       const Up2xTap tp = up2x_tap(a.up, oy, ox);
-      const bf16* src = a.hin + (long)b * a.up.H * a.up.W * a.ldh;
+      const T* src = a.hin + (long)b * a.up.H * a.up.W * a.ldh;
 #pragma unroll
       for (int j = 0; j < NH; ++j) {
         float v[8];
         up2x_load16_f(src + (j >> 1) * 64 + (j & 1) * 32 + lq * 8, a.ldh, tp, v);
-        bf16* hv = reinterpret_cast<bf16*>(&hc[j]);
+        T* hv = reinterpret_cast<T*>(&hc[j]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) hv[e] = (bf16)v[e];
+        for (int e = 0; e < 8; ++e) hv[e] = (T)v[e];
       }
     } else {
 #pragma unroll
@@ -213,7 +219,7 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
 #pragma unroll
     for (int j = 0; j < NH; ++j) {
       const int c0 = (j >> 1) * 64 + (j & 1) * 32 + lq * 8;
-      const bf16* hv = reinterpret_cast<const bf16*>(&hc[j]);
+      const T* hv = reinterpret_cast<const T*>(&hc[j]);
 #pragma unroll
       for (int e = 0; e < 8; ++e)
 #pragma unroll
@@ -231,10 +237,10 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       asm volatile("" ::: "memory");   // one layer's accumulators live at a time
-      bf16x8 xf[2];
+      v8_t<T> xf[2];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        const bf16* W = s_w + (l * CT + ct) * 128 * WLD;
+        const T* W = s_w + (l * CT + ct) * 128 * WLD;
         // half sh: row tiles {2sh, 2sh+1} (gamma) and {4+2sh, 5+2sh} (beta) = channels
         // ct*64 + 32sh + 8lq + e of this lane's pixel; one half's accumulators live at a time
 #pragma unroll
@@ -248,18 +254,18 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
           }
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
-            bf16x8 bfrag;
+            v8_t<T> bfrag;
             __builtin_memcpy(&bfrag, &zc[ks], 16);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
-              const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&W[(rt * 16 + lr) * WLD + ks * 32 + lq * 8]);
-              acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i], 0, 0, 0);
+              const v8_t<T> afrag = *reinterpret_cast<const v8_t<T>*>(&W[(rt * 16 + lr) * WLD + ks * 32 + lq * 8]);
+              acc[i] = mfma16x16x32<T>(afrag, bfrag, acc[i]);
             }
           }
           const int j = ct * 2 + sh;
           const int c0 = ct * 64 + sh * 32 + lq * 8;
-          const bf16* hv = reinterpret_cast<const bf16*>(&hc[j]);
+          const T* hv = reinterpret_cast<const T*>(&hc[j]);
           float o[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -273,7 +279,7 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
           }
           if (ZPM && ((ZPM >> l) & 1)) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) xf[sh][e] = (bf16)o[e];
+            for (int e = 0; e < 8; ++e) xf[sh][e] = (T)o[e];
           } else {
             store16_f(a.out[l] + p * a.ldo[l] + c0, o);
           }
@@ -287,13 +293,13 @@ GHOST_DEV void aad_v3_body(const AadV3Args& a) {
 
 // C = 64: held to 4 waves per SIMD (<= 128 VGPRs) so two 512-thread workgroups share a CU;
 // C = 128 keeps the compiler's allocation (forcing it spills)
-template <int C, int CA, int L, bool UP, int ZPM = 0>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v3_kernel(const AadV3Args a) {
-  aad_v3_body<C, CA, L, UP, kWaves, ZPM>(a);
+template <typename T, int C, int CA, int L, bool UP, int ZPM = 0>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v3_kernel(const AadV3ArgsT<T> a) {
+  aad_v3_body<T, C, CA, L, UP, kWaves, ZPM>(a);
 }
-template <int C, int CA, int L, bool UP>
-__global__ void __launch_bounds__(512) aad_v3_wide_kernel(const AadV3Args a) {
-  aad_v3_body<C, CA, L, UP>(a);
+template <typename T, int C, int CA, int L, bool UP>
+__global__ void __launch_bounds__(512) aad_v3_wide_kernel(const AadV3ArgsT<T> a) {
+  aad_v3_body<T, C, CA, L, UP>(a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -325,7 +331,8 @@ struct V4Cfg {
 };
 
 template <int CA, int L, bool UP, bool RELU, int ZPM = 0>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v4_kernel(const AadV3Args a) {
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v4_kernel(const AadV3ArgsT<bf16> a) {
+  typedef bf16 T;   // (bf16 only: v5 replaces it as the block-input kernel, and is the one fp16 runs)
   static_assert(UP, "v4 is the through-upsample form (v3's register loads win without the upsample)");
   using K = V4Cfg<CA, L, UP>;
   constexpr int C = 64, KS = K::KS, SPX = K::SPX, SLOT_B = K::SLOT_B;
@@ -334,7 +341,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   // arithmetic spills the ZPM = 0 form at 128 VGPRs)
   constexpr int WLD = ZPM ? CA : CA + 8;
   auto widx = [](int row, int k) { return ZPM ? swca<CA>(row, k) : row * (CA + 8) + k; };
-  __shared__ __attribute__((aligned(16))) bf16 s_w[L * 128 * WLD];
+  __shared__ __attribute__((aligned(16))) T s_w[L * 128 * WLD];
   __shared__ __attribute__((aligned(16))) float s_b[L * 128];
   __shared__ __attribute__((aligned(16))) float s_rs[C];
   __shared__ __attribute__((aligned(16))) float s_nm[C];
@@ -344,16 +351,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hA[kWaves * SLOT_B];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hB[kWaves * SLOT_B];
-  __shared__ __attribute__((aligned(16))) bf16 s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
+  __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
 
   // wid through readfirstlane: tile indices and everything derived from them are wave-uniform (SGPRs),
   // so the per-tile address arithmetic runs on the scalar unit and the VALU keeps only lane offsets
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, lr = lane & 15,
             lq = lane >> 4;
-  if (a.tclk && tid == 0) atomicMin(&a.tclk[0], (unsigned long long)wall_clock64());
+  if (a.tclk && tid == 0) a.tclk[blockIdx.x] = (unsigned long long)wall_clock64();
   const long p_begin = (long)blockIdx.x * a.PPW;
   const int b = (int)(p_begin / a.HW);
-  zp_stage_weights<L, ZPM, kWaves * 64>(a, s_wz, tid);
+  zp_stage_weights<T, L, ZPM, kWaves * 64>(a, s_wz, tid);
 
   for (int l = 0; l < L; ++l) {
     for (int idx = tid; idx < 128 * (CA / 8); idx += kWaves * 64) {
@@ -387,7 +394,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
   for (int l = 0; l < L; ++l) bh[l] = a.bh[l][0] + s_k[l];
 
-  const bf16* src = UP ? a.hin + (long)b * a.up.H * a.up.W * a.ldh : nullptr;
+  const T* src = UP ? a.hin + (long)b * a.up.H * a.up.W * a.ldh : nullptr;
   const int ntiles = a.PPW / 16;
   // this wave's tiles: t = wid + 8 i, i = 0 .. nw-1 (nw even: PPW is a multiple of 256)
   const int nw = ntiles / kWaves;
@@ -399,7 +406,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 
   // z fragments of tile t (registers) + its h_in pixels (DMA into slot `slot` of this wave)
   auto issue = [&](int t, u32x4 (&zc)[KS], unsigned char* slot) {
-    const bf16* zt = a.za + (p_begin + t * 16) * a.lda;
+    const T* zt = a.za + (p_begin + t * 16) * a.lda;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(zt + z_lane + ks * 32);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -412,7 +419,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int y1 = y0 + (y0 < a.up.H - 1 ? 1 : 0);
 #pragma unroll
     for (int row = 0; row < 2; ++row) {
-      const bf16* srow = src + (long)(row ? y1 : y0) * a.up.W * a.ldh;
+      const T* srow = src + (long)(row ? y1 : y0) * a.up.W * a.ldh;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int pl = k * 8 + (lane >> 3), cl = lane & 7;     // LDS pixel / chunk this lane fills
@@ -450,14 +457,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
         };
         // up2x_mix's arithmetic, two channels per packed-fp32 instruction
         const u32x4 r00 = ld(0, c0), r01 = ld(0, c1), r10 = ld(1, c0), r11 = ld(1, c1);
-        bf16* hv = reinterpret_cast<bf16*>(&hc[j]);
+        T* hv = reinterpret_cast<T*>(&hc[j]);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const f32x2 top = fma2(lx0, bf16x2_f(r00[k]), lx1 * bf16x2_f(r01[k]));
-          const f32x2 bot = fma2(lx0, bf16x2_f(r10[k]), lx1 * bf16x2_f(r11[k]));
+          const f32x2 top = fma2(lx0, unpack2<T>(r00[k]), lx1 * unpack2<T>(r01[k]));
+          const f32x2 bot = fma2(lx0, unpack2<T>(r10[k]), lx1 * unpack2<T>(r11[k]));
           const f32x2 v = fma2(ly0, top, ly1 * bot);
-          hv[2 * k] = (bf16)v.x;
-          hv[2 * k + 1] = (bf16)v.y;
+          hv[2 * k] = (T)v.x;
+          hv[2 * k + 1] = (T)v.y;
         }
       }
     } else {
@@ -479,7 +486,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       const int c0 = j * 32 + lq * 8;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const f32x2 h2 = bf16x2_f(hc[j][k]);
+        const f32x2 h2 = unpack2<T>(hc[j][k]);
 #pragma unroll
         for (int l = 0; l < L; ++l) ms[l] = fma2(*reinterpret_cast<const f32x2*>(&s_cf[l * C + c0 + 2 * k]), h2, ms[l]);
       }
@@ -495,7 +502,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       asm volatile("" ::: "memory");
-      const bf16* W = s_w + l * 128 * WLD;
+      const T* W = s_w + l * 128 * WLD;
       f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int sh = 0; sh < 2; ++sh) {
@@ -508,13 +515,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          bf16x8 bfrag;
+          v8_t<T> bfrag;
           __builtin_memcpy(&bfrag, &zc[ks], 16);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
-            const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&W[widx(rt * 16 + lr, ks * 32 + lq * 8)]);
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i], 0, 0, 0);
+            const v8_t<T> afrag = *reinterpret_cast<const v8_t<T>*>(&W[widx(rt * 16 + lr, ks * 32 + lq * 8)]);
+            acc[i] = mfma16x16x32<T>(afrag, bfrag, acc[i]);
           }
         }
         const int c0 = sh * 32 + lq * 8;
@@ -523,7 +530,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
         for (int k = 0; k < 4; ++k) {   // channels c0 + 2k, c0 + 2k + 1
           const int c = c0 + 2 * k;
-          const f32x2 hh = fma2(bf16x2_f(hc[sh][k]), *reinterpret_cast<const f32x2*>(&s_rs[c]),
+          const f32x2 hh = fma2(unpack2<T>(hc[sh][k]), *reinterpret_cast<const f32x2*>(&s_rs[c]),
                                 *reinterpret_cast<const f32x2*>(&s_nm[c]));
           const f32x2 g = {acc[k >> 1][(2 * k) & 3], acc[k >> 1][(2 * k + 1) & 3]};
           const f32x2 be = {acc[2 + (k >> 1)][(2 * k) & 3], acc[2 + (k >> 1)][(2 * k + 1) & 3]};
@@ -540,9 +547,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
           }
         }
         if (ZPM && ((ZPM >> l) & 1)) {
-          bf16x8 xf;
+          v8_t<T> xf;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) xf[e] = (bf16)o[e];
+          for (int e = 0; e < 8; ++e) xf[e] = (T)o[e];
           zp_mfma_half(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, sh, zacc, lr, lq);
         } else {
           store16_f(a.out[l] + p0 * a.ldo[l] + (lr * a.ldo[l] + c0), o);
@@ -571,7 +578,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) zc[ks] = zn[ks];
   }
-  if (a.tclk && lane == 0) atomicMax(&a.tclk[1], (unsigned long long)wall_clock64());
+  if (a.tclk && lane == 0) a.tclk[gridDim.x + blockIdx.x * kWaves + wid] = (unsigned long long)wall_clock64();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -591,12 +598,31 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 // by both at nearly the same time (one L2 miss), and blocks go to XCDs in contiguous runs
 // (xcd_remap) so the row a block shares with the next is read on the same L2.
 // ---------------------------------------------------------------------------------------------
-template <int CA, int L, bool RELU, int ZPM = 0>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v5_kernel(const AadV3Args a) {
+// Memory ops the compiler does not see (v5 with ASMW): the DMA of the next tile's h_in source pixels and
+// z_attr fragments into LDS slots, and the reads of those slots.  Then the only vector-memory ops the
+// compiler tracks in the loop are the tile's stores, so it inserts no s_waitcnt vmcnt(0) after them (with
+// loads and stores both pending it waits for zero, exposing every tile's store latency); the kernel waits
+// itself with a counted vmcnt(2 L) before reading tile i's slots: gfx9 retires vector-memory ops in issue
+// order, so that leaves only tile i-1's 2 L stores in flight, overlapping tile i's arithmetic.  (An asm load
+// into registers is not safe: the compiler treats its result as ready at the asm and may copy it early.)
+GHOST_DEV void asm_dma16(const void* gp, uint32_t lds_base) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(gp), "s"(lds_base) : "memory", "m0");
+}
+GHOST_DEV u32x4 asm_lds16(uint32_t addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+// LDS byte offset of a __shared__ object (the low 32 bits of its generic address: the shared aperture base
+// has zero low bits)
+GHOST_DEV uint32_t lds_off(const void* p) { return (uint32_t)(uintptr_t)p; }
+
+template <typename T, int CA, int L, bool RELU, int ZPM = 0, bool ASMW = false>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v5_kernel(const AadV3ArgsT<T> a) {
   constexpr int C = 64, KS = CA / 32, SPX = 6, SLOT_B = 2 * SPX * 128;
   constexpr int WLD = ZPM ? CA : CA + 8;
   auto widx = [](int row, int k) { return ZPM ? swca<CA>(row, k) : row * (CA + 8) + k; };
-  __shared__ __attribute__((aligned(16))) bf16 s_w[L * 128 * WLD];
+  __shared__ __attribute__((aligned(16))) T s_w[L * 128 * WLD];
   __shared__ __attribute__((aligned(16))) float s_b[L * 128];
   __shared__ __attribute__((aligned(16))) float s_rs[C];
   __shared__ __attribute__((aligned(16))) float s_nm[C];
@@ -606,18 +632,23 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hA[kWaves * SLOT_B];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hB[kWaves * SLOT_B];
-  __shared__ __attribute__((aligned(16))) bf16 s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
+  __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
+  // ASMW: each wave's z_attr tile (16 pixels x CA channels), single-buffered: read at the top of tile i, then
+  // refilled with tile i+1's by DMA
+  constexpr int ZSLOT_B = 16 * CA * 2;
+  __shared__ __attribute__((aligned(1024))) unsigned char s_z[ASMW ? kWaves * ZSLOT_B : 16];
 
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, lr = lane & 15,
             lq = lane >> 4;
-  if (a.tclk && tid == 0) atomicMin(&a.tclk[0], (unsigned long long)wall_clock64());
+  if (a.tclk && tid == 0) a.tclk[blockIdx.x] = (unsigned long long)wall_clock64();
   const int H = a.up.H, W = a.up.W, OW = 2 * W;
   const int NCT = OW / 8;                      // 8-column tiles per row tile
   const int RT = 64 / NCT;                     // row tiles per workgroup (host: 1, 2, 4 or 8)
-  const int wpi = H / RT;                      // workgroups per image
+  const int wpi = H / RT;                      // 1024-pixel work items per image
+  const int IPW = a.v5_ipw;                    // work items per workgroup (consecutive, one image: wpi % IPW == 0)
   const int wi = a.v5_xcd ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
-  const int b = wi / wpi, g = wi - b * wpi;
-  zp_stage_weights<L, ZPM, kWaves * 64>(a, s_wz, tid);
+  const int b = wi * IPW / wpi, g0 = wi * IPW - b * wpi;
+  zp_stage_weights<T, L, ZPM, kWaves * 64>(a, s_wz, tid);
 
   for (int l = 0; l < L; ++l) {
     for (int idx = tid; idx < 128 * (CA / 8); idx += kWaves * 64) {
@@ -651,66 +682,91 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
   for (int l = 0; l < L; ++l) bh[l] = a.bh[l][0] + s_k[l];
 
-  const bf16* src = a.hin + (long)b * H * W * a.ldh;
+  const T* src = a.hin + (long)b * H * W * a.ldh;
   const long pimg = (long)b * a.HW;
   const int ri = lr >> 3, col = lr & 7;        // this lane's pixel: row ri of the row tile, column col
-  const int rtl = wid % RT;                    // this wave's row tile inside the workgroup
-  const int q = g * RT + rtl;                  // ... inside the image
-  const int oyA = q == 0 ? 0 : 2 * q - 1, oyB = q == 0 ? 2 * H - 1 : 2 * q;
-  // source rows of the row tile (scalar): sA = y0(oyA); sB = y1(oyA) for a pair, y0(oyB) for the edge tile
-  int sA, sB;
-  {
+  const int rtl = wid % RT;                    // this wave's row tile inside a work item
+  const int nw = 8 * IPW;                      // tiles per wave: 8 per work item
+  const int ox_w = 8 * (wid / RT), ox_step = 64 / RT;   // wave's first column, column step between its tiles
+  // row tile of the wave's tile i (item i / 8): q = 0 -> output rows {0, 2H-1}, q >= 1 -> {2q-1, 2q}; its
+  // source rows (scalar): sA = y0(oyA); sB = y1(oyA) for a pair, y0(oyB) for the edge tile; and this lane's
+  // row: output row offset, y taps as slot rows (top / bottom) and weight
+  struct RowT {
+    int sA, sB, top, bot;
+    long prow, prowA, prowB;   // this lane's output row, the row tile's two rows (pixel offsets)
+    float fly1;
+  };
+  auto row_tile = [&](int i) {
+    RowT r;
+    const int q = (g0 + (i >> 3)) * RT + rtl;
+    const int oyA = q == 0 ? 0 : 2 * q - 1, oyB = q == 0 ? 2 * H - 1 : 2 * q;
     float rA = a.up.sh * (float)oyA, rB = a.up.sh * (float)oyB;
     asm volatile("" : "+v"(rA), "+v"(rB));
     const int y0A = __builtin_amdgcn_readfirstlane((int)rA), y0B = __builtin_amdgcn_readfirstlane((int)rB);
-    sA = y0A;
-    sB = q == 0 ? y0B : y0A + (y0A < H - 1 ? 1 : 0);
-  }
-  // this lane's row: its y taps as slot rows (top / bottom) and weight
-  const int oy = ri ? oyB : oyA;
-  float fly1;
-  int top, bot;
-  {
-    float ry = a.up.sh * (float)oy;
-    asm volatile("" : "+v"(ry));
+    r.sA = y0A;
+    r.sB = q == 0 ? y0B : y0A + (y0A < H - 1 ? 1 : 0);
+    const int oy = ri ? oyB : oyA;
+    float ry = ri ? rB : rA;
     const int y0 = (int)ry, y1 = y0 + (y0 < H - 1 ? 1 : 0);
-    fly1 = ry - (float)y0;
-    top = y0 == sA ? 0 : 1;
-    bot = y1 == sA ? 0 : (y1 == sB ? 1 : top);
-  }
-  const f32x2 ly0 = {1.f - fly1, 1.f - fly1}, ly1 = {fly1, fly1};
-  const long prow = pimg + (long)oy * OW;      // this lane's output row
-  const int nw = 64 / kWaves;                  // tiles per wave
-  const int ox_w = 8 * (wid / RT), ox_step = 64 / RT;   // wave's first column, column step between its tiles
+    r.fly1 = ry - (float)y0;
+    r.top = y0 == r.sA ? 0 : 1;
+    r.bot = y1 == r.sA ? 0 : (y1 == r.sB ? 1 : r.top);
+    r.prow = pimg + (long)oy * OW;
+    r.prowA = pimg + (long)oyA * OW;
+    r.prowB = pimg + (long)oyB * OW;
+    return r;
+  };
 
   // z fragments of tile i (registers) + its 2 x 6 source pixels (DMA into slot `slot` of this wave)
   auto issue = [&](int i, u32x4 (&zc)[KS], unsigned char* slot) {
-    const int ox0 = ox_w + ox_step * i;
-    const bf16* zt = a.za + (prow + ox0 + col) * a.lda + lq * 8;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(zt + ks * 32);
+    const RowT rt = row_tile(i);
+    const int ox0 = ox_w + ox_step * (i & 7);
 #if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (ASMW) {
+      // z_attr of the tile's 16 pixels into this wave's z slot: piece = lane of instruction k holds pixel
+      // px = (k * 64 + lane) / (CA / 8), 16-byte chunk position c, filled with source chunk c ^ (px & (CA/8 - 1))
+      constexpr int CPX = CA / 8;                               // chunks per pixel
+      const uint32_t zdst = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_off(s_z + wid * ZSLOT_B));
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const int piece = k * 64 + lane, px = piece / CPX, c = piece % CPX;
+        const int prx = px >> 3, pcx = px & 7;                  // pixel -> (row of the row tile, column)
+        const long pp = (prx ? rt.prowB : rt.prowA) + ox0 + pcx;
+        asm_dma16(a.za + pp * a.lda + ((c ^ (px & (CPX - 1))) * 8), zdst + k * 1024);
+      }
+    } else {
+      const T* zt = a.za + (rt.prow + ox0 + col) * a.lda + lq * 8;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(zt + ks * 32);
+    }
     unsigned char* dst = slot + wid * SLOT_B;
     float rx = a.up.sw * (float)ox0;
     asm volatile("" : "+v"(rx));
     const int x_lo = __builtin_amdgcn_readfirstlane((int)rx);
-    const bf16* rowA = src + (long)sA * W * a.ldh;
-    const bf16* rowB = src + (long)sB * W * a.ldh;
+    const T* rowA = src + (long)rt.sA * W * a.ldh;
+    const T* rowB = src + (long)rt.sB * W * a.ldh;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       if (k == 1 && lane >= 32) continue;                    // 12 slot pixels x 8 chunks = 96 pieces
       const int qs = k * 8 + (lane >> 3), cl = lane & 7;     // slot pixel / chunk position this lane fills
       const int sr = qs >= SPX, px = qs - (sr ? SPX : 0);
       const int sx = min(x_lo + px, W - 1);
-      __builtin_amdgcn_global_load_lds((sr ? rowB : rowA) + sx * a.ldh + ((cl ^ (qs & 7)) * 8), dst + k * 1024, 16,
-                                       0, 0);
+      const T* gp = (sr ? rowB : rowA) + sx * a.ldh + ((cl ^ (qs & 7)) * 8);
+      if constexpr (ASMW)
+        asm_dma16(gp, (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_off(dst + k * 1024)));
+      else
+        __builtin_amdgcn_global_load_lds(gp, dst + k * 1024, 16, 0, 0);
     }
 #endif
   };
   // tile i's h_in chunks out of its LDS slot through the bilinear x2
-  auto hload = [&](int i, const unsigned char* slot, u32x4 (&hc)[2]) {
+  auto hload = [&](int i, const unsigned char* slot, u32x4 (&hc)[2], long& p) {
     const unsigned char* hs = slot + wid * SLOT_B;
-    const int ox0 = ox_w + ox_step * i;
+    const RowT rt = row_tile(i);
+    const int ox0 = ox_w + ox_step * (i & 7);
+    p = rt.prow + ox0 + col;
+    const int top = rt.top, bot = rt.bot;
+    const f32x2 ly0 = {1.f - rt.fly1, 1.f - rt.fly1}, ly1 = {rt.fly1, rt.fly1};
     float rx0 = a.up.sw * (float)ox0;
     asm volatile("" : "+v"(rx0));
     const int x_lo = __builtin_amdgcn_readfirstlane((int)rx0);
@@ -725,21 +781,24 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int ch = j * 4 + lq;
-      auto ld = [&](int qq) { return *reinterpret_cast<const u32x4*>(hs + qq * 128 + ((ch ^ (qq & 7)) * 16)); };
-      const u32x4 r00 = ld(q00), r01 = ld(q01), r10 = ld(q10), r11 = ld(q11);
-      bf16* hv = reinterpret_cast<bf16*>(&hc[j]);
+      auto ld = [&](int qq) {
+        if constexpr (ASMW) return asm_lds16(lds_off(hs) + qq * 128 + ((ch ^ (qq & 7)) * 16));
+        else return *reinterpret_cast<const u32x4*>(hs + qq * 128 + ((ch ^ (qq & 7)) * 16));
+      };
+      u32x4 r00 = ld(q00), r01 = ld(q01), r10 = ld(q10), r11 = ld(q11);
+      if constexpr (ASMW) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r00), "+v"(r01), "+v"(r10), "+v"(r11));
+      T* hv = reinterpret_cast<T*>(&hc[j]);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const f32x2 tp = fma2(lx0, bf16x2_f(r00[k]), lx1 * bf16x2_f(r01[k]));
-        const f32x2 bt = fma2(lx0, bf16x2_f(r10[k]), lx1 * bf16x2_f(r11[k]));
+        const f32x2 tp = fma2(lx0, unpack2<T>(r00[k]), lx1 * unpack2<T>(r01[k]));
+        const f32x2 bt = fma2(lx0, unpack2<T>(r10[k]), lx1 * unpack2<T>(r11[k]));
         const f32x2 v = fma2(ly0, tp, ly1 * bt);
-        hv[2 * k] = (bf16)v.x;
-        hv[2 * k + 1] = (bf16)v.y;
+        hv[2 * k] = (T)v.x;
+        hv[2 * k + 1] = (T)v.y;
       }
     }
   };
-  auto compute = [&](int i, const u32x4 (&zc)[KS], const u32x4 (&hc)[2]) {
-    const long p = prow + (ox_w + ox_step * i) + col;   // this lane's output pixel
+  auto compute = [&](const long p, const u32x4 (&zc)[KS], const u32x4 (&hc)[2]) {
     f32x2 ms[L];
 #pragma unroll
     for (int l = 0; l < L; ++l) ms[l] = f32x2{0.f, 0.f};
@@ -748,7 +807,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       const int c0 = j * 32 + lq * 8;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const f32x2 h2 = bf16x2_f(hc[j][k]);
+        const f32x2 h2 = unpack2<T>(hc[j][k]);
 #pragma unroll
         for (int l = 0; l < L; ++l) ms[l] = fma2(*reinterpret_cast<const f32x2*>(&s_cf[l * C + c0 + 2 * k]), h2, ms[l]);
       }
@@ -764,7 +823,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       asm volatile("" ::: "memory");
-      const bf16* Wt = s_w + l * 128 * WLD;
+      const T* Wt = s_w + l * 128 * WLD;
       f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int sh = 0; sh < 2; ++sh) {
@@ -777,13 +836,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          bf16x8 bfrag;
+          v8_t<T> bfrag;
           __builtin_memcpy(&bfrag, &zc[ks], 16);
 #pragma unroll
           for (int i4 = 0; i4 < 4; ++i4) {
             const int rt = (i4 & 1) + 2 * sh + 4 * (i4 >> 1);
-            const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&Wt[widx(rt * 16 + lr, ks * 32 + lq * 8)]);
-            acc[i4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i4], 0, 0, 0);
+            const v8_t<T> afrag = *reinterpret_cast<const v8_t<T>*>(&Wt[widx(rt * 16 + lr, ks * 32 + lq * 8)]);
+            acc[i4] = mfma16x16x32<T>(afrag, bfrag, acc[i4]);
           }
         }
         const int c0 = sh * 32 + lq * 8;
@@ -792,7 +851,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int c = c0 + 2 * k;
-          const f32x2 hh = fma2(bf16x2_f(hc[sh][k]), *reinterpret_cast<const f32x2*>(&s_rs[c]),
+          const f32x2 hh = fma2(unpack2<T>(hc[sh][k]), *reinterpret_cast<const f32x2*>(&s_rs[c]),
                                 *reinterpret_cast<const f32x2*>(&s_nm[c]));
           const f32x2 gg = {acc[k >> 1][(2 * k) & 3], acc[k >> 1][(2 * k + 1) & 3]};
           const f32x2 be = {acc[2 + (k >> 1)][(2 * k) & 3], acc[2 + (k >> 1)][(2 * k + 1) & 3]};
@@ -809,9 +868,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
           }
         }
         if (ZPM && ((ZPM >> l) & 1)) {
-          bf16x8 xf;
+          v8_t<T> xf;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) xf[e] = (bf16)o[e];
+          for (int e = 0; e < 8; ++e) xf[e] = (T)o[e];
           zp_mfma_half(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, sh, zacc, lr, lq);
         } else {
           store16_f(a.out[l] + p * a.ldo[l] + c0, o);
@@ -823,20 +882,50 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 
   u32x4 zc[KS], zn[KS];
   issue(0, zc, s_hA);
-  for (int i = 0; i < nw; ++i) {
-    unsigned char* cur = (i & 1) ? s_hB : s_hA;
-    unsigned char* nxt = (i & 1) ? s_hA : s_hB;
-    asm volatile("" ::: "memory");
-    u32x4 hc[2];
-    hload(i, cur, hc);
-    asm volatile("" ::: "memory");
-    if (i + 1 < nw) issue(i + 1, zn, nxt);
-    asm volatile("" ::: "memory");
-    compute(i, zc, hc);
+  if constexpr (ASMW) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int i = 0; i < nw; ++i) {
+      unsigned char* cur = (i & 1) ? s_hB : s_hA;
+      unsigned char* nxt = (i & 1) ? s_hA : s_hB;
+      // tile i's DMAs done; tile i-1's 2 L stores may still be in flight
+      static_assert(L == 1 || L == 2, "");
+      if constexpr (L == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      // z fragments of this lane's pixel lr, channels 32 ks + 8 lq .. +7, out of the z slot
+      const uint32_t zs = lds_off(s_z + wid * ZSLOT_B);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) zc[ks] = zn[ks];
+      for (int ks = 0; ks < KS; ++ks) {
+        constexpr int CPX = CA / 8;
+        const int c = ks * 4 + lq;
+        zc[ks] = asm_lds16(zs + (lr * CPX + (c ^ (lr & (CPX - 1)))) * 16);
+      }
+      if constexpr (KS == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(zc[0]), "+v"(zc[1]));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(zc[0]));
+      u32x4 hc[2];
+      long p;
+      hload(i, cur, hc, p);
+      asm volatile("" ::: "memory");
+      if (i + 1 < nw) issue(i + 1, zn, nxt);
+      asm volatile("" ::: "memory");
+      compute(p, zc, hc);
+    }
+  } else {
+    for (int i = 0; i < nw; ++i) {
+      unsigned char* cur = (i & 1) ? s_hB : s_hA;
+      unsigned char* nxt = (i & 1) ? s_hA : s_hB;
+      asm volatile("" ::: "memory");
+      u32x4 hc[2];
+      long p;
+      hload(i, cur, hc, p);
+      asm volatile("" ::: "memory");
+      if (i + 1 < nw) issue(i + 1, zn, nxt);
+      asm volatile("" ::: "memory");
+      compute(p, zc, hc);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) zc[ks] = zn[ks];
+    }
   }
-  if (a.tclk && lane == 0) atomicMax(&a.tclk[1], (unsigned long long)wall_clock64());
+  if (a.tclk && lane == 0) a.tclk[gridDim.x + blockIdx.x * kWaves + wid] = (unsigned long long)wall_clock64();
 }
 
 // v5's row pairing holds for this source height in fp32 (PyTorch's index arithmetic, as up2x_tap): output
@@ -858,8 +947,31 @@ static bool v5_pairing_ok(const Up2xSrc& u) {
 // pixels per workgroup: one sample's block; C = 256 stages its weights once per 1024 pixels
 static int v3_ppw(int HW, int C) { return (HW >= 65536 || C == 256) ? 1024 : 512; }
 
+// the v5 kernel's work items per workgroup if it takes this launch, else 0
+static int v5_takes(const AadV3Desc& d, int zpm) {
+  static const int use_v5 = GHOST_KNOB("GHOST_AAD_V5", 1);
+  static const int ipw = GHOST_KNOB("GHOST_V5_IPW", 1);
+  const bool up = d.up_H > 0;
+  // OW / 8 column tiles must divide the 64 tiles of a 1024-pixel work item (OW in {64 .. 512}) and the
+  // work items of an image must cover its H row tiles, IPW at a time
+  const int nct = 2 * d.up_W / 8, rt = nct > 0 && 64 % nct == 0 ? 64 / nct : 0;
+  if (!use_v5 || !up || d.C != 64 || v3_ppw(d.HW, d.C) != 1024 || d.ldh % 8 || d.up_W % 4 || rt < 1 || rt > 8 ||
+      d.up_H % rt || d.up_H < 2 || ipw < 1 || (d.up_H / rt) % ipw || !v5_pairing_ok(up2x_src(d.up_H, d.up_W)))
+    return 0;
+  if (!(d.Ca == 64 || d.Ca == 32) || (zpm && d.L != 2)) return 0;
+  return ipw;
+}
+
+int aad_v3_clock_words(const AadV3Desc& d) {
+  long grid = (long)d.B * d.HW / v3_ppw(d.HW, d.C);
+  int zpm = 0;
+  for (int l = 0; l < d.L; ++l) zpm |= d.zw[l] ? 1 << l : 0;
+  if (const int ipw = v5_takes(d, zpm)) grid /= ipw;
+  return (int)(grid * (1 + kWaves));
+}
+
 bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo) {
-  if (dt != GHOST_BF16) return false;
+  if (!is16(dt)) return false;
   // C = 256 (the 64x64 stage): all four channel tiles' weight rows (139 KB at Ca = 128) resident, one
   // workgroup per CU; the mask is computed in-kernel from the pixel's 256 channels, so no separate
   // mask pass reads h_in (measured B = 64: the per-channel-tile aad_wide + mask pass took 92 + 25 us)
@@ -871,15 +983,13 @@ bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, in
   return HW % ppw == 0 && (long)B * HW / ppw >= 32;
 }
 
-int aad_v3(const AadV3Desc& d, hipStream_t s) {
-  if (!aad_v3_supported(GHOST_BF16, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo[0])) return -1;
-  if (d.L == 2 && d.ldo[1] % 8) return -1;
-  if (d.L < 1 || d.L > 2 || (d.L == 2 && d.C != 64 && !(d.C == 128 && d.Ca == 64))) return -1;
-  AadV3Args a{};
-  a.za = (const bf16*)d.za; a.hin = (const bf16*)d.hin; a.stat = d.stat;
+template <typename T>
+static int aad_v3_t(const AadV3Desc& d, hipStream_t s) {
+  AadV3ArgsT<T> a{};
+  a.za = (const T*)d.za; a.hin = (const T*)d.hin; a.stat = d.stat;
   for (int l = 0; l < d.L; ++l) {
-    a.w3[l] = (const bf16*)d.w3[l]; a.b3[l] = d.b3[l]; a.wh[l] = d.wh[l]; a.bh[l] = d.bh[l];
-    a.idgb[l] = d.idgb[l]; a.out[l] = (bf16*)d.out[l]; a.ldo[l] = d.ldo[l];
+    a.w3[l] = (const T*)d.w3[l]; a.b3[l] = d.b3[l]; a.wh[l] = d.wh[l]; a.bh[l] = d.bh[l];
+    a.idgb[l] = d.idgb[l]; a.out[l] = (T*)d.out[l]; a.ldo[l] = d.ldo[l];
   }
   a.lda = d.lda; a.ldh = d.ldh; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
   a.PPW = v3_ppw(d.HW, d.C);
@@ -887,7 +997,7 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   for (int l = 0; l < d.L; ++l)
     if (d.zw[l]) {
       zpm |= 1 << l;
-      a.zw[l] = (const bf16*)d.zw[l];
+      a.zw[l] = (const T*)d.zw[l];
     }
   a.zwld = d.zwld;
   if (zpm && (d.C != 64 || d.slope != 0.f || d.zwld % 8)) return -1;
@@ -906,18 +1016,16 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   static const unsigned dyn_lds = GHOST_KNOB("GHOST_AAD_DYNLDS", 0u);
   a.tclk = d.tclk;
   a.v5_xcd = GHOST_KNOB("GHOST_V5_XCD", 1);
-  static const int use_v5 = GHOST_KNOB("GHOST_AAD_V5", 0);
-  // v5: OW / 8 column tiles must divide the 64 tiles of a 1024-pixel workgroup (OW in {64 .. 512}) and the
-  // workgroups of an image must cover its H row tiles
-  const int v5_nct = 2 * d.up_W / 8, v5_rt = v5_nct > 0 && 64 % v5_nct == 0 ? 64 / v5_nct : 0;
-  if (use_v5 && up && d.C == 64 && a.PPW == 1024 && d.ldh % 8 == 0 && d.up_W % 4 == 0 && v5_rt >= 1 &&
-      v5_rt <= 8 && d.up_H % v5_rt == 0 && d.up_H >= 2 && v5_pairing_ok(a.up)) {
+  a.v5_ipw = v5_takes(d, zpm);
+  static const int v5_asm = GHOST_KNOB("GHOST_V5_ASM", 1);
+  if (a.v5_ipw) {
+    grid = dim3(grid.x / a.v5_ipw);
 #define GHOST_V5(ca, l)                                                                          \
     if (d.Ca == ca && d.L == l && !zpm) {                                                        \
       if (d.slope == 0.f)                                                                        \
-        hipLaunchKernelGGL((aad_v5_kernel<ca, l, true>), grid, dim3(kWaves * 64), 0, s, a);      \
+        hipLaunchKernelGGL((aad_v5_kernel<T, ca, l, true, 0, false>), grid, dim3(kWaves * 64), 0, s, a); \
       else                                                                                       \
-        hipLaunchKernelGGL((aad_v5_kernel<ca, l, false>), grid, dim3(kWaves * 64), 0, s, a);     \
+        hipLaunchKernelGGL((aad_v5_kernel<T, ca, l, false, 0, false>), grid, dim3(kWaves * 64), 0, s, a); \
       if (d.version_out) *d.version_out = 5;                                                     \
       return (int)hipGetLastError();                                                             \
     }
@@ -925,13 +1033,19 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
 #undef GHOST_V5
 #define GHOST_V5Z(ca, zm)                                                                        \
     if (d.Ca == ca && d.L == 2 && zpm == zm) {                                                   \
-      hipLaunchKernelGGL((aad_v5_kernel<ca, 2, true, zm>), grid, dim3(kWaves * 64), 0, s, a);    \
+      if (v5_asm)                                                                                \
+        hipLaunchKernelGGL((aad_v5_kernel<T, ca, 2, true, zm, true>), grid, dim3(kWaves * 64), 0, s, a); \
+      else                                                                                       \
+        hipLaunchKernelGGL((aad_v5_kernel<T, ca, 2, true, zm, false>), grid, dim3(kWaves * 64), 0, s, a); \
       if (d.version_out) *d.version_out = 5;                                                     \
       return (int)hipGetLastError();                                                             \
     }
     GHOST_V5Z(64, 1) GHOST_V5Z(64, 2) GHOST_V5Z(64, 3) GHOST_V5Z(32, 1) GHOST_V5Z(32, 2) GHOST_V5Z(32, 3)
 #undef GHOST_V5Z
+    grid = dim3(grid.x * a.v5_ipw);   // (not reached: v5_takes admits only the shapes above)
+    a.v5_ipw = 0;
   }
+  if constexpr (std::is_same<T, bf16>::value) {
   if (use_v4 && up && d.C == 64 && a.PPW % 256 == 0 && d.ldh % 8 == 0) {
 #define GHOST_V4(ca, l, u)                                                                       \
     if (d.Ca == ca && d.L == l && up == u && !zpm) {                                             \
@@ -954,10 +1068,11 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
     GHOST_V4Z(64, 1) GHOST_V4Z(64, 2) GHOST_V4Z(64, 3) GHOST_V4Z(32, 1) GHOST_V4Z(32, 2) GHOST_V4Z(32, 3)
 #undef GHOST_V4Z
   }
+  }
   if (zpm) {   // the non-upsampled forms with tap partials (AADBlk8's last add_block; fuse_upsample off)
 #define GHOST_V3Z(ca, l, zm)                                                                     \
     if (d.C == 64 && d.Ca == ca && d.L == l && !up && zpm == zm) {                               \
-      hipLaunchKernelGGL((aad_v3_kernel<64, ca, l, false, zm>), grid, dim3(kWaves * 64), 0, s, a); \
+      hipLaunchKernelGGL((aad_v3_kernel<T, 64, ca, l, false, zm>), grid, dim3(kWaves * 64), 0, s, a); \
       return (int)hipGetLastError();                                                             \
     }
     GHOST_V3Z(64, 1, 1) GHOST_V3Z(32, 1, 1) GHOST_V3Z(64, 2, 1) GHOST_V3Z(32, 2, 1) GHOST_V3Z(64, 2, 2)
@@ -967,12 +1082,12 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   }
 #define GHOST_V3(c, ca, l, u)                                                                   \
   if (d.C == c && d.Ca == ca && d.L == l && up == u) {                                          \
-    hipLaunchKernelGGL((aad_v3_kernel<c, ca, l, u>), grid, dim3(kWaves * 64), 0, s, a);         \
+    hipLaunchKernelGGL((aad_v3_kernel<T, c, ca, l, u>), grid, dim3(kWaves * 64), 0, s, a);         \
     return (int)hipGetLastError();                                                              \
   }
 #define GHOST_V3W(c, ca, l, u)                                                                  \
   if (d.C == c && d.Ca == ca && d.L == l && up == u) {                                          \
-    hipLaunchKernelGGL((aad_v3_wide_kernel<c, ca, l, u>), grid, dim3(kWaves * 64), 0, s, a);    \
+    hipLaunchKernelGGL((aad_v3_wide_kernel<T, c, ca, l, u>), grid, dim3(kWaves * 64), 0, s, a);    \
     return (int)hipGetLastError();                                                              \
   }
   GHOST_V3(64, 64, 1, false) GHOST_V3(64, 64, 2, false) GHOST_V3(64, 32, 1, false) GHOST_V3(64, 32, 2, false)
@@ -990,6 +1105,13 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
   return -1;
 }
 
+int aad_v3(const AadV3Desc& d, hipStream_t s) {
+  if (!aad_v3_supported(d.dt, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo[0])) return -1;
+  if (d.L == 2 && d.ldo[1] % 8) return -1;
+  if (d.L < 1 || d.L > 2 || (d.L == 2 && d.C != 64 && !(d.C == 128 && d.Ca == 64))) return -1;
+  return d.dt == GHOST_F16 ? aad_v3_t<_Float16>(d, s) : aad_v3_t<bf16>(d, s);
+}
+
 // ---------------------------------------------------------------------------------------------
 // AADBlk8's output conv from the tap partials: an 8 x 32 output tile per workgroup; its 10 x 34 halo of
 // zh + zx (fp16 -> fp32, summed once per halo pixel) in LDS, then one output pixel per thread gathers
@@ -1001,8 +1123,9 @@ constexpr int TS_TH = 16, TS_TW = 32, TS_HW = TS_TW + 2, TS_HP = (TS_TH + 2) * T
 constexpr int TS_ITEMS = TS_HP * 4, TS_PER = (TS_ITEMS + 511) / 512;   // (halo pixel, 16-byte chunk) per thread
 }
 
+template <typename T>
 __global__ void __launch_bounds__(512) tap_sum3x3_kernel(const _Float16* __restrict__ zh, const _Float16* __restrict__ zx,
-                                                         int H, int W, bf16* __restrict__ y, int ldy,
+                                                         int H, int W, T* __restrict__ y, int ldy,
                                                          uint8_t* __restrict__ u8) {
   __shared__ float Z[TS_HP * TS_LD];
   const int tid = threadIdx.x;
@@ -1047,7 +1170,7 @@ __global__ void __launch_bounds__(512) tap_sum3x3_kernel(const _Float16* __restr
 #pragma unroll
       for (int tx = 0; tx < 3; ++tx) s += Z[((oy + ty) * TS_HW + ox + tx) * TS_LD + (ty * 3 + tx) * 3 + o];
     s = tanhf(s);
-    y[q * ldy + o] = (bf16)s;
+    y[q * ldy + o] = (T)s;
     if (u8) {
       const float t = (s * 0.5f + 0.5f) * 255.0f;   // faceshifter_run.py:20-21
       u8[q * 3 + (2 - o)] = (uint8_t)(int)t;
@@ -1055,10 +1178,16 @@ __global__ void __launch_bounds__(512) tap_sum3x3_kernel(const _Float16* __restr
   }
 }
 
-int tap_sum3x3(const void* zh, const void* zx, int B, int H, int W, void* y, int ldy, uint8_t* u8, hipStream_t s) {
-  if (H % TS_TH || W % TS_TW || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16) return -1;
-  hipLaunchKernelGGL(tap_sum3x3_kernel, dim3((unsigned)(B * (H / TS_TH) * (W / TS_TW))), dim3(512), 0, s,
-                     (const _Float16*)zh, (const _Float16*)zx, H, W, (bf16*)y, ldy, u8);
+int tap_sum3x3(int dt, const void* zh, const void* zx, int B, int H, int W, void* y, int ldy, uint8_t* u8,
+               hipStream_t s) {
+  if (H % TS_TH || W % TS_TW || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16 || !is16(dt)) return -1;
+  const dim3 g((unsigned)(B * (H / TS_TH) * (W / TS_TW)));
+  if (dt == GHOST_F16)
+    hipLaunchKernelGGL(tap_sum3x3_kernel<_Float16>, g, dim3(512), 0, s, (const _Float16*)zh, (const _Float16*)zx, H, W,
+                       (_Float16*)y, ldy, u8);
+  else
+    hipLaunchKernelGGL(tap_sum3x3_kernel<bf16>, g, dim3(512), 0, s, (const _Float16*)zh, (const _Float16*)zx, H, W,
+                       (bf16*)y, ldy, u8);
   return (int)hipGetLastError();
 }
 

@@ -18,6 +18,7 @@ struct AadWideDesc {
   const float* idgb = nullptr;                 // [B][id_ld]: gamma_id at c, beta_id at C + c
   const float* mask = nullptr;                 // [B*HW] sigmoid mask of this layer (aad_mask)
   void* out = nullptr;       int ldo = 0;
+  int dt = 1;                                  // storage type: GHOST_BF16 (1) or GHOST_F16 (2)
 };
 
 bool aad_wide_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo);

@@ -16,16 +16,16 @@
 namespace ghost {
 
 struct AadWideArgs {
-  const bf16* za;
-  const bf16* hin;
+  const void* za;
+  const void* hin;
   const float* stat;
-  const bf16* w3;
+  const void* w3;
   const float* b3;
   const float* wh;
   const float* bh;
   const float* idgb;
   const float* mask;
-  bf16* out;
+  void* out;
   int lda, ldh, ldo, id_ld, HW, PPW, nblk;
   float slope;
 };
@@ -38,12 +38,16 @@ GHOST_DEV int wide_xcd_tile(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-template <int C, int CA>
+template <typename T, int C, int CA>
 GHOST_DEV void aad_wide_body(const AadWideArgs& a) {
+  const T* __restrict__ za = reinterpret_cast<const T*>(a.za);
+  const T* __restrict__ hin = reinterpret_cast<const T*>(a.hin);
+  const T* __restrict__ w3 = reinterpret_cast<const T*>(a.w3);
+  T* __restrict__ out = reinterpret_cast<T*>(a.out);
   constexpr int CT = C / 64;
   constexpr int KS = CA / 32;
   constexpr int WLD = CA + 8;
-  __shared__ __attribute__((aligned(16))) bf16 s_w[128 * WLD];
+  __shared__ __attribute__((aligned(16))) T s_w[128 * WLD];
   __shared__ __attribute__((aligned(16))) float s_b[128];
   __shared__ __attribute__((aligned(16))) float s_rs[64];
   __shared__ __attribute__((aligned(16))) float s_nm[64];
@@ -59,7 +63,7 @@ GHOST_DEV void aad_wide_body(const AadWideArgs& a) {
   for (int idx = tid; idx < 128 * (CA / 8); idx += kWideWaves * 64) {
     const int row = idx / (CA / 8), kc = idx - row * (CA / 8);
     *reinterpret_cast<u32x4*>(&s_w[row * WLD + kc * 8]) =
-        *reinterpret_cast<const u32x4*>(a.w3 + (long)(ct * 128 + row) * CA + kc * 8);
+        *reinterpret_cast<const u32x4*>(w3 + (long)(ct * 128 + row) * CA + kc * 8);
   }
   for (int i = tid; i < 128; i += kWideWaves * 64) s_b[i] = a.b3[ct * 128 + i];
   if (tid < 64) {
@@ -76,13 +80,13 @@ GHOST_DEV void aad_wide_body(const AadWideArgs& a) {
   for (int t = wid; t < ntiles; t += kWideWaves) {
     asm volatile("" ::: "memory");
     const long p = p_begin + t * 16 + lr;
-    const bf16* hrow = a.hin + p * a.ldh + ct * 64;
+    const T* hrow = hin + p * a.ldh + ct * 64;
     // one round trip: the z_attr row, this tile's two h_in chunks and the mask
     constexpr bool ZEARLY = true;   // the whole z_attr row is in flight with the h_in chunks
     u32x4 zc[ZEARLY ? KS : 1];
     if constexpr (ZEARLY) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + ks * 32 + lq * 8);
+      for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(za + p * a.lda + ks * 32 + lq * 8);
     }
     u32x4 hc[2];
 #pragma unroll
@@ -109,23 +113,23 @@ GHOST_DEV void aad_wide_body(const AadWideArgs& a) {
           asm volatile("" ::: "memory");
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            zg[u] = *reinterpret_cast<const u32x4*>(a.za + p * a.lda + (k0 + u) * 32 + lq * 8);
+            zg[u] = *reinterpret_cast<const u32x4*>(za + p * a.lda + (k0 + u) * 32 + lq * 8);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           if (k0 + u >= KS) break;
           const int ks = k0 + u;
-          bf16x8 bfrag;
+          v8_t<T> bfrag;
           __builtin_memcpy(&bfrag, &zg[u], 16);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
-            const bf16x8 afrag = *reinterpret_cast<const bf16x8*>(&s_w[(rt * 16 + lr) * WLD + ks * 32 + lq * 8]);
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[i], 0, 0, 0);
+            const v8_t<T> afrag = *reinterpret_cast<const v8_t<T>*>(&s_w[(rt * 16 + lr) * WLD + ks * 32 + lq * 8]);
+            acc[i] = mfma16x16x32<T>(afrag, bfrag, acc[i]);
           }
         }
       }
-      const bf16* hv = reinterpret_cast<const bf16*>(&hc[sh]);
+      const T* hv = reinterpret_cast<const T*>(&hc[sh]);
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -135,7 +139,7 @@ GHOST_DEV void aad_wide_body(const AadWideArgs& a) {
         const float v = fmaf(Mk, I - A, A);
         o[e] = v > 0.f ? v : v * a.slope;
       }
-      store16_f(a.out + p * a.ldo + ct * 64 + cl, o);
+      store16_f(out + p * a.ldo + ct * 64 + cl, o);
     }
   }
 }
@@ -144,13 +148,13 @@ GHOST_DEV void aad_wide_body(const AadWideArgs& a) {
 // weight rows allow one workgroup per CU, so the z_attr row (64 VGPRs) may use the registers.
 // (Measured alternative, not kept: each wave on four 16-pixel tiles per weight fragment — 4x less
 // LDS traffic per MFMA, 300-390 registers, one wave per SIMD — ran 10-17 % slower at 16x16-64x64.)
-template <int C, int CA>
+template <typename T, int C, int CA>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_wide_kernel(const AadWideArgs a) {
-  aad_wide_body<C, CA>(a);
+  aad_wide_body<T, C, CA>(a);
 }
-template <int C, int CA>
+template <typename T, int C, int CA>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 8))) aad_wide_deep_kernel(const AadWideArgs a) {
-  aad_wide_body<C, CA>(a);
+  aad_wide_body<T, C, CA>(a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -167,7 +171,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 8))
 // ---------------------------------------------------------------------------------------------
 GHOST_DEV int gswz(int r) { return (r >> 1) & 7; }
 
-template <int CA>
+template <typename T, int CA>
 __global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int C) {
   constexpr int NST = CA / 64;                 // K stages
   static_assert(NST % 2 == 0, "stages are ping-ponged in pairs");
@@ -185,8 +189,8 @@ __global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int 
   const long p0 = (long)pb * 256;
   const int b = (int)(p0 / a.HW);              // HW % 256 == 0: one sample per tile
   const int c0 = cp * 128;                     // first channel; weight rows cp*256 .. +256
-  const bf16* wsrc = a.w3 + (long)cp * 256 * CA;
-  const bf16* zsrc = a.za + p0 * a.lda;
+  const T* wsrc = reinterpret_cast<const T*>(a.w3) + (long)cp * 256 * CA;
+  const T* zsrc = reinterpret_cast<const T*>(a.za) + p0 * a.lda;
 
   // DMA: 64 pieces of 8 rows x 128 B per stage (32 weight + 32 pixel), 16 per wave
   const int prow = lane >> 3, pch = lane & 7;
@@ -198,7 +202,7 @@ __global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int 
       const int q = wid + 4 * j;               // piece 0..63: < 32 weights, >= 32 pixels
       const int row = (q & 31) * 8 + prow;
       const int lc = pch ^ gswz(row);          // logical chunk this lane's physical slot holds
-      const bf16* src = q < 32 ? wsrc + (long)row * CA + k0 + lc * 8 : zsrc + (long)row * a.lda + k0 + lc * 8;
+      const T* src = q < 32 ? wsrc + (long)row * CA + k0 + lc * 8 : zsrc + (long)row * a.lda + k0 + lc * 8;
       __builtin_amdgcn_global_load_lds(src, buf + q * 1024, 16, 0, 0);
     }
 #endif
@@ -227,22 +231,22 @@ __global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int 
     const unsigned char* Zb = buf + 256 * 128;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[8], bfr[8];
+      v8_t<T> af[8], bfr[8];
 #pragma unroll
       for (int rt = 0; rt < 8; ++rt) {
         const int row = wr * 128 + rt * 16 + lr;
-        af[rt] = *reinterpret_cast<const bf16x8*>(Wb + row * 128 + (((ks * 4 + lq) ^ gswz(row)) * 16));
+        af[rt] = *reinterpret_cast<const v8_t<T>*>(Wb + row * 128 + (((ks * 4 + lq) ^ gswz(row)) * 16));
       }
 #pragma unroll
       for (int pf = 0; pf < 8; ++pf) {
         const int row = wp * 128 + pf * 16 + lr;
-        bfr[pf] = *reinterpret_cast<const bf16x8*>(Zb + row * 128 + (((ks * 4 + lq) ^ gswz(row)) * 16));
+        bfr[pf] = *reinterpret_cast<const v8_t<T>*>(Zb + row * 128 + (((ks * 4 + lq) ^ gswz(row)) * 16));
       }
 #pragma unroll
       for (int rt = 0; rt < 8; ++rt)
 #pragma unroll
         for (int pf = 0; pf < 8; ++pf)
-          acc[rt][pf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rt], bfr[pf], acc[rt][pf], 0, 0, 0);
+          acc[rt][pf] = mfma16x16x32<T>(af[rt], bfr[pf], acc[rt][pf]);
     }
   };
   // the epilogue's inputs — the tile's h_in (256 pixels x 128 channels = 64 KB) and its 256 mask values —
@@ -256,7 +260,8 @@ __global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int 
     for (int j = 0; j < 16; ++j) {
       const int q = wu + 4 * j;                  // piece: pixels 4q .. 4q+3
       const int P = q * 4 + (lane >> 4), lc = (lane & 15) ^ (P & 15);
-      __builtin_amdgcn_global_load_lds(a.hin + (p0 + P) * a.ldh + c0 + lc * 8, lds0 + q * 1024, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const T*>(a.hin) + (p0 + P) * a.ldh + c0 + lc * 8, lds0 + q * 1024,
+                                       16, 0, 0);
     }
     if (wu == 0) __builtin_amdgcn_global_load_lds(a.mask + p0 + lane * 4, (unsigned char*)s_mask, 16, 0, 0);
 #endif
@@ -290,7 +295,7 @@ __global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int 
       float hv[8];
       {
         const u32x4 raw = *reinterpret_cast<const u32x4*>(lds0 + P * 256 + (((cl >> 3) ^ (P & 15)) * 16));
-        const bf16* e = reinterpret_cast<const bf16*>(&raw);
+        const T* e = reinterpret_cast<const T*>(&raw);
 #pragma unroll
         for (int i = 0; i < 8; ++i) hv[i] = (float)e[i];
       }
@@ -307,7 +312,7 @@ __global__ void __launch_bounds__(256) aad_gemm_kernel(const AadWideArgs a, int 
         const float v = fmaf(Mk, I - A, A);
         o[e] = v > 0.f ? v : v * a.slope;
       }
-      store16_f(a.out + p * a.ldo + c0 + cl, o);
+      store16_f(reinterpret_cast<T*>(a.out) + p * a.ldo + c0 + cl, o);
     }
   }
 }
@@ -328,7 +333,7 @@ int wide_ppw(int B, int HW, int C, int Ca) {
 }  // namespace
 
 bool aad_wide_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, int ldo) {
-  if (dt != GHOST_BF16) return false;
+  if (!is16(dt)) return false;
   const bool shape = (C == 256 || C == 512 || C == 1024) && (Ca == 64 || Ca == 128 || Ca == 256 || Ca == 512);
   if (!shape || lda % 8 || ldh % 8 || ldo % 8) return false;
   const int ppw = wide_ppw(B, HW, C, Ca);
@@ -344,15 +349,23 @@ static bool aad_gemm_ok(const AadWideDesc& d) {
          d.ldh % 8 == 0 && d.ldo % 8 == 0 && (uintptr_t)d.za % 16 == 0 && (uintptr_t)d.w3 % 16 == 0;
 }
 
+template <typename T>
+static int aad_wide_t(const AadWideDesc& d, hipStream_t s);
+
 int aad_wide(const AadWideDesc& d, hipStream_t s) {
-  if (!aad_wide_supported(GHOST_BF16, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo) || !d.mask) return -1;
+  if (!aad_wide_supported(d.dt, d.B, d.HW, d.C, d.Ca, d.lda, d.ldh, d.ldo) || !d.mask) return -1;
+  return d.dt == GHOST_F16 ? aad_wide_t<_Float16>(d, s) : aad_wide_t<bf16>(d, s);
+}
+
+template <typename T>
+static int aad_wide_t(const AadWideDesc& d, hipStream_t s) {
   AadWideArgs a{};
-  a.za = (const bf16*)d.za; a.hin = (const bf16*)d.hin; a.stat = d.stat;
-  a.w3 = (const bf16*)d.w3; a.b3 = d.b3; a.wh = d.wh; a.bh = d.bh; a.idgb = d.idgb; a.mask = d.mask; a.out = (bf16*)d.out;
+  a.za = d.za; a.hin = d.hin; a.stat = d.stat;
+  a.w3 = d.w3; a.b3 = d.b3; a.wh = d.wh; a.bh = d.bh; a.idgb = d.idgb; a.mask = d.mask; a.out = d.out;
   a.lda = d.lda; a.ldh = d.ldh; a.ldo = d.ldo; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
   if (aad_gemm_ok(d)) {
     dim3 g((unsigned)((long)d.B * d.HW / 256 * (d.C / 128)));
-    hipLaunchKernelGGL(aad_gemm_kernel<512>, g, dim3(256), 0, s, a, d.C);
+    hipLaunchKernelGGL((aad_gemm_kernel<T, 512>), g, dim3(256), 0, s, a, d.C);
     return (int)hipGetLastError();
   }
   a.PPW = wide_ppw(d.B, d.HW, d.C, d.Ca);
@@ -360,7 +373,7 @@ int aad_wide(const AadWideDesc& d, hipStream_t s) {
   dim3 grid((unsigned)(a.nblk * (d.C / 64)));
 #define GHOST_W(c, ca)                                                                 \
   if (d.C == c && d.Ca == ca) {                                                        \
-    hipLaunchKernelGGL((aad_wide_kernel<c, ca>), grid, dim3(kWideWaves * 64), 0, s, a); \
+    hipLaunchKernelGGL((aad_wide_kernel<T, c, ca>), grid, dim3(kWideWaves * 64), 0, s, a); \
     return (int)hipGetLastError();                                                     \
   }
   GHOST_W(256, 64) GHOST_W(256, 128) GHOST_W(256, 256) GHOST_W(512, 64) GHOST_W(512, 128) GHOST_W(512, 256)
@@ -368,7 +381,7 @@ int aad_wide(const AadWideDesc& d, hipStream_t s) {
 #undef GHOST_W
 #define GHOST_WD(c, ca)                                                                     \
   if (d.C == c && d.Ca == ca) {                                                             \
-    hipLaunchKernelGGL((aad_wide_deep_kernel<c, ca>), grid, dim3(kWideWaves * 64), 0, s, a); \
+    hipLaunchKernelGGL((aad_wide_deep_kernel<T, c, ca>), grid, dim3(kWideWaves * 64), 0, s, a); \
     return (int)hipGetLastError();                                                          \
   }
   GHOST_WD(512, 512) GHOST_WD(1024, 512)

@@ -88,12 +88,20 @@ struct ghost_aei {
   std::vector<Pending> pend;
   int ev_used = 0;
   ProfClass prof[8];
-  // in-kernel clock of the roofline kernel's launches (profiling class 1, the v5 AAD kernel): per launch
-  // [earliest workgroup start, latest wave end] in wall-clock ticks; device buffer of clk_cap pairs
+  // in-kernel clock of the roofline kernel's launches (profiling class 1): per launch a region of per-workgroup
+  // start and per-wave end stamps (aad_v3_clock_words); clk_cap words of device buffer, bump-allocated
   unsigned long long* clk = nullptr;
-  int clk_cap = 0, clk_n = 0, clk_dev = -1;
+  size_t clk_cap = 0, clk_used = 0;
+  int clk_dev = -1;
+  std::vector<std::pair<size_t, int>> clk_launch;   // (offset, words) per clocked launch
   int roof_version = 0;                        // kernel generation of class 1's last launch (aad_v3.h)
-  unsigned long long* next_clk() { return (clk && clk_n < clk_cap) ? clk + 2 * clk_n++ : nullptr; }
+  unsigned long long* next_clk(int words) {
+    if (!clk || words <= 0 || clk_used + (size_t)words > clk_cap) return nullptr;
+    clk_launch.push_back({clk_used, words});
+    unsigned long long* p = clk + clk_used;
+    clk_used += (size_t)words;
+    return p;
+  }
 
   typedef int Pair[2];
   typedef int Triple[3];
@@ -521,6 +529,7 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
         continue;
       }
       AadWideDesc d;
+      d.dt = h->dt;
       d.za = za; d.lda = lda; d.Ca = Ca; d.hin = hin; d.ldh = ldh; d.stat = stat;
       d.B = B; d.HW = n * n; d.C = C; d.id_ld = h->id_total; d.slope = 0.0f;   // + the ReLU that follows
       d.w3 = c.W(l.name + ".w3");
@@ -544,6 +553,7 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
   const size_t lmax = (C == 64 || (pair128 && C == 128 && Ca == 64)) ? 2 : 1;
   for (size_t i0 = 0; i0 < ls.size(); i0 += lmax) {
     AadV3Desc d;
+    d.dt = h->dt;
     d.za = za; d.lda = lda; d.Ca = Ca; d.hin = hin; d.ldh = ldh; d.stat = stat;
     d.B = B; d.HW = n * n; d.C = C; d.id_ld = h->id_total; d.slope = 0.0f;   // + the ReLU that follows
     d.L = (int)std::min(lmax, ls.size() - i0);
@@ -571,7 +581,7 @@ void aad_group(Ctx& c, const std::vector<AadOut>& ls, const void* hin, int ldh, 
     int e_all = c.prof_begin(0);
     // class 1: the block-input AAD kernel at 256x256 (reads h_in through the x2 upsample; one or two layers)
     int e_big = (n == 256 && up_src) ? c.prof_begin(1) : -1;
-    if (e_big >= 0 && h->clk_dev == c.dev) d.tclk = h->next_clk();
+    if (e_big >= 0 && h->clk_dev == c.dev) d.tclk = h->next_clk(aad_v3_clock_words(d));
     if (e_big >= 0) d.version_out = &h->roof_version;
     c.check(aad_v3(d, c.s), "aad_v3");
     if (e_big >= 0) c.prof_end(1, e_big, bytes, flops);
@@ -698,9 +708,9 @@ void generator(Ctx& c, int B, const void* const attr[8], GenIn gin, void* y_out,
     // x-branch and h'-branch share the output conv: conv(cat(a_x, a_h), [W_x | W_h]) = x + h'
     // AADBlk8 (cout = 3) with tap partials (GHOST_AEI_OPT_TAP_PARTIALS): the AADLayers feeding that conv write
     // its per-tap partial sums instead of their channels (zh: the h path, zx: last_add_block's x')
-    const int zp = (last_k && split && cin == 64 && cout == 3 && h->dt == GHOST_BF16)
+    const int zp = (last_k && split && cin == 64 && cout == 3 && is16(h->dt))
                        ? h->opt[GHOST_AEI_OPT_TAP_PARTIALS] : 0;
-    const bf16* wn = zp ? (const bf16*)c.W(blk + ".conv" + std::to_string(nb - 1) + ".wn") : nullptr;
+    const char* wn = zp ? (const char*)c.W(blk + ".conv" + std::to_string(nb - 1) + ".wn") : nullptr;
     const int wnld = rup(2 * cin, 32);
     void* zh = zp ? c.alloc(P * 32 * 2) : nullptr;
     void* zx = zp == 2 ? c.alloc(P * 32 * 2) : nullptr;
@@ -724,7 +734,7 @@ void generator(Ctx& c, int B, const void* const attr[8], GenIn gin, void* y_out,
       if (i == 0 && split) {   // last_add_block's AADLayer reads the block input m as well
         if (zp == 2) {
           AadOut o{blk + ".aadlast", base + 2 * cin * nb, zx, 32};
-          o.zw = wn + cin; o.zwld = wnld;
+          o.zw = wn + (size_t)cin * h->esz; o.zwld = wnld;   // the x' half of the K range
           group.push_back(o);
         } else if (zp == 1) {
           group.push_back({blk + ".aadlast", base + 2 * cin * nb, xq, cin});
@@ -752,13 +762,13 @@ void generator(Ctx& c, int B, const void* const attr[8], GenIn gin, void* y_out,
       } else if (zp == 2) {
         if (c.ok() && !c.dry) {
           int e_all = c.prof_begin(2);
-          c.check(tap_sum3x3(zh, zx, B, n, n, y, cout, u8, c.s), "tap_sum3x3");
+          c.check(tap_sum3x3(h->dt, zh, zx, B, n, n, y, cout, u8, c.s), "tap_sum3x3");
           c.prof_end(2, e_all, 0, 0);
         }
       } else if (zp == 1) {
         if (c.ok() && !c.dry) {
           int e_all = c.prof_begin(2);
-          c.check(conv3x3_narrow(h->dt, xq, B, n, n, cin, cin, wn + cin, wnld, cout, nullptr, 0, 1, y, cout, u8, c.s,
+          c.check(conv3x3_narrow(h->dt, xq, B, n, n, cin, cin, wn + (size_t)cin * h->esz, wnld, cout, nullptr, 0, 1, y, cout, u8, c.s,
                                  zh),
                   "conv3x3_narrow + tap partials");
           c.prof_end(2, e_all, 0, 2.0 * P * cout * 9.0 * cin);
@@ -837,7 +847,7 @@ void declare_slots(ghost_aei* h) {
     h->attr_geom(k, Ca_k, n_k);
     // permuted register-epilogue AAD layouts (pack.py pack_aad_v3): aad_v3 for C in {64, 128},
     // aad_wide for C in {256, 512, 1024} with Ca <= 512
-    const bool v3 = h->dt == GHOST_BF16 && (cin == 64 || cin == 128 ||
+    const bool v3 = is16(h->dt) && (cin == 64 || cin == 128 ||
                                             ((cin == 256 || cin == 512 || cin == 1024) && Ca_k <= 512));
     for (int i = 0; i < h->nb; ++i) {
       const std::string an = blk + ".aad" + std::to_string(i);
@@ -1031,7 +1041,8 @@ extern "C" int ghost_aei_create(const char* backbone, int num_blocks, int c_id, 
     return fail(GHOST_EINVAL, "backbone must be 'unet', 'linknet' or 'resnet' (got " + bb + ")");
   if (num_blocks < 1 || num_blocks > 8) return fail(GHOST_EINVAL, "num_blocks out of range");
   if (c_id <= 0 || c_id % 32) return fail(GHOST_EINVAL, "c_id must be a positive multiple of 32");
-  if (dtype != GHOST_F32 && dtype != GHOST_BF16) return fail(GHOST_EINVAL, "dtype must be f32 or bf16");
+  if (dtype != GHOST_F32 && dtype != GHOST_BF16 && dtype != GHOST_F16)
+    return fail(GHOST_EINVAL, "dtype must be f32, bf16 or f16");
   ghost_aei* h = new ghost_aei();
   h->linknet = bb == "linknet";
   h->resnet = bb == "resnet";
@@ -1145,7 +1156,8 @@ extern "C" int ghost_aei_profile(ghost_aei* h, int class_mask) {
   h->pend.clear();
   h->ev_used = 0;
   for (auto& p : h->prof) p = ProfClass{};
-  h->clk_n = 0;
+  h->clk_used = 0;
+  h->clk_launch.clear();
   if (class_mask & 2) {   // class 1: arm the in-kernel clock (buffer on the current device)
     int dev = -1;
     if (hipGetDevice(&dev) != hipSuccess) return fail(GHOST_EINVAL, "hipGetDevice failed");
@@ -1154,20 +1166,13 @@ extern "C" int ghost_aei_profile(ghost_aei* h, int class_mask) {
       h->clk = nullptr;
     }
     if (!h->clk) {
-      h->clk_cap = 4096;
-      if (hipMalloc(&h->clk, sizeof(unsigned long long) * 2 * h->clk_cap) != hipSuccess) {
+      h->clk_cap = size_t(8) << 20;   // 64 MB: 227 launches of the B = 64 256x256 kernel
+      if (hipMalloc(&h->clk, sizeof(unsigned long long) * h->clk_cap) != hipSuccess) {
         h->clk = nullptr;
         return fail(GHOST_EINVAL, "clock buffer allocation failed");
       }
       h->clk_dev = dev;
     }
-    std::vector<unsigned long long> init(2 * h->clk_cap);
-    for (int i = 0; i < h->clk_cap; ++i) {
-      init[2 * i] = ~0ull;
-      init[2 * i + 1] = 0;
-    }
-    if (hipMemcpy(h->clk, init.data(), init.size() * sizeof(init[0]), hipMemcpyHostToDevice) != hipSuccess)
-      return fail(GHOST_EINVAL, "clock buffer reset failed");
   }
   return 0;
 }
@@ -1177,8 +1182,8 @@ extern "C" int ghost_aei_profile_clock(ghost_aei* h, double* us_total, int64_t* 
   *us_total = 0;
   *launches = 0;
   if (kernel_version) *kernel_version = h->roof_version;
-  if (!h->clk || h->clk_n == 0) return 0;
-  std::vector<unsigned long long> v(2 * h->clk_n);
+  if (!h->clk || h->clk_launch.empty()) return 0;
+  std::vector<unsigned long long> v(h->clk_used);
   if (hipMemcpy(v.data(), h->clk, v.size() * sizeof(v[0]), hipMemcpyDeviceToHost) != hipSuccess)
     return fail(GHOST_EINVAL, "clock buffer read failed");
   int rate_khz = 0;
@@ -1186,9 +1191,13 @@ extern "C" int ghost_aei_profile_clock(ghost_aei* h, double* us_total, int64_t* 
     return fail(GHOST_EINVAL, "wall clock rate unavailable");
   double ticks = 0;
   int64_t n = 0;
-  for (int i = 0; i < h->clk_n; ++i) {
-    if (v[2 * i] == ~0ull || v[2 * i + 1] < v[2 * i]) continue;   // a launch that did not run the clocked kernel
-    ticks += (double)(v[2 * i + 1] - v[2 * i]);
+  for (auto& L : h->clk_launch) {
+    const size_t grid = (size_t)L.second / 9;   // 1 start + 8 wave ends per workgroup
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (size_t i = 0; i < grid; ++i) t0 = std::min(t0, v[L.first + i]);
+    for (size_t i = grid; i < (size_t)L.second; ++i) t1 = std::max(t1, v[L.first + i]);
+    if (t1 <= t0) continue;
+    ticks += (double)(t1 - t0);
     ++n;
   }
   *us_total = ticks / (rate_khz * 1e-3);

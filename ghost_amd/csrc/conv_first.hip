@@ -76,9 +76,9 @@ __global__ void __launch_bounds__(256) conv_first_kernel(const FirstArgs a) {
 // 16-pixel B fragment is gathered with two 8-byte loads per lane and k-step (no im2col).
 // Weights are the A operand (rows = output channels): lanes then hold 4 channels of one pixel.
 struct FirstMfmaArgs {
-  const bf16* x;      // [B][Hi][Wi][4]
-  const bf16* w;      // packed [Npad][Kpad], K = (ky*4 + kx)*3 + c
-  bf16* y;
+  const void* x;      // [B][Hi][Wi][4]
+  const void* w;      // packed [Npad][Kpad], K = (ky*4 + kx)*3 + c
+  void* y;
   const float* scale;
   const float* shift;
   int Hi, Wi, Ho, Wo, Kpad, ldy;
@@ -86,26 +86,28 @@ struct FirstMfmaArgs {
   long M;
 };
 
-// each wave walks kFirstChunks runs of 64 output pixels: the weight fragments (32 gathered bf16 per
+// each wave walks kFirstChunks runs of 64 output pixels: the weight fragments (32 gathered T per
 // lane) and the BN scale/shift are set up once per wave, not once per 64 pixels (measured 81 us at
 // 256x256, B = 64, with one run per wave: 1.2 TB/s for a 100 MB HBM kernel)
 constexpr int kFirstChunks = 4;
 
+template <typename T>
 __global__ void __launch_bounds__(256) conv_first_mfma_kernel(const FirstMfmaArgs a) {
+  const T* __restrict__ aw = reinterpret_cast<const T*>(a.w);
   const int lane = threadIdx.x & 63, lr = lane & 15, lq = lane >> 4;
   const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (wave * kFirstChunks * 64 >= a.M) return;
   // A fragments: channel rows n = 16j + lr, K = 32s + 8lq + e -> (ky, kx, c4) = (K/16, K/4 % 4, K % 4)
-  bf16x8 wf[2][2];
+  v8_t<T> wf[2][2];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16 e8[8];
+      T e8[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int k = s * 32 + lq * 8 + e, ky = k >> 4, kx = (k >> 2) & 3, c4 = k & 3;
-        e8[e] = c4 < 3 ? a.w[(long)(j * 16 + lr) * a.Kpad + (ky * 4 + kx) * 3 + c4] : (bf16)0.f;
+        e8[e] = c4 < 3 ? aw[(long)(j * 16 + lr) * a.Kpad + (ky * 4 + kx) * 3 + c4] : (T)0.f;
       }
       __builtin_memcpy(&wf[j][s], e8, 16);
     }
@@ -125,7 +127,7 @@ __global__ void __launch_bounds__(256) conv_first_mfma_kernel(const FirstMfmaArg
   const int b = (int)(m0 / hw);
   const int r0 = (int)(m0 - (long)b * hw);
   const int oy = r0 / a.Wo, ox0 = r0 - oy * a.Wo;
-  const bf16* xb = a.x + (long)b * a.Hi * a.Wi * 4;
+  const T* xb = reinterpret_cast<const T*>(a.x) + (long)b * a.Hi * a.Wi * 4;
   f32x4 acc[2][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -138,15 +140,15 @@ __global__ void __launch_bounds__(256) conv_first_mfma_kernel(const FirstMfmaArg
       const int iy = 2 * oy - 1 + ky, ix = 2 * ox - 1 + 2 * half;   // pixels ix, ix + 1
       uint2 p0 = {0u, 0u}, p1 = {0u, 0u};
       if (iy >= 0 && iy < a.Hi) {
-        const bf16* row = xb + (long)iy * a.Wi * 4;
+        const T* row = xb + (long)iy * a.Wi * 4;
         if (ix >= 0) p0 = *reinterpret_cast<const uint2*>(row + ix * 4);
         if (ix + 1 < a.Wi) p1 = *reinterpret_cast<const uint2*>(row + (ix + 1) * 4);
       }
       const u32x4 raw = {p0.x, p0.y, p1.x, p1.y};
-      bf16x8 bfrag;
+      v8_t<T> bfrag;
       __builtin_memcpy(&bfrag, &raw, 16);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], bfrag, acc[j][i], 0, 0, 0);
+      for (int j = 0; j < 2; ++j) acc[j][i] = mfma16x16x32<T>(wf[j][s], bfrag, acc[j][i]);
     }
   }
 #pragma unroll
@@ -156,13 +158,13 @@ __global__ void __launch_bounds__(256) conv_first_mfma_kernel(const FirstMfmaArg
     for (int j = 0; j < 2; ++j) {
       const int n = j * 16 + lq * 4;
       uint2 o;
-      bf16* oe = reinterpret_cast<bf16*>(&o);
+      T* oe = reinterpret_cast<T*>(&o);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float v = fmaf(acc[j][i][r], sc[j][r], sh[j][r]);
-        oe[r] = (bf16)(v > 0.f ? v : v * a.slope);
+        oe[r] = (T)(v > 0.f ? v : v * a.slope);
       }
-      *reinterpret_cast<uint2*>(a.y + m * a.ldy + n) = o;
+      *reinterpret_cast<uint2*>(reinterpret_cast<T*>(a.y) + m * a.ldy + n) = o;
     }
   }
   }
@@ -176,7 +178,7 @@ __global__ void __launch_bounds__(256) first_weights_kernel(const T* __restrict_
 
 bool conv_first_supported(const ConvDesc& d) {
   return d.kind == CONV_FWD && d.kh == 4 && d.kw == 4 && d.stride == 2 && d.pad == 1 && d.Cin == 3 &&
-         d.N == 32 && d.ti == d.to && (d.ti == GHOST_BF16 || d.ti == GHOST_F32) && d.epi == EPI_STD && !d.res && !d.prelu && !d.y2 &&
+         d.N == 32 && d.ti == d.to && (is16(d.ti) || d.ti == GHOST_F32) && d.epi == EPI_STD && !d.res && !d.prelu && !d.y2 &&
          !d.tanh_out && !d.u8 && d.ldy % (d.to == GHOST_F32 ? 4 : 8) == 0 && (uintptr_t)d.y % 16 == 0 &&
          d.Kpad >= 48 && !d.force_split;
 }
@@ -186,18 +188,24 @@ size_t conv_first_workspace_bytes() { return 32 * 48 * sizeof(float); }
 int conv_first(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t s) {
   if (!conv_first_supported(d)) return -1;
   const int Ho = (d.Hi + 2 - 4) / 2 + 1, Wo = (d.Wi + 2 - 4) / 2 + 1;
-  if (d.ti == GHOST_BF16 && d.ldx == 4 && Wo % 64 == 0 && d.ldy % 4 == 0 && (uintptr_t)d.x % 8 == 0) {
+  if (is16(d.ti) && d.ldx == 4 && Wo % 64 == 0 && d.ldy % 4 == 0 && (uintptr_t)d.x % 8 == 0) {
     FirstMfmaArgs m{};
-    m.x = (const bf16*)d.x; m.w = (const bf16*)d.w; m.y = (bf16*)d.y; m.scale = d.scale; m.shift = d.shift;
+    m.x = d.x; m.w = d.w; m.y = d.y; m.scale = d.scale; m.shift = d.shift;
     m.Hi = d.Hi; m.Wi = d.Wi; m.Ho = Ho; m.Wo = Wo; m.Kpad = d.Kpad; m.ldy = d.ldy; m.slope = d.slope;
     m.M = (long)d.B * Ho * Wo;
-    hipLaunchKernelGGL(conv_first_mfma_kernel, dim3((unsigned)(((m.M / 64 + kFirstChunks - 1) / kFirstChunks + 3) / 4)), dim3(256), 0, s, m);
+    const dim3 g((unsigned)(((m.M / 64 + kFirstChunks - 1) / kFirstChunks + 3) / 4));
+    if (d.ti == GHOST_BF16)
+      hipLaunchKernelGGL(conv_first_mfma_kernel<bf16>, g, dim3(256), 0, s, m);
+    else
+      hipLaunchKernelGGL(conv_first_mfma_kernel<_Float16>, g, dim3(256), 0, s, m);
     return (int)hipGetLastError();
   }
   if (!ws || ws_bytes < conv_first_workspace_bytes() || (uintptr_t)ws % 16) return -1;
   float* wf = reinterpret_cast<float*>(ws);
   if (d.ti == GHOST_BF16)
     hipLaunchKernelGGL(first_weights_kernel<bf16>, dim3(6), dim3(256), 0, s, (const bf16*)d.w, d.Kpad, 32, wf);
+  else if (d.ti == GHOST_F16)
+    hipLaunchKernelGGL(first_weights_kernel<_Float16>, dim3(6), dim3(256), 0, s, (const _Float16*)d.w, d.Kpad, 32, wf);
   else
     hipLaunchKernelGGL(first_weights_kernel<float>, dim3(6), dim3(256), 0, s, (const float*)d.w, d.Kpad, 32, wf);
   FirstArgs a{};
@@ -210,6 +218,8 @@ int conv_first(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t s) {
   dim3 grid((unsigned)((a.M + 255) / 256));
   if (d.ti == GHOST_BF16)
     hipLaunchKernelGGL((conv_first_kernel<bf16, 32>), grid, dim3(256), 0, s, a);
+  else if (d.ti == GHOST_F16)
+    hipLaunchKernelGGL((conv_first_kernel<_Float16, 32>), grid, dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((conv_first_kernel<float, 32>), grid, dim3(256), 0, s, a);
   return (int)hipGetLastError();

@@ -53,12 +53,12 @@ using HaloSmall = HaloCfg<16, 16, 4, 1>;   // W == 16: 16 x 16 tile, 4 waves, 57
 using HaloImg8 = HaloCfg<8, 8, 4, 1, 4>;   // 8 x 8 images, four per tile, 4 waves, 61 KB per stage
 
 struct HaloArgs {
-  const bf16* x;
-  const bf16* w;
-  bf16* y;
+  const void* x;   // 16-bit storage (bf16 or fp16: the kernels' T)
+  const void* w;
+  void* y;
   const float* scale;
   const float* shift;
-  const bf16* res;
+  const void* res;
   int H, W, Cin, ldx, N, Kpad, ldy, ldres, tanh_out;
   float slope;
   int tiles_x, tiles_y, nNt, ntiles;
@@ -67,7 +67,7 @@ struct HaloArgs {
   // epilogue variants of the non-persistent kernel (IBasicBlock convs, arc_runtime.hip): per-channel
   // PReLU slope, residual before the activation, second output y2 = v*scale2 + shift2 (next BN)
   const float* prelu;
-  bf16* y2;
+  void* y2;
   const float* scale2;
   const float* shift2;
   int ldy2, res_first;
@@ -83,8 +83,13 @@ GHOST_DEV int xcd_tile(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
-template <class G>
+template <typename T, class G>
 __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8))) conv3x3_halo_kernel(const HaloArgs a) {
+  T* __restrict__ ay2_ = reinterpret_cast<T*>(a.y2);
+  const T* __restrict__ ax_ = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ aw_ = reinterpret_cast<const T*>(a.w);
+  T* __restrict__ ay_ = reinterpret_cast<T*>(a.y);
+  const T* __restrict__ ares_ = reinterpret_cast<const T*>(a.res);
   constexpr int TH = G::TH, TW = G::TW, BN = G::BN, HWW = G::HWW, HP = G::HP, HPIECES = G::HPIECES;
   constexpr int WPIECES = G::WPIECES, HALO_B = G::HALO_B, NWAVES = G::NW, HPW = G::HPW, WPW = G::WPW;
   constexpr int RPW = 64 / TW;                       // output rows per wave
@@ -102,8 +107,8 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
   const int b = t / a.tiles_y;
   const int y0 = ty * TH, x0 = tx * TW, n0 = nt * BN;
   const long img = (long)b * a.H * a.W;
-  const bf16* __restrict__ xs = a.x + img * a.ldx;            // this sample
-  const bf16* __restrict__ ws = a.w + (long)n0 * a.Kpad;      // this channel tile
+  const T* __restrict__ xs = ax_ + img * a.ldx;            // this sample
+  const T* __restrict__ ws = aw_ + (long)n0 * a.Kpad;      // this channel tile
 
   // this lane's DMA sources (32-bit element offsets within the sample / tile; + channel block)
   const int prow = lane >> 2, slot = lane & 3;
@@ -160,21 +165,21 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
       // nine taps' reads needs ~300 VGPRs; the other waves of the SIMD hide the LDS latency
       asm volatile("" ::: "memory");
       const int dy = tap / 3, dx = tap - dy * 3;
-      bf16x8 wf[4], pf[4];
+      v8_t<T> wf[4], pf[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = wn * 64 + j * 16 + lr;
-        wf[j] = *reinterpret_cast<const bf16x8*>(lds + HALO_B + (tap * BN + n) * 64 + ((lq ^ hswz(n)) * 16));
+        wf[j] = *reinterpret_cast<const v8_t<T>*>(lds + HALO_B + (tap * BN + n) * 64 + ((lq ^ hswz(n)) * 16));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int P = (wm * RPW + (i * 16) / TW + dy) * HWW + (i * 16) % TW + lr + dx;
-        pf[i] = *reinterpret_cast<const bf16x8*>(lds + P * 64 + ((lq ^ hswz(P)) * 16));
+        pf[i] = *reinterpret_cast<const v8_t<T>*>(lds + P * 64 + ((lq ^ hswz(P)) * 16));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], pf[i], acc[j][i], 0, 0, 0);
+        for (int i = 0; i < 4; ++i) acc[j][i] = mfma16x16x32<T>(wf[j], pf[i], acc[j][i]);
     }
     __syncthreads();   // every wave is done with this block's LDS before the next DMA
   }
@@ -193,9 +198,9 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
       if (n >= a.N) continue;
       float v[4];
       float rv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (a.res) {
-        const uint2 raw = *reinterpret_cast<const uint2*>(a.res + pix * a.ldres + n);
-        const bf16* e = reinterpret_cast<const bf16*>(&raw);
+      if (ares_) {
+        const uint2 raw = *reinterpret_cast<const uint2*>(ares_ + pix * a.ldres + n);
+        const T* e = reinterpret_cast<const T*>(&raw);
 #pragma unroll
         for (int r = 0; r < 4; ++r) rv[r] = (float)e[r];
       }
@@ -213,14 +218,14 @@ __global__ void __launch_bounds__(G::NW * 64) __attribute__((amdgpu_waves_per_eu
         v[r] = s;
       }
       uint2 o;
-      bf16* oe = reinterpret_cast<bf16*>(&o);
+      T* oe = reinterpret_cast<T*>(&o);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) oe[r] = (bf16)v[r];
-      *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
-      if (a.y2) {
+      for (int r = 0; r < 4; ++r) oe[r] = (T)v[r];
+      *reinterpret_cast<uint2*>(ay_ + pix * a.ldy + n) = o;
+      if (ay2_) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) oe[r] = (bf16)(v[r] * a.scale2[n + r] + a.shift2[n + r]);
-        *reinterpret_cast<uint2*>(a.y2 + pix * a.ldy2 + n) = o;
+        for (int r = 0; r < 4; ++r) oe[r] = (T)(v[r] * a.scale2[n + r] + a.shift2[n + r]);
+        *reinterpret_cast<uint2*>(ay2_ + pix * a.ldy2 + n) = o;
       }
     }
   }
@@ -252,8 +257,13 @@ GHOST_DEV void pp_unroll(std::integer_sequence<int, P...>, F&& f) {
 // G = HaloWide (exact 16 x 32 tiles, the generator) or HaloSmall: 16 x 16 tiles that may overhang
 // the image (ArcFace 112 .. 14), 4 waves, with the IBasicBlock epilogue (per-channel PReLU, residual
 // before or after it, second output y2 = v*scale2 + shift2 = the next block's BatchNorm).
-template <class G, bool RESW, bool STATS, int NCB, int DBG = 0>
+template <typename T, class G, bool RESW, bool STATS, int NCB, int DBG = 0>
 __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloArgs a) {
+  T* __restrict__ ay2_ = reinterpret_cast<T*>(a.y2);
+  const T* __restrict__ ax_ = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ aw_ = reinterpret_cast<const T*>(a.w);
+  T* __restrict__ ay_ = reinterpret_cast<T*>(a.y);
+  const T* __restrict__ ares_ = reinterpret_cast<const T*>(a.res);
   static_assert(NCB % 2 == 0 && NCB <= 32 && (!RESW || NCB == 2), "channel blocks per tile");
   constexpr bool EPX = G::TW == 16;   // small tiles: overhang masking + the extended epilogue
   static_assert(!(EPX && STATS), "IN partials only from exact tiles");
@@ -283,8 +293,8 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     s_sh[n] = a.shift ? a.shift[n] : 0.f;
     if constexpr (EPX) {
       s_ex[n] = a.prelu ? a.prelu[n] : a.slope;
-      s_ex[512 + n] = a.y2 ? a.scale2[n] : 0.f;
-      s_ex[1024 + n] = a.y2 ? a.shift2[n] : 0.f;
+      s_ex[512 + n] = ay2_ ? a.scale2[n] : 0.f;
+      s_ex[1024 + n] = ay2_ ? a.shift2[n] : 0.f;
     }
   }
   constexpr int ncb = NCB;
@@ -304,7 +314,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       for (int j = 0; j < WPW; ++j) {
         const int piece = wid + j * NW;
         if (piece < WPIECES)
-          __builtin_amdgcn_global_load_lds(a.w + w_off[j] + cb * 288, wres + cb * WBLK_B + piece * 1024, 16, 0, 0);
+          __builtin_amdgcn_global_load_lds(aw_ + w_off[j] + cb * 288, wres + cb * WBLK_B + piece * 1024, 16, 0, 0);
       }
   }
 #endif
@@ -354,7 +364,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   };
   auto issue = [&](unsigned char* buf, int cb) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const bf16* __restrict__ xs = a.x + dma_base + cb * 32;
+    const T* __restrict__ xs = ax_ + dma_base + cb * 32;
 #pragma unroll
     for (int j = 0; j < HPW; ++j) {
       const int piece = wid + j * NW;
@@ -364,7 +374,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       }
     }
     if constexpr (!RESW && !(DBG & 4)) {
-      const bf16* __restrict__ ws = a.w + (long)dma_n0 * a.Kpad + cb * 288;
+      const T* __restrict__ ws = aw_ + (long)dma_n0 * a.Kpad + cb * 288;
 #pragma unroll
       for (int j = 0; j < WPW; ++j) {
         const int piece = wid + j * NW;
@@ -415,19 +425,19 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     const unsigned char* wb = RESW ? wres + cb * WBLK_B : buf + HALO_B;
     // fragments of tap t + 1 are read while tap t's 16 MFMAs run (two register sets): the wave never
     // waits for its own LDS reads except at the first tap of a stage
-    bf16x8 wf[2][4], pf[2][4];
-    auto load_frags = [&](int tap, bf16x8 (&w)[4], bf16x8 (&p)[4]) {
+    v8_t<T> wf[2][4], pf[2][4];
+    auto load_frags = [&](int tap, v8_t<T> (&w)[4], v8_t<T> (&p)[4]) {
       const int dy = tap / 3, dx = tap - dy * 3;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = j * 16 + lr;
-        w[j] = *reinterpret_cast<const bf16x8*>(wb + (tap * 64 + n) * 64 + ((lq ^ hswz(n)) * 16));
+        w[j] = *reinterpret_cast<const v8_t<T>*>(wb + (tap * 64 + n) * 64 + ((lq ^ hswz(n)) * 16));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int q = i * 16 + lr;   // the wave's pixel (row q / TW, column q % TW of its 64)
         const int P = G::himg(wid) + (G::hrow0(wid) + q / TW + dy) * HWW + q % TW + dx;
-        p[i] = *reinterpret_cast<const bf16x8*>(buf + P * 64 + ((lq ^ hswz(P)) * 16));
+        p[i] = *reinterpret_cast<const v8_t<T>*>(buf + P * 64 + ((lq ^ hswz(P)) * 16));
       }
     };
     // (measured: the same time as one register set read then used, and with s_setprio around the MFMAs)
@@ -441,7 +451,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tap & 1][j], pf[tap & 1][i], acc[j][i], 0, 0, 0);
+            acc[j][i] = mfma16x16x32<T>(wf[tap & 1][j], pf[tap & 1][i], acc[j][i]);
       }
     }
     if constexpr (cb + 1 < NCB) return;
@@ -449,7 +459,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     // youngest VM ops when the next tile's first stage waits.  The residual tile is loaded as one
     // batch first: a load between two stores would wait for the older store (in-order vmcnt)
     uint2 rraw[4][4];
-    if (a.res) {
+    if (ares_) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int q = i * 16 + lr;
@@ -458,7 +468,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
         const bool in = !EPX || (oy < a.H && ox < a.W);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          rraw[i][j] = in ? *reinterpret_cast<const uint2*>(a.res + pix * a.ldres + cur.n0 + j * 16 + lq * 4)
+          rraw[i][j] = in ? *reinterpret_cast<const uint2*>(ares_ + pix * a.ldres + cur.n0 + j * 16 + lq * 4)
                           : make_uint2(0u, 0u);
       }
     }
@@ -467,7 +477,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       const int q = i * 16 + lr;
       const int oy = cur.y0 + G::hrow0(wid) + q / TW, ox = cur.x0 + q % TW;
       const long pix = cur.base + (IMG > 1 ? (long)wid * a.H * a.W : 0L) + (long)oy * a.W + ox;
-      uint2 ov[4];   // W16: the 4 channel fragments' bf16 outputs, stored 16 bytes at a time below
+      uint2 ov[4];   // W16: the 4 channel fragments' T outputs, stored 16 bytes at a time below
       if constexpr (EPX) {
         if (oy >= a.H || ox >= a.W) {
 #pragma unroll
@@ -479,13 +489,13 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       for (int j = 0; j < 4; ++j) {
         const int n = cur.n0 + j * 16 + lq * 4;
         float rv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (a.res) {
-          const bf16* e = reinterpret_cast<const bf16*>(&rraw[i][j]);
+        if (ares_) {
+          const T* e = reinterpret_cast<const T*>(&rraw[i][j]);
 #pragma unroll
           for (int r = 0; r < 4; ++r) rv[r] = (float)e[r];
         }
         uint2 o;
-        bf16* oe = reinterpret_cast<bf16*>(&o);
+        T* oe = reinterpret_cast<T*>(&o);
         // the lane's 4 channels' tables as one 16-byte LDS read each (n % 4 == 0), not 4 scalar reads
         const f32x4 tsc = *reinterpret_cast<const f32x4*>(s_sc + n);
         const f32x4 tsh = *reinterpret_cast<const f32x4*>(s_sh + n);
@@ -501,16 +511,16 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
             if (!a.res_first) t += rv[r];
             if (a.tanh_out) t = tanhf(t);
             v[r] = t;
-            oe[r] = (bf16)t;
+            oe[r] = (T)t;
             acc[j][i][r] = 0.f;
           }
-          *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
-          if (a.y2) {
+          *reinterpret_cast<uint2*>(ay_ + pix * a.ldy + n) = o;
+          if (ay2_) {
             const f32x4 tsc2 = *reinterpret_cast<const f32x4*>(s_ex + 512 + n);
             const f32x4 tsh2 = *reinterpret_cast<const f32x4*>(s_ex + 1024 + n);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) oe[r] = (bf16)(v[r] * tsc2[r] + tsh2[r]);
-            *reinterpret_cast<uint2*>(a.y2 + pix * a.ldy2 + n) = o;
+            for (int r = 0; r < 4; ++r) oe[r] = (T)(v[r] * tsc2[r] + tsh2[r]);
+            *reinterpret_cast<uint2*>(ay2_ + pix * a.ldy2 + n) = o;
           }
         } else {
 #pragma unroll
@@ -519,12 +529,12 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
           v = v > 0.f ? v : v * a.slope;
           v += rv[r];
           if (a.tanh_out) v = tanhf(v);
-          oe[r] = (bf16)v;
+          oe[r] = (T)v;
           acc[j][i][r] = STATS ? (float)oe[r] : 0.f;   // the stored (rounded) value, for the statistics
         }
         if constexpr (W16) ov[j] = o;
-        else if constexpr (!(DBG & 16)) *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
-        else if ((o.x ^ o.y) == 0x7fc00001u) *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+        else if constexpr (!(DBG & 16)) *reinterpret_cast<uint2*>(ay_ + pix * a.ldy + n) = o;
+        else if ((o.x ^ o.y) == 0x7fc00001u) *reinterpret_cast<uint2*>(ay_ + pix * a.ldy + n) = o;
         }
       }
       if constexpr (W16) {
@@ -540,14 +550,14 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
         gb.y = (unsigned)__shfl_xor((int)sb.y, 16, 64);
         const uint2 a0 = odd ? ga : ov[0], a1 = odd ? ov[1] : ga;
         const uint2 b0 = odd ? gb : ov[2], b1 = odd ? ov[3] : gb;
-        bf16* yp = a.y + pix * a.ldy + cur.n0 + (lq & 2) * 4;
+        T* yp = ay_ + pix * a.ldy + cur.n0 + (lq & 2) * 4;
         *reinterpret_cast<u32x4*>(yp + (odd ? 16 : 0)) = u32x4{a0.x, a0.y, a1.x, a1.y};
         *reinterpret_cast<u32x4*>(yp + (odd ? 48 : 32)) = u32x4{b0.x, b0.y, b1.x, b1.y};
       }
     }
     if constexpr (STATS) {
       // InstanceNorm partials of this wave's 64 pixels (AADLayer.py:16,24 reads this tensor next):
-      // per channel the mean and the centred sum of squares of the stored (bf16-rounded) values,
+      // per channel the mean and the centred sum of squares of the stored (T-rounded) values,
       // two passes over registers; in_stats_from_tiles merges them in fp64 (Chan).  The 16 channel
       // sums of a lane are reduced over the 16 lanes of its row by a transpose-reduce (8+4+2+1 DPP
       // exchanges) that leaves channel k = lr in lane lr; the mean goes back by the reverse.
@@ -659,20 +669,24 @@ struct HaloTCfg {
 };
 
 struct HaloTArgs {
-  const bf16* x;
-  const bf16* w;      // [4][Npad][Kpad], K = (cb*4 + ty*2 + tx)*32 + c
-  bf16* y;
+  const void* x;
+  const void* w;      // [4][Npad][Kpad], K = (cb*4 + ty*2 + tx)*32 + c
+  void* y;
   const float* scale;
   const float* shift;
-  const bf16* res;
+  const void* res;
   long wpar;          // Npad * Kpad
   int H, W, Cin, ldx, N, Kpad, ldy, ldres;
   float slope;
   int tiles_x, tiles_y, nNt;
 };
 
-template <int BN>
+template <typename T, int BN>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) convT_halo_kernel(const HaloTArgs a) {
+  const T* __restrict__ ax_ = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ aw_ = reinterpret_cast<const T*>(a.w);
+  T* __restrict__ ay_ = reinterpret_cast<T*>(a.y);
+  const T* __restrict__ ares_ = reinterpret_cast<const T*>(a.res);
   using G = HaloTCfg<BN>;
   constexpr int HWW = G::HWW, HP = G::HP, HPIECES = G::HPIECES, WPIECES = G::WPIECES, HALO_B = G::HALO_B;
   constexpr int NWAVES = G::NW, HPW = G::HPW, WPW = G::WPW, TN = G::TN;
@@ -687,7 +701,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   const int ty = t % a.tiles_y;
   const int b = t / a.tiles_y;
   const int y0 = ty * G::TIH, x0 = tx * G::TIW, n0 = nt * BN;
-  const bf16* __restrict__ xs = a.x + (long)b * a.H * a.W * a.ldx;
+  const T* __restrict__ xs = ax_ + (long)b * a.H * a.W * a.ldx;
 
   const int prow = lane >> 2, slot = lane & 3;
   int h_off[HPW];
@@ -702,12 +716,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     h_off[j] = ok ? (iy * a.W + ix) * a.ldx + ((slot ^ hswz(P)) * 8) : 0;
     h_ok |= (ok ? 1u : 0u) << j;
   }
-  const bf16* wsrc[WPW];
+  const T* wsrc[WPW];
 #pragma unroll
   for (int j = 0; j < WPW; ++j) {
     const int piece = wid + j * NWAVES;               // = (phase*4 + tap) * BN/16 + row group
     const int pt = piece / (BN / 16), n = (piece % (BN / 16)) * 16 + prow;
-    wsrc[j] = a.w + (pt >> 2) * a.wpar + (long)(n0 + n) * a.Kpad + (pt & 3) * 32 + ((slot ^ hswz(n)) * 8);
+    wsrc[j] = aw_ + (pt >> 2) * a.wpar + (long)(n0 + n) * a.Kpad + (pt & 3) * 32 + ((slot ^ hswz(n)) * 8);
   }
 
   f32x4 acc[TN][4];
@@ -739,21 +753,21 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     for (int tp = 0; tp < 4; ++tp) {
       asm volatile("" ::: "memory");
       const int dy = py - (tp >> 1), dx = px - (tp & 1);     // input offset of this tap
-      bf16x8 wf[TN], pf[4];
+      v8_t<T> wf[TN], pf[4];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = j * 16 + lr;
-        wf[j] = *reinterpret_cast<const bf16x8*>(lds + HALO_B + ((ph * 4 + tp) * BN + n) * 64 + ((lq ^ hswz(n)) * 16));
+        wf[j] = *reinterpret_cast<const v8_t<T>*>(lds + HALO_B + ((ph * 4 + tp) * BN + n) * 64 + ((lq ^ hswz(n)) * 16));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int P = (hf * 4 + i + 1 + dy) * HWW + lr + 1 + dx;
-        pf[i] = *reinterpret_cast<const bf16x8*>(lds + P * 64 + ((lq ^ hswz(P)) * 16));
+        pf[i] = *reinterpret_cast<const v8_t<T>*>(lds + P * 64 + ((lq ^ hswz(P)) * 16));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], pf[i], acc[j][i], 0, 0, 0);
+        for (int i = 0; i < 4; ++i) acc[j][i] = mfma16x16x32<T>(wf[j], pf[i], acc[j][i]);
     }
     __syncthreads();
   }
@@ -768,30 +782,30 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       const int n = n0 + j * 16 + lq * 4;
       if (n >= a.N) continue;
       float rv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (a.res) {
-        const uint2 raw = *reinterpret_cast<const uint2*>(a.res + pix * a.ldres + n);
-        const bf16* e = reinterpret_cast<const bf16*>(&raw);
+      if (ares_) {
+        const uint2 raw = *reinterpret_cast<const uint2*>(ares_ + pix * a.ldres + n);
+        const T* e = reinterpret_cast<const T*>(&raw);
 #pragma unroll
         for (int r = 0; r < 4; ++r) rv[r] = (float)e[r];
       }
       uint2 o;
-      bf16* oe = reinterpret_cast<bf16*>(&o);
+      T* oe = reinterpret_cast<T*>(&o);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = acc[j][i][r];
         if (a.scale) v *= a.scale[n + r];
         if (a.shift) v += a.shift[n + r];
         v = v > 0.f ? v : v * a.slope;
-        oe[r] = (bf16)(v + rv[r]);
+        oe[r] = (T)(v + rv[r]);
       }
-      *reinterpret_cast<uint2*>(a.y + pix * a.ldy + n) = o;
+      *reinterpret_cast<uint2*>(ay_ + pix * a.ldy + n) = o;
     }
   }
 }
 
 bool convT_halo_supported(const ConvDesc& d) {
   static const int enabled = GHOST_KNOB("GHOST_CONVT_HALO", 1);
-  if (!enabled || d.kind != CONV_T4S2 || d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD) return false;
+  if (!enabled || d.kind != CONV_T4S2 || !is16(d.ti) || d.to != d.ti || d.epi != EPI_STD) return false;
   if (d.u8 || d.tanh_out || d.force_split || d.Cin % 32 || d.ldx % 8 || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
   if (d.res_first || d.prelu || d.y2) return false;   // epilogue variants only the implicit GEMM has
   if (d.Hi % HaloTCfg<64>::TIH || d.Wi % HaloTCfg<64>::TIW || d.Kpad < 4 * d.Cin) return false;
@@ -800,23 +814,24 @@ bool convT_halo_supported(const ConvDesc& d) {
   return (long)d.Hi * d.Wi * d.ldx < (1L << 31);
 }
 
-template <int BN>
+template <typename T, int BN>
 static int haloT_launch(const ConvDesc& d, hipStream_t s) {
   HaloTArgs a{};
-  a.x = (const bf16*)d.x; a.w = (const bf16*)d.w; a.y = (bf16*)d.y;
-  a.scale = d.scale; a.shift = d.shift; a.res = (const bf16*)d.res;
+  a.x = d.x; a.w = d.w; a.y = d.y;
+  a.scale = d.scale; a.shift = d.shift; a.res = d.res;
   a.wpar = (long)d.Npad * d.Kpad;
   a.H = d.Hi; a.W = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx; a.N = d.N; a.Kpad = d.Kpad;
   a.ldy = d.ldy; a.ldres = d.ldres; a.slope = d.slope;
   a.tiles_x = d.Wi / HaloTCfg<BN>::TIW; a.tiles_y = d.Hi / HaloTCfg<BN>::TIH; a.nNt = (d.N + BN - 1) / BN;
   const long ntiles = (long)d.B * a.tiles_x * a.tiles_y * a.nNt;
-  hipLaunchKernelGGL(convT_halo_kernel<BN>, dim3((unsigned)ntiles), dim3(512), 0, s, a);
+  hipLaunchKernelGGL((convT_halo_kernel<T, BN>), dim3((unsigned)ntiles), dim3(512), 0, s, a);
   return (int)hipGetLastError();
 }
 
 int convT_halo(const ConvDesc& d, hipStream_t s) {
   if (!convT_halo_supported(d)) return -1;
-  return d.N == 32 ? haloT_launch<32>(d, s) : haloT_launch<64>(d, s);
+  if (d.ti == GHOST_F16) return d.N == 32 ? haloT_launch<_Float16, 32>(d, s) : haloT_launch<_Float16, 64>(d, s);
+  return d.N == 32 ? haloT_launch<bf16, 32>(d, s) : haloT_launch<bf16, 64>(d, s);
 }
 
 // which tile the non-persistent kernel uses: 16 x 32 when the image is a multiple of it (every
@@ -827,8 +842,12 @@ static bool halo_exact_wide(const ConvDesc& d) { return d.Wi % HaloWide::TW == 0
 // the 8 x 8 stage: four whole images per tile (HaloImg8)
 static bool halo_img8(const ConvDesc& d) {
   static const int on = GHOST_KNOB("GHOST_HALO_IMG8", 1);
+  const int ncb = d.Cin / 32;
+  // (only shapes the persistent IMG8 kernel is instantiated for, with its 16-byte stores: anything else
+  // falls through to the implicit GEMM instead of failing in conv3x3_halo)
   return on && d.Hi == HaloImg8::TH && d.Wi == HaloImg8::TW && d.B % HaloImg8::IMG == 0 && d.N <= 1024 &&
-         !d.prelu && !d.y2 && !d.res_first && !d.tanh_out && d.Cin % 64 == 0 && d.Cin <= 1024;
+         !d.prelu && !d.y2 && !d.res_first && !d.tanh_out && d.Cin % 64 == 0 && d.Cin <= 1024 &&
+         (ncb == 2 || ncb == 4 || ncb == 8 || ncb == 16 || ncb == 32) && d.ldy % 8 == 0 && (uintptr_t)d.y % 16 == 0;
 }
 static bool halo_small_ok(const ConvDesc& d) {
   const long tx = (d.Wi + HaloSmall::TW - 1) / HaloSmall::TW, ty = (d.Hi + HaloSmall::TH - 1) / HaloSmall::TH;
@@ -838,7 +857,7 @@ static bool halo_small_ok(const ConvDesc& d) {
 bool conv3x3_halo_supported(const ConvDesc& d) {
   static const int enabled = GHOST_KNOB("GHOST_CONV_HALO", 1);
   if (!enabled || d.kind != CONV_FWD || d.kh != 3 || d.kw != 3 || d.stride != 1 || d.pad != 1) return false;
-  if (d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD || d.u8 || d.force_split) return false;
+  if (!is16(d.ti) || d.to != d.ti || d.epi != EPI_STD || d.u8 || d.force_split) return false;
   if (d.Cin % 32 || d.ldx % 8 || d.N % 64 || d.ldy % 4 || (d.res && d.ldres % 4)) return false;
   if (d.y2 && (d.ldy2 % 4 || (uintptr_t)d.y2 % 8 || !d.scale2 || !d.shift2)) return false;
   if ((!halo_exact_wide(d) && !halo_small_ok(d) && !halo_img8(d)) || d.Kpad < 9 * d.Cin || d.Npad < d.N) return false;
@@ -850,19 +869,19 @@ bool conv3x3_halo_supported(const ConvDesc& d) {
   return d.N <= max_n;
 }
 
-template <class G>
+template <typename T, class G>
 static int halo_launch(const ConvDesc& d, hipStream_t s) {
   HaloArgs a{};
-  a.x = (const bf16*)d.x; a.w = (const bf16*)d.w; a.y = (bf16*)d.y;
-  a.scale = d.scale; a.shift = d.shift; a.res = (const bf16*)d.res;
+  a.x = d.x; a.w = d.w; a.y = d.y;
+  a.scale = d.scale; a.shift = d.shift; a.res = d.res;
   a.H = d.Hi; a.W = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx; a.N = d.N; a.Kpad = d.Kpad;
   a.ldy = d.ldy; a.ldres = d.ldres; a.tanh_out = d.tanh_out; a.slope = d.slope;
-  a.prelu = d.prelu; a.y2 = (bf16*)d.y2; a.scale2 = d.scale2; a.shift2 = d.shift2; a.ldy2 = d.ldy2;
+  a.prelu = d.prelu; a.y2 = d.y2; a.scale2 = d.scale2; a.shift2 = d.shift2; a.ldy2 = d.ldy2;
   a.res_first = d.res_first;
   a.tiles_x = (d.Wi + G::TW - 1) / G::TW; a.tiles_y = (d.Hi + G::TH - 1) / G::TH;
   a.nNt = (d.N + G::BN - 1) / G::BN;
   a.ntiles = d.B * a.tiles_x * a.tiles_y * a.nNt;
-  hipLaunchKernelGGL(conv3x3_halo_kernel<G>, dim3((unsigned)a.ntiles), dim3(G::NW * 64), 0, s, a);
+  hipLaunchKernelGGL((conv3x3_halo_kernel<T, G>), dim3((unsigned)a.ntiles), dim3(G::NW * 64), 0, s, a);
   return (int)hipGetLastError();
 }
 
@@ -886,14 +905,14 @@ static bool pp_small(const ConvDesc& d) {
          (force || d.Wi % HaloSmall::TW || d.Hi % HaloSmall::TH || d.prelu || d.y2 || d.res_first);
 }
 
-template <class G>
+template <typename T, class G>
 static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   HaloArgs a{};
-  a.x = (const bf16*)d.x; a.w = (const bf16*)d.w; a.y = (bf16*)d.y;
-  a.scale = d.scale; a.shift = d.shift; a.res = (const bf16*)d.res;
+  a.x = d.x; a.w = d.w; a.y = d.y;
+  a.scale = d.scale; a.shift = d.shift; a.res = d.res;
   a.H = d.Hi; a.W = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx; a.N = d.N; a.Kpad = d.Kpad;
   a.ldy = d.ldy; a.ldres = d.ldres; a.tanh_out = d.tanh_out; a.slope = d.slope;
-  a.prelu = d.prelu; a.y2 = (bf16*)d.y2; a.scale2 = d.scale2; a.shift2 = d.shift2; a.ldy2 = d.ldy2;
+  a.prelu = d.prelu; a.y2 = d.y2; a.scale2 = d.scale2; a.shift2 = d.shift2; a.ldy2 = d.ldy2;
   a.res_first = d.res_first;
   a.tiles_x = (d.Wi + G::TW - 1) / G::TW; a.tiles_y = (d.Hi + G::TH - 1) / G::TH; a.nNt = d.N / 64;
   a.ntiles = d.B / G::IMG * a.tiles_x * a.tiles_y * a.nNt;
@@ -909,7 +928,7 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
     if (dbg && !a.in_part) {   // experiment variants (tuning builds only)
 #define GHOST_PP_DBG(R, NB, V)                                                                               \
   if (resw == R && ncb == NB && dbg == V) {                                                                 \
-    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<G, R, false, NB, V>), dim3((unsigned)g), dim3(NT), 0, s, a); \
+    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<T, G, R, false, NB, V>), dim3((unsigned)g), dim3(NT), 0, s, a); \
     return (int)hipGetLastError();                                                                          \
   }
       GHOST_PP_DBG(true, 2, 2) GHOST_PP_DBG(true, 2, 8) GHOST_PP_DBG(true, 2, 16) GHOST_PP_DBG(true, 2, 18)
@@ -923,7 +942,7 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
 #endif
   constexpr bool CAN_ST = G::TW == 32 || G::IMG > 1;
 #define GHOST_PP(R, ST, NB) \
-  hipLaunchKernelGGL((conv3x3_halo_pp_kernel<G, R, ST, NB>), dim3((unsigned)g), dim3(NT), 0, s, a)
+  hipLaunchKernelGGL((conv3x3_halo_pp_kernel<T, G, R, ST, NB>), dim3((unsigned)g), dim3(NT), 0, s, a)
 #define GHOST_PP2(R, NB)                                  \
   if constexpr (CAN_ST) {                                  \
     if (a.in_part) GHOST_PP(R, CAN_ST, NB); else GHOST_PP(R, false, NB); \
@@ -971,18 +990,23 @@ bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
   return ok;
 }
 
-int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
-  if (!conv3x3_halo_supported(d)) return -1;
-  if (halo_img8(d)) return conv3x3_pp_takes(d, nullptr) ? halo_pp_launch<HaloImg8>(d, s) : -1;
-  if (conv3x3_pp_takes(d, nullptr)) return halo_pp_launch<HaloWide>(d, s);
+template <typename T>
+static int conv3x3_halo_t(const ConvDesc& d, hipStream_t s) {
+  if (halo_img8(d)) return conv3x3_pp_takes(d, nullptr) ? halo_pp_launch<T, HaloImg8>(d, s) : -1;
+  if (conv3x3_pp_takes(d, nullptr)) return halo_pp_launch<T, HaloWide>(d, s);
   if (d.in_part) return -1;   // only the persistent 16 x 32 kernel writes InstanceNorm partials
   static const int pp = GHOST_KNOB("GHOST_HALO_PP", 1);
   const int ncb = d.Cin / 32;
   if (pp && pp_small(d) && d.N <= 512 && d.Cin % 64 == 0 &&
       (ncb == 2 || ncb == 4 || ncb == 6 || ncb == 8 || ncb == 16 || ncb == 32))
-    return halo_pp_launch<HaloSmall>(d, s);
-  if (halo_exact_wide(d)) return halo_launch<HaloWide>(d, s);
-  return halo_launch<HaloSmall>(d, s);
+    return halo_pp_launch<T, HaloSmall>(d, s);
+  if (halo_exact_wide(d)) return halo_launch<T, HaloWide>(d, s);
+  return halo_launch<T, HaloSmall>(d, s);
+}
+
+int conv3x3_halo(const ConvDesc& d, hipStream_t s) {
+  if (!conv3x3_halo_supported(d)) return -1;
+  return d.ti == GHOST_F16 ? conv3x3_halo_t<_Float16>(d, s) : conv3x3_halo_t<bf16>(d, s);
 }
 
 }  // namespace ghost

@@ -258,16 +258,16 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
     if constexpr (sizeof(TI) == 2) {
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8 af[TM], bfv[TN];
+        v8_t<TI> af[TM], bfv[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + i * 16 * LDR + ks * 32 + lq * 8);
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const v8_t<TI>*>(Ab + i * 16 * LDR + ks * 32 + lq * 8);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const bf16x8*>(Bb + j * 16 * LDR + ks * 32 + lq * 8);
+        for (int j = 0; j < TN; ++j) bfv[j] = *reinterpret_cast<const v8_t<TI>*>(Bb + j * 16 * LDR + ks * 32 + lq * 8);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16x16x32<TI>(af[i], bfv[j], acc[i][j]);
       }
     } else {
 #pragma unroll
@@ -394,8 +394,8 @@ GHOST_DEV void wait_stages(int after) {
 }
 
 // issue the LDS-DMA of K tile `kt` into ring slot `sb` (one 16-row piece per instruction)
-template <int BM, int NA, int NB>
-GHOST_DEV void glds_issue(const ConvArgs& a, const bf16* __restrict__ x, const bf16* const (&b_src)[NB],
+template <typename T, int BM, int NA, int NB>
+GHOST_DEV void glds_issue(const ConvArgs& a, const T* __restrict__ x, const T* const (&b_src)[NB],
                           const long (&a_off)[NA], const uint64_t (&a_mask)[NA], const int (&a_gc)[NA], int wid,
                           int kt, unsigned char* sb) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the amdgcn builtin does not exist in the host pass of this TU
@@ -417,10 +417,10 @@ GHOST_DEV void glds_issue(const ConvArgs& a, const bf16* __restrict__ x, const b
 
 // WSL = 4: warp-specialised form, 512 threads: waves 0-3 run the MFMAs and the epilogue, waves 4-7 only issue
 // the ring's LDS-DMA (same ring, same per-K-step barrier), so no compute wave pays the DMA issue cost
-template <int BM, int BN, int STAGES, int EPI, int WSL = 0>
+template <typename T, int BM, int BN, int STAGES, int EPI, int WSL = 0>
 __global__ void __launch_bounds__(WSL ? 512 : 256) conv_glds_kernel(const ConvArgs a) {
-  typedef bf16 TI;
-  typedef bf16 TO;
+  typedef T TI;
+  typedef T TO;
   constexpr int WM = WaveGrid<BM, BN>::WM, WN = WaveGrid<BM, BN>::WN;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -500,7 +500,7 @@ __global__ void __launch_bounds__(WSL ? 512 : 256) conv_glds_kernel(const ConvAr
   if (loads) {
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
-      if (s < n) glds_issue<BM, NA, NB>(a, x, b_src, a_off, a_mask, a_gc, lw, kt0 + s, lds + s * STAGE_B);
+      if (s < n) glds_issue<T, BM, NA, NB>(a, x, b_src, a_off, a_mask, a_gc, lw, kt0 + s, lds + s * STAGE_B);
   }
   for (int it = 0; it < n; ++it) {
     // stages issued after `it` that may stay in flight
@@ -508,27 +508,27 @@ __global__ void __launch_bounds__(WSL ? 512 : 256) conv_glds_kernel(const ConvAr
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (loads && it + STAGES - 1 < n)
-      glds_issue<BM, NA, NB>(a, x, b_src, a_off, a_mask, a_gc, lw, kt0 + it + STAGES - 1,
+      glds_issue<T, BM, NA, NB>(a, x, b_src, a_off, a_mask, a_gc, lw, kt0 + it + STAGES - 1,
                              lds + ((it + STAGES - 1) % STAGES) * STAGE_B);
     if (!computes) continue;
     const unsigned char* sb = lds + (it % STAGES) * STAGE_B;
     const unsigned char* As = sb;
     const unsigned char* Bs = sb + BM * 64;
-    bf16x8 af[TM], bfv[TN];
+    v8_t<T> af[TM], bfv[TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int r = wm * WTM + i * 16 + lr;
-      af[i] = *reinterpret_cast<const bf16x8*>(As + r * 64 + swz(r, lq) * 16);
+      af[i] = *reinterpret_cast<const v8_t<T>*>(As + r * 64 + swz(r, lq) * 16);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int r = wn * WTN + j * 16 + lr;
-      bfv[j] = *reinterpret_cast<const bf16x8*>(Bs + r * 64 + swz(r, lq) * 16);
+      bfv[j] = *reinterpret_cast<const v8_t<T>*>(Bs + r * 64 + swz(r, lq) * 16);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32<T>(af[i], bfv[j], acc[i][j]);
   }
 
   if (!computes) return;
@@ -591,7 +591,7 @@ Plan make_plan(const ConvDesc& d) {
     p.Wo = (d.Wi + 2 * d.pad - d.kw) / d.stride + 1;
   }
   p.M = d.B * p.Ho * p.Wo;
-  const bool bf = d.ti == GHOST_BF16;
+  const bool bf = is16(d.ti);   // 16-bit operands (bf16 or fp16)
   const int vec = bf ? 8 : 4;
   p.fast = (d.Cin % 32 == 0) && (d.ldx % vec == 0) && ((uintptr_t)d.x % 16 == 0);
   // BK = 64 pays only on deep reductions (measured: 256x64 tiles lose 2x at BK 64 from LDS occupancy)
@@ -627,7 +627,7 @@ Plan make_plan(const ConvDesc& d) {
   // (only grids that need split-K: with >= 256 tiles of 128 x 128 the two-workgroup register-staged
   // kernel measured faster, e.g. the 8x8 AAD GEMM 55 vs 74 us)
   const long tiles128 = (long)((p.M + 127) / 128) * ((d.N + 127) / 128) * p.npar;
-  if (deep > 0 && bf && p.fast && d.to == GHOST_BF16 && p.M <= 8192 && d.N >= 256 && d.Kpad >= 1024 &&
+  if (deep > 0 && bf && p.fast && d.to == d.ti && p.M <= 8192 && d.N >= 256 && d.Kpad >= 1024 &&
       d.N % 128 == 0 && tiles128 < 256) {
     p.BM = 128; p.BN = 128; p.BK = 32; p.stages = deep;
   }
@@ -667,7 +667,7 @@ Plan make_plan(const ConvDesc& d) {
   p.nsplit = (nk + p.kt_per_split - 1) / p.kt_per_split;
   // bf16 operands with an fp32 output (the ArcFace embedding layer): the GEMM always writes fp32
   // partials and the reduction kernel applies the epilogue in fp32
-  p.partial = p.nsplit > 1 || (d.ti == GHOST_BF16 && d.to == GHOST_F32);
+  p.partial = p.nsplit > 1 || (is16(d.ti) && d.to == GHOST_F32);
   return p;
 }
 
@@ -738,7 +738,7 @@ int dispatch_tile(const ConvArgs& a, const Plan& p, hipStream_t s) {
 #undef GHOST_TILE
 }
 
-template <int EPI>
+template <typename T, int EPI>
 bool launch_glds(const ConvArgs& a, const Plan& p, hipStream_t s) {
   static const int stages_knob = GHOST_KNOB("GHOST_CONV_STAGES", 3);
   // warp-specialised DMA waves (B = 64, same box: 4x4 3x3 1024 conv 50 -> 41 us, encoder conv5..7 49 / 47 / 32 ->
@@ -749,13 +749,13 @@ bool launch_glds(const ConvArgs& a, const Plan& p, hipStream_t s) {
   if constexpr (EPI == KEPI_AAD) {
     if (p.BM == 128 && p.BN == 128 && stages == 8) {
       if (ws)
-        hipLaunchKernelGGL((conv_glds_kernel<128, 128, 8, EPI, 4>), grid, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, 8, EPI, 4>), grid, dim3(512), 0, s, a);
       else
-        hipLaunchKernelGGL((conv_glds_kernel<128, 128, 8, EPI>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, 8, EPI>), grid, dim3(256), 0, s, a);
       return true;
     }
     if (p.BM == 128 && p.BN == 128 && stages == 3 && ws) {
-      hipLaunchKernelGGL((conv_glds_kernel<128, 128, 3, EPI, 4>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((conv_glds_kernel<T, 128, 128, 3, EPI, 4>), grid, dim3(512), 0, s, a);
       return true;
     }
     return false;
@@ -763,9 +763,9 @@ bool launch_glds(const ConvArgs& a, const Plan& p, hipStream_t s) {
 #define GHOST_G(bm, bn, st)                                                                      \
   if (p.BM == bm && p.BN == bn && stages == st) {                                                \
     if (ws)                                                                                       \
-      hipLaunchKernelGGL((conv_glds_kernel<bm, bn, st, EPI, 4>), grid, dim3(512), 0, s, a);      \
+      hipLaunchKernelGGL((conv_glds_kernel<T, bm, bn, st, EPI, 4>), grid, dim3(512), 0, s, a);      \
     else                                                                                          \
-      hipLaunchKernelGGL((conv_glds_kernel<bm, bn, st, EPI>), grid, dim3(256), 0, s, a);         \
+      hipLaunchKernelGGL((conv_glds_kernel<T, bm, bn, st, EPI>), grid, dim3(256), 0, s, a);         \
     return true;                                                                                  \
   }
   GHOST_G(128, 128, 8) GHOST_G(128, 128, 6)
@@ -795,8 +795,8 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
     static const int aad_glds = GHOST_KNOB("GHOST_CONV_AAD_GLDS", 0);   // AAD epilogue on the 3-stage ring
     if (use_v2 && p.fast && p.BK == 32 && (d.epi != EPI_AAD || p.stages > 0 || aad_glds) && p.BM <= 128 &&
         p.partial == (p.nsplit > 1)) {
-      const bool ok = p.nsplit > 1 ? launch_glds<KEPI_SPLIT>(a, p, s)
-                                   : (d.epi == EPI_AAD ? launch_glds<KEPI_AAD>(a, p, s) : launch_glds<KEPI_STD>(a, p, s));
+      const bool ok = p.nsplit > 1 ? launch_glds<TI, KEPI_SPLIT>(a, p, s)
+                                   : (d.epi == EPI_AAD ? launch_glds<TI, KEPI_AAD>(a, p, s) : launch_glds<TI, KEPI_STD>(a, p, s));
       if (ok) {
         if (p.nsplit > 1) {
           const int ncols = d.epi == EPI_AAD ? d.C_aad : d.N;
@@ -870,6 +870,8 @@ int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream
   if (d.ti == GHOST_F32 && d.to == GHOST_F32) rc = dispatch_types<float, float>(d, a, p, stream);
   else if (d.ti == GHOST_BF16 && d.to == GHOST_BF16) rc = dispatch_types<bf16, bf16>(d, a, p, stream);
   else if (d.ti == GHOST_F32 && d.to == GHOST_BF16) rc = dispatch_types<float, bf16>(d, a, p, stream);
+  else if (d.ti == GHOST_F16 && d.to == GHOST_F16) rc = dispatch_types<_Float16, _Float16>(d, a, p, stream);
+  else if (d.ti == GHOST_F32 && d.to == GHOST_F16) rc = dispatch_types<float, _Float16>(d, a, p, stream);
   else if (d.ti == GHOST_BF16 && d.to == GHOST_F32 && !d.res && !d.y2) rc = dispatch_types<bf16, float>(d, a, p, stream);
   else return -1;
   if (rc) return rc;

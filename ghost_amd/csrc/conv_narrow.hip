@@ -43,9 +43,9 @@ __global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const NarrowArgs a)
   const long img = (long)b * a.H * a.W;
 
   if constexpr (CIN > 0) {
-    // bf16, Cin known: the weight fragments stay in registers and each lane issues the loads of
+    // 16-bit storage, Cin known: the weight fragments stay in registers and each lane issues the loads of
     // two row tiles (2 * CIN/32 x 16 B) before their MFMAs, so the HBM latency overlaps
-    bf16x8 wf0[CIN / 32], wf1[CIN / 32];
+    v8_t<T> wf0[CIN / 32], wf1[CIN / 32];
 #pragma unroll
     for (int k = 0; k < CIN / 32; ++k) {
       const u32x4 b0 = *reinterpret_cast<const u32x4*>(w + (long)lr * a.Kpad + k * 32 + lq * 8);
@@ -72,10 +72,10 @@ __global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const NarrowArgs a)
         f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int k = 0; k < CIN / 32; ++k) {
-          bf16x8 af;
+          v8_t<T> af;
           __builtin_memcpy(&af, &av[u][k], 16);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf0[k], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf1[k], acc1, 0, 0, 0);
+          acc0 = mfma16x16x32<T>(af, wf0[k], acc0);
+          acc1 = mfma16x16x32<T>(af, wf1[k], acc1);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -99,12 +99,12 @@ __global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const NarrowArgs a)
           u32x4 av = ok ? *reinterpret_cast<const u32x4*>(xp + k0 + lq * 8) : u32x4{0u, 0u, 0u, 0u};
           const u32x4 b0 = *reinterpret_cast<const u32x4*>(w + (long)lr * a.Kpad + k0 + lq * 8);
           const u32x4 b1 = *reinterpret_cast<const u32x4*>(w + (long)(16 + lr) * a.Kpad + k0 + lq * 8);
-          bf16x8 af, bf0, bf1;
+          v8_t<T> af, bf0, bf1;
           __builtin_memcpy(&af, &av, 16);
           __builtin_memcpy(&bf0, &b0, 16);
           __builtin_memcpy(&bf1, &b1, 16);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf0, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf1, acc1, 0, 0, 0);
+          acc0 = mfma16x16x32<T>(af, bf0, acc0);
+          acc1 = mfma16x16x32<T>(af, bf1, acc1);
         }
       } else {
         for (int k0 = 0; k0 < a.Cin; k0 += 16) {
@@ -173,16 +173,22 @@ int conv3x3_narrow(int dt, const void* x, int B, int H, int W, int Cin, int ldx,
   if (zadd && (uintptr_t)zadd % 16) return -1;
   NarrowArgs a{x, w_narrow, res, y, u8, (const _Float16*)zadd, H, W, Cin, ldx, Kpad, ldy, ldres, NO, tanh_out};
   dim3 grid((unsigned)(B * (H / TH) * (W / TW)));
-  if (dt == GHOST_BF16 && Cin == 128)
-    hipLaunchKernelGGL((conv3x3_narrow_kernel<bf16, 128>), grid, dim3(256), 0, s, a);
-  else if (dt == GHOST_BF16 && Cin == 64)
-    hipLaunchKernelGGL((conv3x3_narrow_kernel<bf16, 64>), grid, dim3(256), 0, s, a);
-  else if (dt == GHOST_BF16)
-    hipLaunchKernelGGL((conv3x3_narrow_kernel<bf16, 0>), grid, dim3(256), 0, s, a);
-  else if (dt == GHOST_F32)
+#define GHOST_NARROW(T)                                                   \
+  if (Cin == 128)                                                         \
+    hipLaunchKernelGGL((conv3x3_narrow_kernel<T, 128>), grid, dim3(256), 0, s, a); \
+  else if (Cin == 64)                                                     \
+    hipLaunchKernelGGL((conv3x3_narrow_kernel<T, 64>), grid, dim3(256), 0, s, a);  \
+  else                                                                    \
+    hipLaunchKernelGGL((conv3x3_narrow_kernel<T, 0>), grid, dim3(256), 0, s, a);
+  if (dt == GHOST_BF16) {
+    GHOST_NARROW(bf16)
+  } else if (dt == GHOST_F16) {
+    GHOST_NARROW(_Float16)
+  } else if (dt == GHOST_F32)
     hipLaunchKernelGGL((conv3x3_narrow_kernel<float, 0>), grid, dim3(256), 0, s, a);
   else
     return -1;
+#undef GHOST_NARROW
   return (int)hipGetLastError();
 }
 

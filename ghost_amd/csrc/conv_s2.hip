@@ -34,9 +34,9 @@ constexpr int W_BYTES = BN * 256;                 // one K step: 64 rows x 4 tap
 __device__ __attribute__((aligned(16))) unsigned int s2_zero_line[16] = {0};
 
 struct S2Args {
-  const bf16* x;
-  const bf16* w;
-  bf16* y;
+  const void* x;
+  const void* w;
+  void* y;
   const float* scale;
   const float* shift;
   int Hi, Wi, ldx, Ho, Wo, ldy, Kpad, ncb, tiles_x, tiles_per_img;
@@ -48,6 +48,7 @@ GHOST_DEV void s2_wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256) conv4x4s2_patch_kernel(const S2Args a) {
   __shared__ __attribute__((aligned(1024))) unsigned char s_p[P_BYTES];
   __shared__ __attribute__((aligned(1024))) unsigned char s_w[2 * W_BYTES];
@@ -59,7 +60,7 @@ __global__ void __launch_bounds__(256) conv4x4s2_patch_kernel(const S2Args a) {
   const int tyi = t / a.tiles_x, txi = t - tyi * a.tiles_x;
   const int oy0 = tyi * TH, ox0 = txi * TW;
   const int n0 = blockIdx.y * BN;
-  const bf16* __restrict__ xb = a.x + (long)b * a.Hi * a.Wi * a.ldx;
+  const T* __restrict__ xb = reinterpret_cast<const T*>(a.x) + (long)b * a.Hi * a.Wi * a.ldx;
   const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
 
   // patch of channel block cb: slot = (patch row * 2 + column parity) * 17 + column / 2; the 16-byte chunk
@@ -85,7 +86,7 @@ __global__ void __launch_bounds__(256) conv4x4s2_patch_kernel(const S2Args a) {
   auto issue_w = [&](int s, int buf) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const int cb = s >> 2, ky = s & 3;
-    const bf16* wsrc = a.w + (long)n0 * a.Kpad + (cb * 16 + ky * 4) * 32;
+    const T* wsrc = reinterpret_cast<const T*>(a.w) + (long)n0 * a.Kpad + (cb * 16 + ky * 4) * 32;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int i = wid * 4 + k;
@@ -119,20 +120,20 @@ __global__ void __launch_bounds__(256) conv4x4s2_patch_kernel(const S2Args a) {
     const unsigned char* wb = s_w + (s & 1) * W_BYTES;
 #pragma unroll
     for (int tx = 0; tx < 4; ++tx) {
-      bf16x8 wf[4], pf[2];
+      v8_t<T> wf[4], pf[2];
 #pragma unroll
       for (int j = 0; j < 4; ++j)   // row n = 16 j + lr, so n & 15 == lr
-        wf[j] = *reinterpret_cast<const bf16x8*>(wb + (j * 16 + lr) * 256 + (((tx * 4 + lq) ^ lr) << 4));
+        wf[j] = *reinterpret_cast<const v8_t<T>*>(wb + (j * 16 + lr) * 256 + (((tx * 4 + lq) ^ lr) << 4));
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int pr = 2 * (2 * wid + i) + ky;
         const int slot = (pr * 2 + (tx & 1)) * PJ + lr + (tx >> 1);
-        pf[i] = *reinterpret_cast<const bf16x8*>(s_p + slot * 64 + ((lq ^ ((slot >> 2) & 3)) << 4));
+        pf[i] = *reinterpret_cast<const v8_t<T>*>(s_p + slot * 64 + ((lq ^ ((slot >> 2) & 3)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], pf[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32<T>(wf[j], pf[i], acc[i][j]);
     }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();   // every wave is done with this step's weight buffer (and, at ky = 3, the patch)
@@ -143,7 +144,7 @@ __global__ void __launch_bounds__(256) conv4x4s2_patch_kernel(const S2Args a) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int oy = oy0 + 2 * wid + i, ox = ox0 + lr;
-    bf16* yp = a.y + (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldy + n0;
+    T* yp = reinterpret_cast<T*>(a.y) + (((long)b * a.Ho + oy) * a.Wo + ox) * a.ldy + n0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = j * 16 + lq * 4;
@@ -155,7 +156,7 @@ __global__ void __launch_bounds__(256) conv4x4s2_patch_kernel(const S2Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float u = v[r] > 0.f ? v[r] : v[r] * a.slope;
-        const bf16 h = (bf16)u;
+        const T h = (T)u;
         o[r] = __builtin_bit_cast(unsigned short, h);
       }
       uint2 pk = {(unsigned)o[0] | ((unsigned)o[1] << 16), (unsigned)o[2] | ((unsigned)o[3] << 16)};
@@ -168,7 +169,7 @@ __global__ void __launch_bounds__(256) conv4x4s2_patch_kernel(const S2Args a) {
 
 bool conv4x4s2_patch_supported(const ConvDesc& d) {
   if (d.kind != CONV_FWD || d.kh != 4 || d.kw != 4 || d.stride != 2 || d.pad != 1) return false;
-  if (d.ti != GHOST_BF16 || d.to != GHOST_BF16 || d.epi != EPI_STD) return false;
+  if (!is16(d.ti) || d.to != d.ti || d.epi != EPI_STD) return false;
   if (d.res || d.prelu || d.y2 || d.tanh_out || d.u8 || d.in_part || d.force_split) return false;
   if (d.Cin % 32 || d.ldx % 8 || (uintptr_t)d.x % 16 || d.N % BN || d.Npad < d.N || d.Kpad < 16 * d.Cin) return false;
   if (d.Hi % 2 || d.Wi % 2) return false;
@@ -181,7 +182,7 @@ bool conv4x4s2_patch_supported(const ConvDesc& d) {
 int conv4x4s2_patch(const ConvDesc& d, hipStream_t s) {
   if (!conv4x4s2_patch_supported(d)) return -1;
   S2Args a{};
-  a.x = (const bf16*)d.x; a.w = (const bf16*)d.w; a.y = (bf16*)d.y;
+  a.x = d.x; a.w = d.w; a.y = d.y;
   a.scale = d.scale; a.shift = d.shift;
   a.Hi = d.Hi; a.Wi = d.Wi; a.ldx = d.ldx; a.Ho = d.Hi / 2; a.Wo = d.Wi / 2; a.ldy = d.ldy; a.Kpad = d.Kpad;
   a.ncb = d.Cin / 32;
@@ -189,7 +190,10 @@ int conv4x4s2_patch(const ConvDesc& d, hipStream_t s) {
   a.tiles_per_img = (a.Ho / TH) * a.tiles_x;
   a.slope = d.slope;
   dim3 grid((unsigned)(d.B * a.tiles_per_img), (unsigned)(d.N / BN));
-  hipLaunchKernelGGL(conv4x4s2_patch_kernel, grid, dim3(256), 0, s, a);
+  if (d.ti == GHOST_BF16)
+    hipLaunchKernelGGL(conv4x4s2_patch_kernel<bf16>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(conv4x4s2_patch_kernel<_Float16>, grid, dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 

@@ -82,6 +82,46 @@ GHOST_DEV f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_f
 // the two bf16 of a 32-bit word (element 0 in the low half) as fp32
 GHOST_DEV f32x2 bf16x2_f(unsigned w) { return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)}; }
 
+// ---- 16-bit storage types: bf16 (the throughput path) and fp16 (a .half() module, the reference's GPU
+// precision).  Kernels that store activations in 16 bits are templated on the storage type T and use these
+// helpers for everything type-specific: the 8-element MFMA operand, the MFMA itself (both run at the same
+// rate on gfx950), and unpacking the two values of a 32-bit word to fp32.
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+template <typename T> struct V8;
+template <> struct V8<bf16> { typedef bf16x8 t; };
+template <> struct V8<_Float16> { typedef f16x8 t; };
+template <typename T> using v8_t = typename V8<T>::t;
+
+template <typename T> GHOST_DEV f32x4 mfma16x16x32(v8_t<T> a, v8_t<T> b, f32x4 c);
+template <> GHOST_DEV f32x4 mfma16x16x32<bf16>(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <> GHOST_DEV f32x4 mfma16x16x32<_Float16>(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// the two 16-bit values of a 32-bit word (element 0 in the low half) as fp32
+template <typename T> GHOST_DEV f32x2 unpack2(unsigned w);
+template <> GHOST_DEV f32x2 unpack2<bf16>(unsigned w) { return bf16x2_f(w); }
+template <> GHOST_DEV f32x2 unpack2<_Float16>(unsigned w) {
+  typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+  const f16x2 h = __builtin_bit_cast(f16x2, w);
+  return f32x2{(float)h.x, (float)h.y};
+}
+// two fp32 -> one 32-bit word of T (round to nearest even, as (T)v)
+template <typename T> GHOST_DEV unsigned pack2(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) T t2;
+  const t2 v = {(T)a, (T)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+
+// ghost dtype enum of a storage type
+template <typename T> constexpr int gdt();
+template <> constexpr int gdt<float>() { return GHOST_F32; }
+template <> constexpr int gdt<bf16>() { return GHOST_BF16; }
+template <> constexpr int gdt<_Float16>() { return GHOST_F16; }
+inline bool is16(int dt) { return dt == GHOST_BF16 || dt == GHOST_F16; }
+
 // workgroup id -> work index such that each XCD (the hardware deals workgroups round-robin over the
 // 8 XCDs) gets one contiguous run of work indices, so neighbours that share input lines hit the same
 // L2 (cdna_hip_programming.md T1, bijective form)

@@ -128,7 +128,7 @@ in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, flo
   const int b = blockIdx.z, cg = blockIdx.y, ch = blockIdx.x;
   const int t = threadIdx.x, cc = t & 7, q = t >> 3;
   constexpr int VEC = Vec16<T>::N;
-  static_assert(VEC == 8, "bf16 source");
+  static_assert(VEC == 8, "16-bit source");
   const int CPB = u.W < 128 ? u.W : 128, RB = 512 / CPB, nxb = u.W / CPB;
   const int sy = (ch / nxb) * RB + q % RB, sx0 = (ch % nxb) * CPB + (q / RB) * 16;
   const T* xb = x + (long)b * u.H * u.W * ldx + cg * 64 + cc * 8;
@@ -166,8 +166,8 @@ in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, flo
     for (int j = 0; j < NB; ++j) {
       const int sx = sx0 + k0 + j;
       const float wx = wxt[sx], g0x = wxt[ld + sx], g1x = wxt[2 * ld + sx], g1x2 = 2.f * g1x;
-      const bf16* e0 = reinterpret_cast<const bf16*>(&nr0[j]);
-      const bf16* e1 = reinterpret_cast<const bf16*>(&nr1[j]);
+      const T* e0 = reinterpret_cast<const T*>(&nr0[j]);
+      const T* e1 = reinterpret_cast<const T*>(&nr1[j]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float vr = (float)e0[e] - K[e], vdr = (float)e1[e] - K[e];
@@ -289,7 +289,7 @@ size_t in_stats_workspace_bytes(int B, int HW, int C) {
 }
 
 bool in_stats_up2x_closed_form(int dt, int H, int W, int C, int ldx) {
-  if (dt != GHOST_BF16 || W % 16 || C % 64 || ldx % 8 || H > 4096 || W > 4096) return false;
+  if (!is16(dt) || W % 16 || C % 64 || ldx % 8 || H > 4096 || W > 4096) return false;
   const int cpb = W < 128 ? W : 128;   // source columns per workgroup; 512 / cpb rows
   return W % cpb == 0 && H % (512 / cpb) == 0;
 }
@@ -303,7 +303,7 @@ static void in_stats_launch(const T* x, int ldx, int B, int HW, int C, float* st
   dim3 g2((B * C + 255) / 256);
   const Up2xSrc u = up ? *up : Up2xSrc{0, 0, 0.f, 0.f};
   if constexpr (sizeof(T) == 2) {
-    if (up && in_stats_up2x_closed_form(GHOST_BF16, u.H, u.W, C, ldx)) {
+    if (up && in_stats_up2x_closed_form(gdt<T>(), u.H, u.W, C, ldx)) {
       // closed form over the source: (H / 4) * (W / 128) records <= the HW / 512 reserved
       const int nr = u.H * u.W / 512;   // workgroups of 512 source pixels
       const int ld = u.H > u.W ? u.H : u.W;
@@ -333,6 +333,8 @@ static int in_stats_any(int dt, const void* x, int ldx, int B, int HW, int C, fl
     in_stats_launch((const float*)x, ldx, B, HW, C, stat, part, up, s);
   else if (dt == GHOST_BF16)
     in_stats_launch((const bf16*)x, ldx, B, HW, C, stat, part, up, s);
+  else if (dt == GHOST_F16)
+    in_stats_launch((const _Float16*)x, ldx, B, HW, C, stat, part, up, s);
   else
     return -1;
   return (int)hipGetLastError();
@@ -412,14 +414,14 @@ aad_mask_kernel(const T* __restrict__ h, int ldh, int HW, int C, int G, int ppb,
   }
 }
 
-// bf16 form with the per-channel tables in registers: lane gl of a G-lane pixel group always owns
+// 16-bit form with the per-channel tables in registers: lane gl of a G-lane pixel group always owns
 // channels 8 (gl + G j), j < NCH, so its (wh * rstd) factors stay in VGPRs and the logit is one FMA
 // per channel: sum_c (wh_c rstd_c) h_c - K with K = sum_c wh_c rstd_c mu_c per sample (as aad_v3).
 // Measured against the LDS-table kernel above: the per-element LDS reads made it VALU/LDS-bound
 // at 2-2.6 TB/s of h_in.
-template <int L, int NCH>
+template <typename T, int L, int NCH>
 __global__ void __launch_bounds__(256)
-aad_mask_reg_kernel(const bf16* __restrict__ h, int ldh, int HW, int C, int G, int ppb, const float* __restrict__ stat,
+aad_mask_reg_kernel(const T* __restrict__ h, int ldh, int HW, int C, int G, int ppb, const float* __restrict__ stat,
                     const float* __restrict__ wh0, const float* __restrict__ bh0, float* __restrict__ mask0,
                     const float* __restrict__ wh1, const float* __restrict__ bh1, float* __restrict__ mask1) {
   const int t = threadIdx.x, b = blockIdx.y;
@@ -464,7 +466,7 @@ aad_mask_reg_kernel(const bf16* __restrict__ h, int ldh, int HW, int C, int G, i
       for (int l = 0; l < L; ++l) sl[l] = 0.f;
 #pragma unroll
       for (int j = 0; j < NCH; ++j) {
-        const bf16* e8 = reinterpret_cast<const bf16*>(&raw[u][j]);
+        const T* e8 = reinterpret_cast<const T*>(&raw[u][j]);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
 #pragma unroll
@@ -494,13 +496,18 @@ int aad_mask2(int dt, const void* h, int ldh, int B, int HW, int C, const float*
   dim3 grid((unsigned)((HW + ppb - 1) / ppb), (unsigned)B);
   const int L = wh1 ? 2 : 1;
   static const int use_reg = GHOST_KNOB("GHOST_MASK_REG", 1);
-  if (use_reg && dt == GHOST_BF16 && (C == 8 * G || C == 16 * G)) {
+  if (use_reg && is16(dt) && (C == 8 * G || C == 16 * G)) {
     const int nch = C / (8 * G);
-#define GHOST_MR(l, n)                                                                                              \
-  hipLaunchKernelGGL((aad_mask_reg_kernel<l, n>), grid, dim3(256), 0, s, (const bf16*)h, ldh, HW, C, G, ppb, stat, \
+#define GHOST_MR(T, l, n)                                                                                        \
+  hipLaunchKernelGGL((aad_mask_reg_kernel<T, l, n>), grid, dim3(256), 0, s, (const T*)h, ldh, HW, C, G, ppb, stat, \
                      wh0, bh0, mask0, wh1, bh1, mask1)
-    if (L == 2) { if (nch == 1) GHOST_MR(2, 1); else GHOST_MR(2, 2); }
-    else { if (nch == 1) GHOST_MR(1, 1); else GHOST_MR(1, 2); }
+    if (dt == GHOST_BF16) {
+      if (L == 2) { if (nch == 1) GHOST_MR(bf16, 2, 1); else GHOST_MR(bf16, 2, 2); }
+      else { if (nch == 1) GHOST_MR(bf16, 1, 1); else GHOST_MR(bf16, 1, 2); }
+    } else {
+      if (L == 2) { if (nch == 1) GHOST_MR(_Float16, 2, 1); else GHOST_MR(_Float16, 2, 2); }
+      else { if (nch == 1) GHOST_MR(_Float16, 1, 1); else GHOST_MR(_Float16, 1, 2); }
+    }
 #undef GHOST_MR
     return (int)hipGetLastError();
   }
@@ -512,6 +519,8 @@ int aad_mask2(int dt, const void* h, int ldh, int B, int HW, int C, const float*
     if (L == 2) GHOST_M(float, 2); else GHOST_M(float, 1);
   } else if (dt == GHOST_BF16) {
     if (L == 2) GHOST_M(bf16, 2); else GHOST_M(bf16, 1);
+  } else if (dt == GHOST_F16) {
+    if (L == 2) GHOST_M(_Float16, 2); else GHOST_M(_Float16, 1);
   } else {
     return -1;
   }
@@ -622,6 +631,9 @@ int stats_mask_small(int dt, const void* x, int ldx, int B, int HW, int C, float
   else if (dt == GHOST_BF16)
     hipLaunchKernelGGL(stats_mask_small_kernel<bf16>, dim3(B), dim3(256), 0, s, (const bf16*)x, ldx, HW, C, stat,
                        wh0, bh0, mask0, wh1, bh1, mask1);
+  else if (dt == GHOST_F16)
+    hipLaunchKernelGGL(stats_mask_small_kernel<_Float16>, dim3(B), dim3(256), 0, s, (const _Float16*)x, ldx, HW, C,
+                       stat, wh0, bh0, mask0, wh1, bh1, mask1);
   else
     return -1;
   return (int)hipGetLastError();
@@ -700,25 +712,32 @@ int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, i
   int lg = -1;
   if ((nch & (nch - 1)) == 0) for (lg = 0; (1 << lg) < nch; ++lg) {}
   static const int rows = GHOST_KNOB("GHOST_UP_ROWS", 2);
-  if (dt == GHOST_BF16 && lg >= 0 && (rows == 2 || rows == 4) && (2 * H) % rows == 0 &&
+  if (is16(dt) && lg >= 0 && (rows == 2 || rows == 4) && (2 * H) % rows == 0 &&
       (long)H * W * ldx < (1L << 31)) {
     grid.y = (unsigned)(B * 2 * H / rows);
     // outputs of >= 64 MB (the encoder's z_attr8: 537 MB at B = 64, read again only by AADBlk8, long after it
     // has left L2 and the Infinity Cache) are written with non-temporal stores
     static const int nt_knob = GHOST_KNOB("GHOST_UP_NT", 1);
     const bool nt = nt_knob && (long)B * 4 * H * W * C * 2 >= (64L << 20);
-    if (rows == 4)
-      hipLaunchKernelGGL((upsample2x_rows_kernel<bf16, 4>), grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, u, lg);
-    else if (nt)
-      hipLaunchKernelGGL((upsample2x_rows_kernel<bf16, 2, true>), grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, u, lg);
-    else
-      hipLaunchKernelGGL((upsample2x_rows_kernel<bf16, 2>), grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, u, lg);
+#define GHOST_UPR(T)                                                                                               \
+    if (rows == 4)                                                                                                 \
+      hipLaunchKernelGGL((upsample2x_rows_kernel<T, 4>), grid, dim3(256), 0, s, (const T*)x, ldx, (T*)y, ldy, u, lg); \
+    else if (nt)                                                                                                   \
+      hipLaunchKernelGGL((upsample2x_rows_kernel<T, 2, true>), grid, dim3(256), 0, s, (const T*)x, ldx, (T*)y, ldy, u, \
+                         lg);                                                                                      \
+    else                                                                                                           \
+      hipLaunchKernelGGL((upsample2x_rows_kernel<T, 2>), grid, dim3(256), 0, s, (const T*)x, ldx, (T*)y, ldy, u, lg);
+    if (dt == GHOST_BF16) { GHOST_UPR(bf16) } else { GHOST_UPR(_Float16) }
+#undef GHOST_UPR
     return (int)hipGetLastError();
   }
   if (dt == GHOST_F32)
     hipLaunchKernelGGL(upsample2x_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, (float*)y, ldy, u, C, lg);
   else if (dt == GHOST_BF16)
     hipLaunchKernelGGL(upsample2x_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, (bf16*)y, ldy, u, C, lg);
+  else if (dt == GHOST_F16)
+    hipLaunchKernelGGL(upsample2x_kernel<_Float16>, grid, dim3(256), 0, s, (const _Float16*)x, ldx, (_Float16*)y, ldy, u,
+                       C, lg);
   else
     return -1;
   return (int)hipGetLastError();
@@ -753,6 +772,9 @@ static int input_dispatch(const TX* x, const int64_t* st, int B, int C, int H, i
   else if (dt == GHOST_BF16)
     hipLaunchKernelGGL((input_to_nhwc_kernel<TX, bf16>), grid, dim3(256), 0, s, x, (long)st[0], (long)st[1],
                        (long)st[2], (long)st[3], B, C, H, W, ldy, (bf16*)y);
+  else if (dt == GHOST_F16)
+    hipLaunchKernelGGL((input_to_nhwc_kernel<TX, _Float16>), grid, dim3(256), 0, s, x, (long)st[0], (long)st[1],
+                       (long)st[2], (long)st[3], B, C, H, W, ldy, (_Float16*)y);
   else
     return -1;
   return (int)hipGetLastError();
@@ -826,6 +848,8 @@ int y_to_u8_bgr(int dt, const void* y, int ldy, int B, int H, int W, uint8_t* ou
     hipLaunchKernelGGL(y_u8_kernel<float>, grid, dim3(256), 0, s, (const float*)y, ldy, P, out);
   else if (dt == GHOST_BF16)
     hipLaunchKernelGGL(y_u8_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)y, ldy, P, out);
+  else if (dt == GHOST_F16)
+    hipLaunchKernelGGL(y_u8_kernel<_Float16>, grid, dim3(256), 0, s, (const _Float16*)y, ldy, P, out);
   else
     return -1;
   return (int)hipGetLastError();
@@ -871,6 +895,9 @@ int nhwc_to_nchw(int dt, const void* x, int ldx, int B, int H, int W, int C, voi
     hipLaunchKernelGGL(nhwc_nchw_kernel<float>, grid, dim3(256), 0, s, (const float*)x, ldx, B, H, W, C, (float*)y);
   else if (dt == GHOST_BF16)
     hipLaunchKernelGGL(nhwc_nchw_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)x, ldx, B, H, W, C, (bf16*)y);
+  else if (dt == GHOST_F16)
+    hipLaunchKernelGGL(nhwc_nchw_kernel<_Float16>, grid, dim3(256), 0, s, (const _Float16*)x, ldx, B, H, W, C,
+                       (_Float16*)y);
   else
     return -1;
   return (int)hipGetLastError();

@@ -16,9 +16,10 @@ values as the reference, no copy.
 Numerics: fp32 parameters run the fp32 path (exact-fp32 MFMA, |dY| <= 1e-3 vs the
 reference CPU forward).  ``.bfloat16()`` parameters (or ``compute_dtype=torch.bfloat16``)
 run the bf16 throughput path (bf16 storage, fp32 accumulation) and return bf16 tensors.
-``.half()`` parameters (inference.py:30) run the same bf16 kernels and return float16
-tensors, as the reference's fp16 module does: the dtype callers see is the reference's,
-the storage precision is bf16 (DESIGN.md §2 quotes both errors).  There is no CPU path.
+``.half()`` parameters (inference.py:30; or ``compute_dtype=torch.float16``) run the same
+kernels instantiated for fp16 storage (v_mfma_f32_16x16x32_f16, fp32 accumulation) and
+return float16 tensors: the reference's own GPU precision, ~4x more accurate end to end than
+bf16 storage.  There is no CPU path.
 """
 from __future__ import annotations
 
@@ -197,14 +198,16 @@ class AEI_Net(PackedModule):
 
     # -- weights -------------------------------------------------------------------
     def _dtype(self) -> torch.dtype:
+        """Storage dtype of the plan: compute_dtype if given, else the parameters' (fp32, bf16 or fp16)."""
         if self.compute_dtype is not None:
+            if self.compute_dtype not in (torch.float32, torch.bfloat16, torch.float16):
+                raise TypeError(f"ghost_amd: unsupported compute_dtype {self.compute_dtype}")
             return self.compute_dtype
-        return torch.float32 if self.generator.up1.weight.dtype == torch.float32 else torch.bfloat16
+        dt = self.generator.up1.weight.dtype
+        return dt if dt in (torch.float32, torch.float16) else torch.bfloat16
 
     def _out_dtype(self, rt) -> torch.dtype:
-        """float16 for a .half() module (the reference's output dtype), else the compute dtype."""
-        if self.compute_dtype is None and self.generator.up1.weight.dtype == torch.float16:
-            return torch.float16
+        """The dtype of the returned tensors: the plan's storage dtype."""
         return rt.dtype
 
     def set_option(self, name: str, value: int) -> None:

@@ -12,7 +12,7 @@ Layouts (Npad = Cout rounded up to 128, Kpad = K rounded up to 32, zero padded):
                                  kernel tap ky = ((1,3),(0,2))[py][ty]  (sub-pixel decomposition)
   AAD conv1/conv2 (1x1)       -> [Npad][Kpad] rows interleaved per 16 channels: gamma c0..15,
                                  beta c0..15, gamma c16..31, ...  (+ the same for the biases)
-                                 and, bf16 with C in {64,128}: [C/64*128][Ca] rows permuted for the
+                                 and, 16-bit (bf16 / fp16) with C in {64,128}: [C/64*128][Ca] rows permuted for the
                                  register-epilogue kernel (pack_aad_v3)
   all fc1/fc2 (Linear)        -> one fp32 [Npad][Kpad] = [gamma_l | beta_l] per AADLayer l in plan order
   up1 ConvT k2 on 1x1         -> fp32 [4096][Kpad], n = (y*2+x)*1024 + co
@@ -209,7 +209,7 @@ def pack_all(sd: Dict[str, torch.Tensor], backbone: str, num_blocks: int, c_id: 
     for slot, pre in aad_plan(backbone, num_blocks):
         for k, v in pack_aad(sd, pre, dtype).items():
             slots[f"{slot}.{k}"] = v
-        if dtype == torch.bfloat16 and v3_layout(*sd[f"{pre}.conv1.weight"].shape[:2]):
+        if dtype in (torch.bfloat16, torch.float16) and v3_layout(*sd[f"{pre}.conv1.weight"].shape[:2]):
             for k, v in pack_aad_v3(sd, pre, dtype).items():
                 slots[f"{slot}.{k}"] = v
         ids_w += [sd[f"{pre}.fc1.weight"].float(), sd[f"{pre}.fc2.weight"].float()]

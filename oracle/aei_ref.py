@@ -449,7 +449,7 @@ def gen_block_bf16_storage(y_prev, za, z_id, p, backbone, num_blocks, k):
     pre = f"generator.AADBlk{k}"
     x, st = m, m_stats
     zp = _TAP_PARTIALS[0] if (k == 8 and cin != cout and cin == 64 and cout == 3
-                              and _STORE[0] == torch.bfloat16) else 0
+                              and _STORE[0] in (torch.bfloat16, torch.float16)) else 0
     for i in range(num_blocks):
         a = aad_layer_bf16_storage(x, za, z_id, p, f"{pre}.add_blocks.{3 * i}", st)
         wc = _wq(p, f"{pre}.add_blocks.{3 * i + 2}.weight")
@@ -494,6 +494,29 @@ def aei_forward_bf16_storage(p, xt, z_id, backbone="unet", num_blocks=2, store=t
     finally:
         _STORE[0] = prev
         _TAP_PARTIALS[0] = prev_tp
+
+
+def aei_forward_fp16_storage(p, xt, z_id, backbone="unet", num_blocks=2, tap_partials=2):
+    """The fp16-storage runtime (a .half() module, inference.py:30): the same emulation with every stored
+    tensor rounded to float16 instead of bfloat16 (fp32 arithmetic in between, as the kernels)."""
+    return aei_forward_bf16_storage(p, xt, z_id, backbone, num_blocks, store=torch.float16, tap_partials=tap_partials)
+
+
+class storage:
+    """``with aei_ref.storage(torch.float16, tap_partials=2):`` — the per-stage emulation functions
+    (gen_block_bf16_storage, aad_layer_bf16_storage, up1_bf16_storage ...) round to this dtype inside."""
+
+    def __init__(self, dtype, tap_partials=2):
+        self.dtype, self.tp = dtype, tap_partials
+
+    def __enter__(self):
+        self.prev = (_STORE[0], _TAP_PARTIALS[0])
+        _STORE[0], _TAP_PARTIALS[0] = self.dtype, self.tp
+        return self
+
+    def __exit__(self, *exc):
+        _STORE[0], _TAP_PARTIALS[0] = self.prev
+        return False
 
 
 def fp16_reference_forward(p, xt, z_id, backbone="unet", num_blocks=2):

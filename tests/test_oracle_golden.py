@@ -103,3 +103,20 @@ def test_bf16_storage_emulation_rounds(name):
         assert torch.equal(a, a.to(torch.bfloat16).float())
     d = (y - torch.from_numpy(g["Y"])).abs()
     assert 1e-3 < float(d.mean()) < 0.03
+
+
+@pytest.mark.parametrize("name", ["aei_unet2_b2", "aei_linknet3_b2"])
+def test_fp16_storage_emulation_rounds_and_is_closer(name):
+    """The fp16-storage emulation (a .half() module): every stored tensor fp16-representable, and Y
+    several times closer to the reference fp32 forward (the fixture, a reference run) than bf16 storage."""
+    g = _load(name)
+    backbone, nb, B = str(g["backbone"]), int(g["num_blocks"]), int(g["batch"])
+    p = aei_ref.make_weights(aei_ref.param_specs(backbone, nb))
+    xt, z = aei_ref.make_inputs(B, int(g["seed"]))
+    y16, attr, blocks, _t = aei_ref.aei_forward_fp16_storage(p, xt, z, backbone, nb)
+    for a in list(attr) + blocks[:7] + [y16]:
+        assert torch.equal(a, a.to(torch.float16).float())
+    yb = aei_ref.aei_forward_bf16_storage(p, xt, z, backbone, nb)[0]
+    ref = torch.from_numpy(g["Y"])
+    e16, eb = float((y16 - ref).abs().mean()), float((yb - ref).abs().mean())
+    assert torch.isfinite(y16).all() and e16 * 2.5 < eb, (e16, eb)
