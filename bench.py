@@ -301,8 +301,8 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
       2. paste-back (get_final_video, video_processing.py:207-241): the full 1080p frames H2D in chunks,
          warp + mask composite on the device (blend.blend_swaps) from the device-resident swaps, D2H of
          the blended frames; copies on their own streams overlap the previous chunk's blend.
-    The reference's cv2.resize 256 -> 224 of the swap is folded into the warp (transform scaled by
-    256/224, the mask made at 256); landmarks / mask construction / the video writer stay on the host."""
+    The swap is resized 256 -> 224 as the reference does (cv2.resize INTER_LINEAR, on the device) before
+    the warp; landmarks / mask construction / the video writer stay on the host."""
     from ghost_amd.inference.blend import blend_swaps
     from ghost_amd.inference.core import swap_identity_frames
     rng = np.random.Generator(np.random.PCG64(9))
@@ -313,7 +313,7 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
     frames_h = torch.empty(n_frames, H, W, 3, dtype=torch.uint8, pin_memory=True)
     for i in range(0, n_frames, 16):
         frames_h[i:i + 16] = tile[:min(16, n_frames - i)]
-    # crop <- frame affine maps (a face of ~300 px somewhere in the frame), scaled by 256/224
+    # crop <- frame affine maps (a 224-px crop of a ~300 px face somewhere in the frame)
     ang = rng.uniform(-0.3, 0.3, n_frames)
     sc = rng.uniform(0.7, 0.9, n_frames)
     tx, ty = rng.uniform(600, 1300, n_frames), rng.uniform(200, 700, n_frames)
@@ -322,10 +322,9 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
     mats[:, 1, 0], mats[:, 1, 1] = sc * np.sin(ang), sc * np.cos(ang)
     mats[:, 0, 2] = -(mats[:, 0, 0] * tx + mats[:, 0, 1] * ty)
     mats[:, 1, 2] = -(mats[:, 1, 0] * tx + mats[:, 1, 1] * ty)
-    mats *= 256.0 / 224.0
-    yy, xx = np.mgrid[0:256, 0:256]
-    mask = np.clip(1.0 - (((yy - 128) / 110.0) ** 2 + ((xx - 128) / 95.0) ** 2), 0, 1).astype(np.float32)
-    masks_d = torch.from_numpy(np.broadcast_to(mask, (n_frames, 256, 256)).copy()).to(dev)
+    yy, xx = np.mgrid[0:224, 0:224]
+    mask = np.clip(1.0 - (((yy - 112) / 96.0) ** 2 + ((xx - 112) / 83.0) ** 2), 0, 1).astype(np.float32)
+    masks_d = torch.from_numpy(np.broadcast_to(mask, (n_frames, 224, 224)).copy()).to(dev)
     mats_d = torch.from_numpy(mats).to(dev)
     valid_d = torch.from_numpy(present.astype(np.int32)).to(dev)
     z = identity_rows(1, dev)
@@ -350,7 +349,7 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
                 loaded = torch.cuda.Event()
                 loaded.record(s_in)
             cur.wait_event(loaded)
-            blend_swaps(b[:f1 - f0], swaps_f[f0:f1], masks_d[f0:f1], mats_d[f0:f1], valid_d[f0:f1])
+            blend_swaps(b[:f1 - f0], swaps_f[f0:f1], masks_d[f0:f1], mats_d[f0:f1], valid_d[f0:f1], resize_to=224)
             blended = torch.cuda.Event()
             blended.record(cur)
             with torch.cuda.stream(s_out):
@@ -371,7 +370,8 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
     assert len(final) == n_frames and sum(1 for f in final if len(f)) == n_face
     return {"workload": f"config 3: {n_frames}-frame {W}x{H} video, 1 identity, {n_face} frames with a face; "
                         f"crops H2D -> swaps (BS={BS}, per-batch D2H) -> present re-insertion -> frames H2D -> "
-                        "device paste-back -> frames D2H (host detect/align/landmarks/mask/writer excluded)",
+                        "device resize 256->224 + paste-back -> frames D2H (host detect/align/landmarks/mask/writer "
+                        "excluded)",
             "frames_per_s": round(n_frames / el, 1), "seconds": round(el, 3),
             "host_bytes_moved": int(n_face * 196608 * 2 + 2 * n_frames * H * W * 3)}
 

@@ -237,6 +237,19 @@ int ghost_arc_match(const float* face_emb, int F, const float* target_emb, int T
 int ghost_blend_swaps_u8(uint8_t* frames, int64_t frame_stride, int F, int H, int W, const uint8_t* swaps,
                          int64_t swap_stride, int Hs, int Ws, const float* masks, int64_t mask_stride,
                          const float* mats, const int32_t* valid, void* stream);
+/* cv2.resize(src, (Wd, Hd)) INTER_LINEAR for F uint8 [Hs,Ws,3] images (OpenCV's fixed point): the
+ * resize of the 256x256 swap to the 224x224 crop size that precedes the warp (video_processing.py:212,
+ * image_processing.py:63). */
+int ghost_resize_u8_linear(const uint8_t* src, int64_t src_stride, int F, int Hs, int Ws, uint8_t* dst,
+                           int64_t dst_stride, int Hd, int Wd, void* stream);
+/* get_final_image (utils/inference/image_processing.py:51-76) for one full frame [H,W,3] u8, in place: for
+ * each identity j in order, swap_t = cv2.warpAffine(swaps[j] (S x S, already resized), invertAffineTransform
+ * (tfm_j), BORDER_REPLICATE), mask_t = the same warp of masks[j] with the constant 0 border, final =
+ * mask_t*swap_t + (1-mask_t)*final in float32; one uint8 cast at the end.  maps[j] = the [2][3] double
+ * matrix warpAffine samples with (the inverse of invertAffineTransform(tfm_j), computed on the host as
+ * OpenCV does: ghost_amd.inference.blend.cv_warp_map). */
+int ghost_blend_image_u8(uint8_t* frame, int H, int W, const uint8_t* swaps, int64_t swap_stride, int J, int S,
+                         const float* masks, int64_t mask_stride, const double* maps, void* stream);
 
 #ifdef __cplusplus
 }

@@ -68,3 +68,78 @@ def test_blend_kernel_matches_oracle_multi_frame_multi_identity():
     got = fr.cpu().numpy()
     d = np.abs(got.astype(np.int16) - frames.astype(np.int16))
     assert d.max() <= 1 and (d > 0).mean() < 5e-3, (d.max(), (d > 0).mean())
+
+
+def test_cv_resize_restatement_is_bilinear_cpu():
+    """oracle resize_linear_u8 (cv2 INTER_LINEAR fixed point, 256 -> 224) against float bilinear with half-pixel
+    centres (torch, align_corners=False): the same sampling, within the fixed-point rounding (< 1 LSB)."""
+    import torch.nn.functional as F
+    img = np.random.default_rng(3).integers(0, 256, (256, 256, 3), dtype=np.uint8)
+    got = R.resize_linear_u8(img, (224, 224)).astype(np.float32)
+    ref = F.interpolate(torch.from_numpy(img).permute(2, 0, 1)[None].float(), size=(224, 224), mode="bilinear",
+                        align_corners=False)[0].permute(1, 2, 0).numpy()
+    assert np.abs(got - ref).max() <= 1.0
+
+
+def test_cv_warp_restatement_identity_and_replicate_cpu():
+    """warp_affine_cv with an identity transform reproduces the image; BORDER_REPLICATE extends the edge
+    pixels outward while the constant border leaves the float mask 0 outside."""
+    img = np.random.default_rng(4).integers(0, 256, (224, 224, 3), dtype=np.uint8)
+    eye = np.array([[1.0, 0.0, 0.0], [0.0, 1.0, 0.0]])
+    assert np.array_equal(R.warp_affine_cv(img, eye, (224, 224), "replicate"), img)
+    shift = np.array([[1.0, 0.0, 10.0], [0.0, 1.0, 0.0]])          # content moves right by 10 px
+    out = R.warp_affine_cv(img, shift, (224, 224), "replicate")
+    assert np.array_equal(out[:, :10], np.repeat(img[:, :1], 10, axis=1)) and np.array_equal(out[:, 10:], img[:, :-10])
+    m = R.warp_affine_cv(np.ones((224, 224), np.float32), shift, (224, 224), "constant")
+    assert (m[:, :9] == 0).all() and (m[:, 10:] == 1).all()
+
+
+def _image_case(seed, J=2, H=270, W=480):
+    cs = [R.make_case(seed * 10 + j, H, W) for j in range(J)]
+    g = np.random.default_rng(seed)
+    swaps256 = g.integers(0, 256, (J, 256, 256, 3), dtype=np.uint8)
+    return cs[0][0], swaps256, np.stack([c[2] for c in cs]), [c[3].astype(np.float64) for c in cs]
+
+
+@pytest.mark.gpu
+def test_resize_kernel_bit_exact_vs_cv_restatement():
+    from ghost_amd.inference.blend import resize_u8
+    g = np.random.default_rng(7)
+    src = g.integers(0, 256, (5, 256, 256, 3), dtype=np.uint8)
+    got = resize_u8(torch.from_numpy(src).to("cuda:0"), (224, 224)).cpu().numpy()
+    for f in range(5):
+        assert np.array_equal(got[f], R.resize_linear_u8(src[f], (224, 224))), f
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+def test_blend_image_matches_get_final_image(seed):
+    """get_final_image (image_processing.py:51-76): two identities, BORDER_REPLICATE swap warp, constant-0
+    mask warp, float32 accumulation, one uint8 cast — within 1 LSB of the restatement."""
+    from ghost_amd.inference.blend import blend_image
+    frame, swaps256, masks, tfms = _image_case(seed)
+    ref = R.get_final_image(list(swaps256), frame, tfms, list(masks))
+    fr = torch.from_numpy(frame.copy()).to("cuda:0")
+    got = blend_image(fr, torch.from_numpy(swaps256), torch.from_numpy(masks), tfms).cpu().numpy()
+    d = np.abs(got.astype(np.int16) - ref.astype(np.int16))
+    assert d.max() <= 1 and (d > 0).mean() < 1e-3, (d.max(), (d > 0).mean())
+
+
+@pytest.mark.gpu
+def test_blend_video_resize_then_warp_matches_reference_order():
+    """video_processing.py:212-227: the 256x256 swap is resized to 224 (cv2) before the kornia warp; the
+    device path (blend_swaps(resize_to=224)) against paste_back_video, within 1 LSB."""
+    from ghost_amd.inference.blend import blend_swaps
+    cases = [R.make_case(s) for s in range(20, 24)]
+    g = np.random.default_rng(9)
+    swaps256 = g.integers(0, 256, (4, 256, 256, 3), dtype=np.uint8)
+    frames = np.stack([c[0] for c in cases])
+    masks = np.stack([c[2] for c in cases])
+    mats = np.stack([c[3] for c in cases])
+    fr = torch.from_numpy(frames.copy()).to("cuda:0")
+    blend_swaps(fr, torch.from_numpy(swaps256), torch.from_numpy(masks), mats, resize_to=224)
+    got = fr.cpu().numpy()
+    for f in range(4):
+        ref = R.paste_back_video(frames[f], swaps256[f], masks[f], mats[f])
+        d = np.abs(got[f].astype(np.int16) - ref.astype(np.int16))
+        assert d.max() <= 1 and (d > 0).mean() < 5e-3, (f, d.max(), (d > 0).mean())
