@@ -57,6 +57,7 @@ _SIGS = {
     "ghost_arc_workspace_bytes": (i64, [vp, i32]),
     "ghost_arc_forward": (i32, [vp, vp, i32, i64p, i32, vp, vp, i64, vp]),
     "ghost_arc_embed_u8": (i32, [vp, vp, i64, i32, i32, i32, vp, vp, i64, vp]),
+    "ghost_arc_set_taps": (i32, [vp, C.POINTER(vp), i32]),
     "ghost_arc_match": (i32, [vp, i32, vp, i32, i32, f32, vp, vp, vp, vp]),
     "ghost_blend_swaps_u8": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, i32, vp, i64, vp, vp, vp]),
     "ghost_resize_u8_linear": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, i32, vp]),

@@ -170,6 +170,28 @@ class IResNet(PackedModule):
         return emb
 
     @torch.no_grad()
+    def forward_taps(self, x):
+        """forward + every stage's stored tensors (parity bisection against the storage-emulating oracle):
+        a list over stages (0 = stem, i = IBasicBlock i) of (X_i, BN(X_i)) as NCHW views in the compute
+        dtype — X_i the residual stream, BN(X_i) the next BatchNorm's output the next conv reads."""
+        _lib.require_gpu(x, "IResNet.forward_taps")
+        rt = self._runtime(x.device)
+        N, dev = x.shape[0], x.device
+        shapes = [(112, 64)]
+        for planes, n in zip((64, 128, 256, 512), self.layers_cfg):
+            for b in range(n):
+                shapes.append((shapes[-1][0] // (2 if b == 0 else 1), planes))
+        bufs = [(torch.empty(N, h, h, c, dtype=rt.dtype, device=dev), torch.empty(N, h, h, c, dtype=rt.dtype, device=dev))
+                for h, c in shapes]
+        ptrs = (C.c_void_p * (2 * len(bufs)))(*[t.data_ptr() for pair in bufs for t in pair])
+        _lib.check(rt.lib.ghost_arc_set_taps(rt.h, ptrs, 2 * len(bufs)), "arc taps")
+        try:
+            emb = self.forward(x)
+        finally:
+            rt.lib.ghost_arc_set_taps(rt.h, None, 0)
+        return emb, [(a.permute(0, 3, 1, 2), b.permute(0, 3, 1, 2)) for a, b in bufs]
+
+    @torch.no_grad()
     def embed_u8(self, crops: torch.Tensor) -> torch.Tensor:
         """Fused netArc(F.interpolate(normalize_and_torch_batch(crops), 0.5, bilinear, align_corners=True))
         on device uint8 crops [N,224,224,3] (video_processing.py:136-139, core.py:43-44)."""

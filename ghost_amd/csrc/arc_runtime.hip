@@ -38,6 +38,9 @@ struct ghost_arc {
   int nf = 512;
   int dt = GHOST_F32, esz = 4;
   std::map<std::string, const void*> slots;
+  // diagnostic taps (ghost_arc_set_taps): stage i (0 = stem, i = block i) copies its stored residual
+  // stream X into taps[2i] and the next BatchNorm's second output XB into taps[2i+1] when non-null
+  std::vector<void*> taps;
 };
 
 namespace {
@@ -141,8 +144,17 @@ void arc_plan(ArcCtx& c, const void* xin, int N, float* emb) {
   auto next_bn = [&](size_t i) {   // BN applied to the output of block i-1 (i = index of the consumer)
     return i < blks.size() ? blk_name(blks[i].first, blks[i].second) + ".bn1" : std::string("head.bn2");
   };
+  // per-stage tap copies (parity bisection: the oracle recomputes each stage from the GPU's own inputs)
+  auto tap = [&](size_t stage, const void* x, const void* xb, size_t bytes) {
+    if (c.dry || !c.ok() || 2 * stage + 1 >= h->taps.size()) return;
+    if (h->taps[2 * stage])
+      c.check((int)hipMemcpyAsync(h->taps[2 * stage], x, bytes, hipMemcpyDeviceToDevice, c.s), "tap copy");
+    if (h->taps[2 * stage + 1])
+      c.check((int)hipMemcpyAsync(h->taps[2 * stage + 1], xb, bytes, hipMemcpyDeviceToDevice, c.s), "tap copy");
+  };
   // stem: conv1 3x3 3->64 + bn1 + prelu  (X), bn1 of the first block (XB)
   conv_bn(c, "stem.w", "stem.bn", xin, 4, N, 112, 3, 64, 3, 1, X[0], "stem.prelu", nullptr, XB[0], next_bn(0));
+  tap(0, X[0], XB[0], (size_t)N * 112 * 112 * 64 * es);
   int cur = 0, H = 112, C = 64;
   for (size_t i = 0; i < blks.size(); ++i) {
     const int li = blks[i].first, b = blks[i].second;
@@ -162,6 +174,7 @@ void arc_plan(ArcCtx& c, const void* xin, int N, float* emb) {
     cur ^= 1;
     H = Ho;
     C = planes;
+    tap(i + 1, X[cur], XB[cur], (size_t)N * H * H * C * es);
   }
   // head: fc over flatten(bn2(X)) as a 7x7 valid conv, features BatchNorm1d folded with the fc bias
   ConvDesc d;
@@ -424,6 +437,12 @@ extern "C" int ghost_arc_embed_u8(ghost_arc* h, const uint8_t* crops, int64_t cr
   // F.interpolate(scale_factor=0.5) output size floor(H/2) must be the network's 112
   if (H / 2 != 112 || W / 2 != 112) return arc_fail(GHOST_EINVAL, "crops must be 224x224 (or 225) to give 112x112");
   return run_arc(h, N, nullptr, 0, nullptr, crops, crop_batch_stride, H, W, emb, ws, ws_bytes, stream);
+}
+
+extern "C" int ghost_arc_set_taps(ghost_arc* h, void* const* taps, int ntaps) {
+  if (!h || ntaps < 0 || (ntaps && !taps)) return arc_fail(GHOST_EINVAL, "bad argument");
+  h->taps.assign(taps, taps + ntaps);
+  return 0;
 }
 
 extern "C" int ghost_arc_match(const float* face_emb, int F, const float* target_emb, int T, int dim,

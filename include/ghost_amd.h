@@ -225,6 +225,12 @@ int ghost_arc_embed_u8(ghost_arc* h, const uint8_t* crops, int64_t crop_batch_st
                        float* emb, void* ws, int64_t ws_bytes, void* stream);
 /* per target j: best_idx[j] = argmax_i cos(face_i, target_j) (first on ties), best_sim[j] = that
  * cosine, accepted[j] = best_sim[j] > similarity_th */
+/* Diagnostic taps (parity bisection): while set, every forward copies, for stage i (0 = the stem, i >= 1 =
+ * the i-th IBasicBlock in forward order), the stored residual stream X_i into taps[2i] and the next
+ * BatchNorm's output BN(X_i) (the producer's second output, what the next block's conv reads) into
+ * taps[2i+1], NHWC [N, H_i, W_i, C_i] in the handle dtype, where those pointers are non-NULL.
+ * ntaps = 0 clears them. */
+int ghost_arc_set_taps(ghost_arc* h, void* const* taps, int ntaps);
 int ghost_arc_match(const float* face_emb, int F, const float* target_emb, int T, int dim, float similarity_th,
                     int32_t* best_idx, float* best_sim, int32_t* accepted, void* stream);
 

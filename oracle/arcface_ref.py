@@ -142,6 +142,66 @@ def iresnet_forward(p, x, layers=LAYERS["iresnet100"]):
                         p["features.weight"].to(dt), p["features.bias"].to(dt), False, 0.0, BN_EPS)
 
 
+# ----------------------------------------------------------------------------------------------------
+# bf16-storage emulation of the runtime's plan (arc_runtime.hip): the same network with every tensor the
+# runtime stores rounded to bf16 where it stores it, fp32 in between:
+#   input x (after the prep kernel)                   -> bf16
+#   conv weights (stem, conv1/conv2, downsample, fc)  -> bf16 (BatchNorms stay fp32 epilogue scale/shift)
+#   stem  v = PReLU(bn1(conv(x)));         X = q(v), XB = q(bn1_block1(v))
+#   block T = q(PReLU(bn2(conv1(XB))));    R = q(bn(down(X))) (first block of a layer);
+#         v = bn3(conv2/s(T)) + (R | X);   X' = q(v), XB' = q(next BN(v))  (the head's bn2 after the last)
+#   head  emb = features(fc(flatten(XB))) in fp32 (bf16 operands)
+# ----------------------------------------------------------------------------------------------------
+def _qs(t, store):
+    return t.to(store).float()
+
+
+def stem_storage(p, x, store=torch.bfloat16, first_bn="layer1.0.bn1"):
+    """Stage 0 from the stored input x: (X, XB)."""
+    v = F.prelu(_bn(F.conv2d(x, _qs(p["conv1.weight"].float(), store), None, padding=1), p, "bn1"),
+                p["prelu.weight"].float())
+    return _qs(v, store), _qs(_bn(v, p, first_bn), store)
+
+
+def block_storage(p, X, XB, li, b, stride, next_bn, store=torch.bfloat16):
+    """IBasicBlock (li, b) from the stored (X, XB) of the stage before it: its stored (X', XB')."""
+    pre = f"layer{li}.{b}"
+    wq = lambda k: _qs(p[k].float(), store)  # noqa: E731
+    t = F.conv2d(XB, wq(f"{pre}.conv1.weight"), None, padding=1)
+    T = _qs(F.prelu(_bn(t, p, f"{pre}.bn2"), p[f"{pre}.prelu.weight"].float()), store)
+    res = X
+    if b == 0:
+        res = _qs(_bn(F.conv2d(X, wq(f"{pre}.downsample.0.weight"), None, stride=stride), p, f"{pre}.downsample.1"),
+                  store)
+    v = _bn(F.conv2d(T, wq(f"{pre}.conv2.weight"), None, stride=stride, padding=1), p, f"{pre}.bn3") + res
+    return _qs(v, store), _qs(_bn(v, p, next_bn), store)
+
+
+def head_storage(p, XB, store=torch.bfloat16):
+    x = F.linear(torch.flatten(XB, 1), _qs(p["fc.weight"].float(), store), p["fc.bias"].float())
+    return F.batch_norm(x, p["features.running_mean"].float(), p["features.running_var"].float(),
+                        p["features.weight"].float(), p["features.bias"].float(), False, 0.0, BN_EPS)
+
+
+def next_bn_names(layers):
+    """The BatchNorm each stage's second output applies: the next block's bn1, the head's bn2 last."""
+    bl = blocks(layers)
+    return [f"layer{li}.{b}.bn1" for li, b, *_ in bl] + ["bn2"]
+
+
+@torch.no_grad()
+def iresnet_forward_storage(p, x, layers=LAYERS["iresnet100"], store=torch.bfloat16):
+    """The runtime's bf16 plan end to end -> (emb, [(X_i, XB_i)] per stage)."""
+    nb = next_bn_names(layers)
+    x = _qs(x.float(), store)
+    X, XB = stem_storage(p, x, store, nb[0])
+    stages = [(X, XB)]
+    for i, (li, b, _inp, _planes, stride) in enumerate(blocks(layers)):
+        X, XB = block_storage(p, X, XB, li, b, stride, nb[i + 1], store)
+        stages.append((X, XB))
+    return head_storage(p, XB, store), stages
+
+
 def normalize_batch_u8(frames_u8: np.ndarray) -> torch.Tensor:
     """normalize_and_torch_batch (image_processing.py:37-48) on CPU: u8 NHWC -> NCHW in [-1, 1]."""
     t = torch.from_numpy(frames_u8.copy())
@@ -151,12 +211,16 @@ def normalize_batch_u8(frames_u8: np.ndarray) -> torch.Tensor:
     return (t - 0.5) / 0.5
 
 
-def embed_crops(p, frames_u8: np.ndarray, layers=LAYERS["iresnet100"]) -> torch.Tensor:
-    """netArc(F.interpolate(normalize_and_torch_batch(crops), scale_factor=0.5, bilinear, align_corners=True))
-    (core.py:43-44, video_processing.py:137-139)."""
+def preprocess_crops(frames_u8: np.ndarray) -> torch.Tensor:
+    """F.interpolate(normalize_and_torch_batch(crops), scale_factor=0.5, bilinear, align_corners=True)
+    (core.py:43-44, video_processing.py:137-139): the network input."""
     x = normalize_batch_u8(frames_u8).float()
-    x = F.interpolate(x, scale_factor=0.5, mode="bilinear", align_corners=True)
-    return iresnet_forward(p, x, layers)
+    return F.interpolate(x, scale_factor=0.5, mode="bilinear", align_corners=True)
+
+
+def embed_crops(p, frames_u8: np.ndarray, layers=LAYERS["iresnet100"]) -> torch.Tensor:
+    """netArc(preprocess_crops(crops))."""
+    return iresnet_forward(p, preprocess_crops(frames_u8), layers)
 
 
 def match_faces(face_embeds: torch.Tensor, target_embeds: torch.Tensor, similarity_th: float):

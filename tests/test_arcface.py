@@ -7,7 +7,12 @@ pipeline arithmetic around the network (normalize_and_torch_batch, the 0.5x alig
 face matching) is restated from the reference files cited in the oracle.
 
 Gates: fp32 path max|d emb| <= 2e-3 * max|emb| and cosine >= 0.99999 per row (100 residual blocks
-of fp32 MFMA in a different summation order); bf16 path cosine >= 0.99 per row.
+of fp32 MFMA in a different summation order).  bf16 path: against the storage-emulating oracle
+(arcface_ref.iresnet_forward_storage: every tensor the runtime stores rounded to bf16 where it stores
+it), per stage teacher-forced — the stem and every IBasicBlock recomputed from the GPU's own stored
+inputs must match the GPU's stored (X, BN(X)) within 2 bf16 ulps of max|ref| and a mean of 5e-3 of
+mean|ref|, the head's embedding within 1e-3 relative — and end to end no further from the fp32
+forward than the emulated bf16 arithmetic itself (1.25x in the mean and the max).
 """
 import ctypes as C
 
@@ -140,15 +145,55 @@ def test_embed_u8_batch_without_values_above_one():
     _close(emb, ref, 2e-3, 0.99999)
 
 
+def _ulp_bf16(x):
+    return 2.0 ** (np.floor(np.log2(max(x, 1e-30))) - 7)
+
+
+def _stage_close(g, r, what):
+    d = (g - r).abs()
+    assert float(d.max()) <= 2 * _ulp_bf16(float(r.abs().max())), (what, float(d.max()), float(r.abs().max()))
+    assert float(d.mean()) <= 5e-3 * float(r.abs().mean()), (what, float(d.mean()), float(r.abs().mean()))
+
+
 @pytest.mark.gpu
-def test_bf16_path_cosine():
+@pytest.mark.parametrize("arch", ["iresnet18", "iresnet100"])
+def test_bf16_each_stage_matches_storage_emulation(arch):
+    """Bisection by construction: each stage from the GPU's own stored inputs (ghost_arc_set_taps)."""
+    m = net(arch, compute_dtype=torch.bfloat16)
+    layers, p = A.LAYERS[arch], weights(arch)
+    x = torch.from_numpy(np.random.Generator(np.random.PCG64(6)).uniform(-1, 1, (2, 3, 112, 112)).astype(np.float32))
+    emb, taps = m.forward_taps(x.to(DEV))
+    torch.cuda.synchronize()
+    emb = emb.cpu()
+    assert emb.dtype == torch.float32 and taps[0][0].dtype == torch.bfloat16
+    taps = [(a.float().cpu(), b.float().cpu()) for a, b in taps]
+    nb = A.next_bn_names(layers)
+    with torch.no_grad():
+        X, XB = A.stem_storage(p, x.bfloat16().float(), torch.bfloat16, nb[0])
+        _stage_close(taps[0][0], X, "stem X")
+        _stage_close(taps[0][1], XB, "stem XB")
+        for i, (li, b, _inp, _planes, stride) in enumerate(A.blocks(layers)):
+            X, XB = A.block_storage(p, taps[i][0], taps[i][1], li, b, stride, nb[i + 1])
+            _stage_close(taps[i + 1][0], X, f"layer{li}.{b} X")
+            _stage_close(taps[i + 1][1], XB, f"layer{li}.{b} XB")
+        head = A.head_storage(p, taps[-1][1])
+    assert float((emb - head).abs().max()) <= 1e-3 * float(head.abs().max())
+
+
+@pytest.mark.gpu
+def test_bf16_end_to_end_error_is_the_intrinsic_storage_error():
     m = net(compute_dtype=torch.bfloat16)
-    crops = A.make_u8_faces(8, seed=5)
+    p = weights("iresnet100")
+    crops = A.make_u8_faces(4, seed=5)
     emb = m.embed_u8(torch.from_numpy(crops).to(DEV)).cpu()
     assert emb.dtype == torch.float32
-    ref = A.embed_crops(weights("iresnet100"), crops)
-    cos = F.cosine_similarity(emb, ref, dim=1)
-    assert float(cos.min()) >= 0.99, cos
+    ref = A.embed_crops(p, crops)
+    with torch.no_grad():
+        emu, _ = A.iresnet_forward_storage(p, A.preprocess_crops(crops))
+    dg, de = (emb - ref).abs(), (emu - ref).abs()
+    assert float(dg.mean()) <= 1.25 * float(de.mean()), (float(dg.mean()), float(de.mean()))
+    assert float(dg.max()) <= 1.25 * float(de.max()), (float(dg.max()), float(de.max()))
+    assert float(F.cosine_similarity(emb, ref, dim=1).min()) >= 0.999
 
 
 @pytest.mark.gpu
