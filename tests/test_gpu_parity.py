@@ -103,6 +103,37 @@ def test_conv2d_op(lib, dt, cin, cout, k, s, p, H):
     assert float((got - ref).abs().max()) <= tol * max(1.0, float(ref.abs().max()))
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H,B", [(256, 2), (256, 1), (64, 3), (128, 1)])
+def test_conv3x3_ring_op(lib, dt, H, B):
+    """The four-deep DMA ring (conv_halo.hip conv3x3_ring_kernel: 64 -> 64, no residual, 16 x 16 tiles) —
+    AADBlk8's first conv at 256 x 256 — against torch's fp32 conv of the same 16-bit operands; B = 1 at
+    128 x 128 gives 32 workgroups of two tiles, B = 3 at 64 x 64 an odd tile count per workgroup."""
+    from ghost_amd import _lib
+    from ghost_amd.network.pack import pack_conv, rup
+    g = torch.Generator().manual_seed(H + B)
+    x = torch.randn(B, 64, H, H, generator=g)
+    w = torch.randn(64, 64, 3, 3, generator=g) * (2.0 / (64 * 9)) ** 0.5
+    sc = torch.rand(64, generator=g) + 0.5
+    sh = torch.randn(64, generator=g) * 0.1
+    xr, wr = x.to(dt).float(), w.to(dt).float()
+    ref = F.leaky_relu(F.conv2d(xr, wr, padding=1) * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1), 0.2)
+    wp = pack_conv(w, dt).to(DEV)
+    xd = nhwc(x).to(dt).to(DEV)
+    y = torch.full((B, H, H, 64), float("nan"), dtype=dt, device=DEV)
+    scp = torch.zeros(128, device=DEV); scp[:64] = sc.to(DEV)
+    shp = torch.zeros(128, device=DEV); shp[:64] = sh.to(DEV)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=DEV)
+    _lib.check(lib.ghost_conv2d_nhwc(_lib.gdtype(dt), xd.data_ptr(), B, H, H, 64, 64, wp.data_ptr(), 64,
+                                     wp.shape[0], wp.shape[1], 3, 3, 1, 1, scp.data_ptr(), shp.data_ptr(), 0.2,
+                                     None, 0, 0, y.data_ptr(), 64, ws.data_ptr(), ws.numel(), stream(lib)))
+    got = y.float().cpu().permute(0, 3, 1, 2)
+    assert torch.isfinite(got).all()
+    ulp = 2.0 ** -7 if dt == torch.bfloat16 else 2.0 ** -10
+    d = (got - ref).abs()
+    assert float((d / ref.abs().clamp_min(1.0)).max()) <= 1.01 * ulp, float(d.max())
+
+
 @pytest.mark.parametrize("cin,cout,H,B,xoff,yoff,bn", [(32, 64, 32, 2, 32, 64, True), (64, 128, 64, 2, 0, 0, True),
                                                  (128, 256, 32, 3, 128, 256, True), (32, 64, 64, 1, 0, 0, False),
                                                  (256, 64, 32, 2, 256, 0, True)])
