@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--video", type=int, default=900, help="frames of the config-3 video leg")
     ap.add_argument("--cpu-batches", default="1,64", help="CPU baseline batch sizes ('' = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
-    ap.add_argument("--arc-batch", type=int, default=64, help="faces per ArcFace embedding batch in its leg")
+    ap.add_argument("--arc-batch", type=int, default=128, help="faces per ArcFace embedding batch in its leg")
     ap.add_argument("--streams", type=int, default=2,
                     help="batches in flight on the GPU (dp.GatherPipeline streams; 1 = one batch at a time)")
     ap.add_argument("--opt", action="append", default=[],

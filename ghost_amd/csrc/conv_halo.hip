@@ -29,10 +29,12 @@ namespace ghost {
 // IMG > 1: the tile is IMG whole TH x TW images (64 pixels, one per wave) of consecutive samples,
 // each with its own zero-padded halo — the generator's 8x8 stage (AADBlk3), where a 16 x 16 tile
 // would be three quarters padding and the implicit GEMM re-reads every pixel nine times.
+// IMG > 1 with TH * TW > 64: the tile is the same TH x TW window of IMG consecutive samples, WPI waves
+// per image (ArcFace's 14 x 14 / 28 x 28 stages: two samples share every weight stage).
 template <int TH_, int TW_, int WM_, int WN_, int IMG_ = 1>
 struct HaloCfg {
   static constexpr int TH = TH_, TW = TW_, WM = WM_, WN = WN_, IMG = IMG_;
-  static constexpr int BN = 64 * WN, NW = WM * WN;
+  static constexpr int BN = 64 * WN, NW = WM * WN, WPI = WM / IMG;
   static constexpr int HWW = TW + 2, HHH = TH + 2;
   static constexpr int HIMG = HHH * HWW;                    // halo pixels of one image
   static constexpr int HP = IMG * HIMG;                     // halo pixels
@@ -43,14 +45,16 @@ struct HaloCfg {
   static constexpr int HPW = (HPIECES + NW - 1) / NW;       // halo pieces per wave
   static constexpr int WPW = (WPIECES + NW - 1) / NW;       // weight pieces per wave
   static_assert(IMG * TH * TW == 64 * WM, "each wave owns 64 output pixels");
-  static_assert(IMG == 1 || (TH * TW == 64 && WN == 1), "multi-image tiles: one image per wave");
-  // wave w's pixel p (0..63): halo pixel index of tap (0, 0) and output offset within the tile
-  GHOST_DEV static int hrow0(int w) { return IMG > 1 ? 0 : w * (64 / TW); }
-  GHOST_DEV static int himg(int w) { return IMG > 1 ? w * HIMG : 0; }
+  static_assert(IMG == 1 || (WN == 1 && WM % IMG == 0), "multi-image tiles: whole waves per image");
+  // wave w: its image within the tile, the first tile row of its 64 pixels, its image's halo base
+  GHOST_DEV static int img(int w) { return IMG > 1 ? w / WPI : 0; }
+  GHOST_DEV static int hrow0(int w) { return (IMG > 1 ? w % WPI : w) * (64 / TW); }
+  GHOST_DEV static int himg(int w) { return img(w) * HIMG; }
 };
 using HaloWide = HaloCfg<16, 32, 8, 1>;    // W % 32 == 0: 16 x 32 tile, 8 waves, 75 KB LDS
 using HaloSmall = HaloCfg<16, 16, 4, 1>;   // W == 16: 16 x 16 tile, 4 waves, 57 KB LDS
 using HaloImg8 = HaloCfg<8, 8, 4, 1, 4>;   // 8 x 8 images, four per tile, 4 waves, 61 KB per stage
+using HaloPair = HaloCfg<16, 16, 8, 1, 2>; // a 16 x 16 window of two samples, 8 waves, 77 KB per stage
 
 struct HaloArgs {
   const void* x;   // 16-bit storage (bf16 or fp16: the kernels' T)
@@ -339,7 +343,8 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   // its channel block's 9 x 64 weight rows too (75 KB).
   constexpr int TW = G::TW, HWW = G::HWW, HP = G::HP, HPIECES = G::HPIECES, WPIECES = G::WPIECES;
   constexpr int HALO_B = G::HALO_B, NW = G::NW, HPW = G::HPW, WPW = G::WPW, IMG = G::IMG;
-  constexpr int NMAX = IMG > 1 ? 1024 : 512;   // channel tables (N <= NMAX)
+  // channel tables (N <= NMAX): the two-sample window fills LDS with its stages (2 x 77 KB) and takes N <= 256
+  constexpr int NMAX = IMG > 1 ? (EPX ? 256 : 1024) : 512;
   constexpr int WBLK_B = 9 * 64 * 64;                           // one channel block of weights
   constexpr int STAGE_B = RESW ? HALO_B : HALO_B + WBLK_B;
   // two stage buffers as DISTINCT objects, read/written in an unrolled ping-pong: hipcc then proves
@@ -349,7 +354,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   __shared__ __attribute__((aligned(1024))) unsigned char lds1[STAGE_B];
   __shared__ __attribute__((aligned(1024))) unsigned char ldsw[RESW ? 2 * WBLK_B : 16];
   __shared__ __attribute__((aligned(16))) float s_sc[NMAX], s_sh[NMAX];   // N <= NMAX (conv3x3_pp_takes / conv3x3_halo)
-  __shared__ __attribute__((aligned(16))) float s_ex[EPX ? 3 * 512 : 4];   // PReLU slope, scale2, shift2 (EPX)
+  __shared__ __attribute__((aligned(16))) float s_ex[EPX ? 3 * NMAX : 4];   // PReLU slope, scale2, shift2 (EPX)
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
   const int prow = lane >> 2, slot = lane & 3;
 
@@ -358,8 +363,8 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     s_sh[n] = a.shift ? a.shift[n] : 0.f;
     if constexpr (EPX) {
       s_ex[n] = a.prelu ? a.prelu[n] : a.slope;
-      s_ex[512 + n] = ay2_ ? a.scale2[n] : 0.f;
-      s_ex[1024 + n] = ay2_ ? a.shift2[n] : 0.f;
+      s_ex[NMAX + n] = ay2_ ? a.scale2[n] : 0.f;
+      s_ex[2 * NMAX + n] = ay2_ ? a.shift2[n] : 0.f;
     }
   }
   constexpr int ncb = NCB;
@@ -401,7 +406,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     const int tx = t % a.tiles_x;
     t /= a.tiles_x;
     const int ty = t % a.tiles_y;
-    r.base = (long)(t / a.tiles_y) * IMG * a.H * a.W;   // IMG > 1: tiles_x = tiles_y = 1, t = image group
+    r.base = (long)(t / a.tiles_y) * IMG * a.H * a.W;   // IMG > 1: t = group of IMG samples
     r.y0 = ty * G::TH;
     r.x0 = tx * TW;
     r.n0 = nt * 64;
@@ -529,7 +534,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       for (int i = 0; i < 4; ++i) {
         const int q = i * 16 + lr;
         const int oy = cur.y0 + G::hrow0(wid) + q / TW, ox = cur.x0 + q % TW;
-        const long pix = cur.base + (IMG > 1 ? (long)wid * a.H * a.W : 0L) + (long)oy * a.W + ox;
+        const long pix = cur.base + (long)G::img(wid) * a.H * a.W + (long)oy * a.W + ox;
         const bool in = !EPX || (oy < a.H && ox < a.W);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -541,7 +546,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     for (int i = 0; i < 4; ++i) {
       const int q = i * 16 + lr;
       const int oy = cur.y0 + G::hrow0(wid) + q / TW, ox = cur.x0 + q % TW;
-      const long pix = cur.base + (IMG > 1 ? (long)wid * a.H * a.W : 0L) + (long)oy * a.W + ox;
+      const long pix = cur.base + (long)G::img(wid) * a.H * a.W + (long)oy * a.W + ox;
       uint2 ov[4];   // W16: the 4 channel fragments' T outputs, stored 16 bytes at a time below
       if constexpr (EPX) {
         if (oy >= a.H || ox >= a.W) {
@@ -581,8 +586,8 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
           }
           *reinterpret_cast<uint2*>(ay_ + pix * a.ldy + n) = o;
           if (ay2_) {
-            const f32x4 tsc2 = *reinterpret_cast<const f32x4*>(s_ex + 512 + n);
-            const f32x4 tsh2 = *reinterpret_cast<const f32x4*>(s_ex + 1024 + n);
+            const f32x4 tsc2 = *reinterpret_cast<const f32x4*>(s_ex + NMAX + n);
+            const f32x4 tsh2 = *reinterpret_cast<const f32x4*>(s_ex + 2 * NMAX + n);
 #pragma unroll
             for (int r = 0; r < 4; ++r) oe[r] = (T)(v[r] * tsc2[r] + tsh2[r]);
             *reinterpret_cast<uint2*>(ay2_ + pix * a.ldy2 + n) = o;
@@ -628,7 +633,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       const int c = cur.n0 + (lr >> 2) * 16 + lq * 4 + (lr & 3);
       float* dst;
       if constexpr (IMG > 1) {   // the wave's 64 pixels are its whole image: one record per sample
-        const long b = cur.base / ((long)a.H * a.W) + wid;
+        const long b = cur.base / ((long)a.H * a.W) + G::img(wid);
         dst = a.in_part + (b * (long)a.N + c) * 2;
       } else {
         const int tile = (cur.y0 / G::TH) * a.tiles_x + cur.x0 / TW;
@@ -1181,7 +1186,7 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
     }
   }
 #endif
-  constexpr bool CAN_ST = G::TW == 32 || G::IMG > 1;
+  constexpr bool CAN_ST = G::TW != 16;   // the partials come from exact 16 x 32 tiles or whole 8 x 8 images
 #define GHOST_PP(R, ST, NB) \
   hipLaunchKernelGGL((conv3x3_halo_pp_kernel<T, G, R, ST, NB>), dim3((unsigned)g), dim3(NT), 0, s, a)
 #define GHOST_PP2(R, NB)                                  \
@@ -1269,8 +1274,12 @@ static int conv3x3_halo_t(const ConvDesc& d, hipStream_t s) {
   static const int pp = GHOST_KNOB("GHOST_HALO_PP", 1);
   const int ncb = d.Cin / 32;
   if (pp && pp_small(d) && d.N <= 512 && d.Cin % 64 == 0 &&
-      (ncb == 2 || ncb == 4 || ncb == 6 || ncb == 8 || ncb == 16 || ncb == 32))
+      (ncb == 2 || ncb == 4 || ncb == 6 || ncb == 8 || ncb == 16 || ncb == 32)) {
+    // two samples per tile (HaloPair) when the batch pairs up: every weight stage serves both
+    static const int pair = GHOST_KNOB("GHOST_HALO_PAIR", 0);
+    if (pair && d.B % 2 == 0 && d.N <= 256) return halo_pp_launch<T, HaloPair>(d, s);
     return halo_pp_launch<T, HaloSmall>(d, s);
+  }
   if (halo_exact_wide(d)) return halo_launch<T, HaloWide>(d, s);
   return halo_launch<T, HaloSmall>(d, s);
 }
