@@ -63,8 +63,9 @@ def parse():
     ap.add_argument("--num-blocks", type=int, default=2)
     ap.add_argument("--identities", type=int, default=1, help="source identities mixed in every batch (config 5: 4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--legs", default="d2h,config5,video,latency,arcface",
-                    help="side measurements at N=1 (comma list of d2h, config5, video, latency, arcface; '' = none)")
+    ap.add_argument("--legs", default="d2h,fp16,config5,video,latency,arcface",
+                    help="side measurements at N=1 (comma list of d2h, fp16, config5, video, latency, arcface; "
+                         "'' = none)")
     ap.add_argument("--video", type=int, default=900, help="frames of the config-3 video leg")
     ap.add_argument("--cpu-batches", default="1,64", help="CPU baseline batch sizes ('' = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
@@ -214,6 +215,39 @@ def arcface_leg(dev, n, steps, nstreams=1):
             "gflop_per_face": round(arcface_flops_per_face() / 1e9, 2),
             "mfma_tflops": round(fl / (ms / 1e3) / 1e12, 1),
             "mfma_frac": round(fl / (ms / 1e3) / 1e12 / BF16_PEAK_TFLOPS, 4)}
+
+
+def fp16_leg(dev, crops, z, steps, warmup, backbone, nb, nstreams=1):
+    """Config 2 with the reference's own GPU precision: the module .half()'d after loading its weights
+    (inference.py:27-30), fp16 crops' identity row (core.py:20-21): fp16 storage kernels
+    (v_mfma_f32_16x16x32_f16), about 4x closer to the fp32 forward than bf16 storage."""
+    from ghost_amd.network import AEI_Net
+    from oracle.aei_ref import make_weights, param_specs
+    G = AEI_Net(backbone, num_blocks=nb, c_id=512).eval()
+    G.load_state_dict(make_weights(param_specs(backbone, nb)))
+    G = G.to(dev).half()
+    zh = z.half()
+    B = crops.shape[0]
+    ns = max(1, nstreams)
+    outs = [torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev) for _ in range(ns)]
+    main = torch.cuda.current_stream(dev)
+    comp = [main] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+    for c in comp[1:]:
+        c.wait_stream(main)
+    k = [0]
+
+    def step():
+        i = k[0] % ns
+        with torch.cuda.stream(comp[i]):
+            G.swap_u8(crops, zh, out=outs[i])
+        k[0] += 1
+
+    el = timed(step, steps, warmup)
+    del G
+    torch.cuda.empty_cache()
+    return {"workload": f"config 2 with a .half() module: batch={B} {backbone}/{nb} fp16 storage (fp32 accumulation), "
+                        f"u8 in -> u8 out, {ns} batch(es) in flight",
+            "dtype": "f16", "frames_per_s": round(B * steps / el, 1), "ms_per_batch": round(el * 1e3 / steps, 3)}
 
 
 def d2h_leg(G, crops, z, steps, nstreams=1):
@@ -666,6 +700,8 @@ def main():
             res["legs"] = {}
         if "d2h" in legs:
             res["legs"]["d2h"] = d2h_leg(G, crops, z, a.steps, pipe.nstreams)
+        if "fp16" in legs:
+            res["legs"]["fp16"] = fp16_leg(dev, crops, z, a.steps, 3, a.backbone, a.num_blocks, pipe.nstreams)
         if "video" in legs and a.video > 0:
             res["legs"]["config3_video"] = video_leg(G, dev, a.video)
         if "config5" in legs:
