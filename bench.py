@@ -414,7 +414,7 @@ def latency_leg(dev, n=20):
     """BASELINE config 1 on the GPU: one 256x256 image-to-image swap (B = 1, unet/2), fp32 and bf16.
     latency_ms = wall time of one synchronous swap_u8 call (median of n, after warm-up); host_ms = the
     host time of the call alone (the Python wrapper + the native plan's launches onto an idle stream,
-    median of n)."""
+    median of n); graphed = the same through GraphedSwap (one HIP graph launch per call)."""
     out = {"workload": "config 1 on 1 GPU: B=1 unet/2 swap_u8 (u8 crop in -> u8 swap out, device-resident), "
                        "one call at a time, synchronised after each"}
     crop = torch.from_numpy(np.random.Generator(np.random.PCG64(21)).integers(0, 256, (1, 256, 256, 3),
@@ -437,7 +437,25 @@ def latency_leg(dev, n=20):
             lat.append(t2 - t0)
         out[name] = {"latency_ms": round(float(np.median(lat)) * 1e3, 3),
                      "host_ms": round(float(np.median(host)) * 1e3, 3)}
-        del G
+        # the same swap replayed as one HIP graph (ghost_amd.inference.GraphedSwap: inputs copied into the
+        # captured buffers, one hipGraphLaunch; identical bytes)
+        from ghost_amd.inference import GraphedSwap
+        gs = GraphedSwap(G, 1, dev)
+        for _ in range(5):
+            gs(crop, z, out=y)
+        torch.cuda.synchronize()
+        lat, host = [], []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            gs(crop, z, out=y)
+            t1 = time.perf_counter()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            host.append(t1 - t0)
+            lat.append(t2 - t0)
+        out[name]["graphed"] = {"latency_ms": round(float(np.median(lat)) * 1e3, 3),
+                                "host_ms": round(float(np.median(host)) * 1e3, 3)}
+        del gs, G
         torch.cuda.empty_cache()
     return out
 

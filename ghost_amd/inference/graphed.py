@@ -1,0 +1,61 @@
+"""One swap of a fixed batch shape replayed as a HIP graph (BASELINE config 1: image-to-image at B = 1).
+
+``AEI_Net.swap_u8`` issues the native plan's ~100 kernel launches from the host on every call (≈ 0.3-0.4 ms
+of host time at B = 1, comparable to the GPU time of the whole forward).  For a caller that swaps batches of
+one shape over and over — one target image after another (inference.py's image mode), or frame batches of a
+video — ``GraphedSwap`` captures that launch sequence once (``torch.cuda.graph``: hipStreamBeginCapture on a
+side stream; the plan's second, up-path stream joins the capture through the events it already records) and
+replays it with one ``hipGraphLaunch``.  The inputs are copied into the graph's own device buffers first and
+the result is read from its output buffer, so the replay runs the same kernels on the same weights: the
+output bytes are identical to ``swap_u8``'s (tests/test_gpu_pipeline.py).
+
+The graph holds the module's packed weights and workspace as they were at capture: after
+``load_state_dict`` / ``.to`` / an in-place parameter change, build a new ``GraphedSwap``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+
+class GraphedSwap:
+    def __init__(self, G, B: int, device, z_rows: int = 1, z_dtype: Optional[torch.dtype] = None):
+        dev = torch.device(device)
+        if z_rows not in (1, B):
+            raise ValueError("ghost_amd: z_rows must be 1 or B")
+        self.G, self.B, self.device = G, B, dev
+        zt = z_dtype or next(G.parameters()).dtype
+        self.crops = torch.zeros(B, 256, 256, 3, dtype=torch.uint8, device=dev)
+        self.z = torch.zeros(z_rows, G.c_id, dtype=zt, device=dev)
+        self.out = torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev)
+        side = torch.cuda.Stream(dev)
+        cur = torch.cuda.current_stream(dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):       # warm-up outside the capture: packs the weights, creates the
+            for _ in range(2):              # native handle's streams/events, sizes the workspace
+                G.swap_u8(self.crops, self.z, out=self.out)
+        cur.wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            G.swap_u8(self.crops, self.z, out=self.out)
+        torch.cuda.synchronize(dev)
+
+    def __call__(self, crops_u8: torch.Tensor, z_id: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """swap_u8(crops_u8, z_id): inputs copied into the graph's buffers, one graph launch on the current
+        stream; returns ``out`` (copied) or the graph's own output buffer (overwritten by the next call)."""
+        if tuple(crops_u8.shape) != tuple(self.crops.shape) or crops_u8.dtype != torch.uint8:
+            raise RuntimeError(f"ghost_amd: GraphedSwap was captured for uint8 {tuple(self.crops.shape)}, got "
+                               f"{crops_u8.dtype} {tuple(crops_u8.shape)}")
+        z = z_id.reshape(z_id.shape[0], -1)
+        if tuple(z.shape) != tuple(self.z.shape):
+            raise RuntimeError(f"ghost_amd: GraphedSwap was captured for z_id {tuple(self.z.shape)}, got "
+                               f"{tuple(z_id.shape)}")
+        self.crops.copy_(crops_u8, non_blocking=True)
+        self.z.copy_(z, non_blocking=True)
+        self.graph.replay()
+        if out is None:
+            return self.out
+        out.copy_(self.out, non_blocking=True)
+        return out

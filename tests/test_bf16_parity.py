@@ -78,9 +78,12 @@ def run(backbone, nb, B=64, rows=ROWS, st="bf16"):
     ri = torch.tensor(rows)
     zr = z[ri] if st == "bf16" else z[ri].half().float()
     xr = xt[ri] if st == "bf16" else xt[ri].half().float()
-    r = {"p": p, "z": zr, "xt": xr, "Y": Y[ri].float().cpu(), "u8": u8[ri].cpu().numpy(),
+    # a .half() module holds every parameter and buffer in float16 (fc1/fc2, conv_h, biases, BatchNorm
+    # statistics included: torch's Module.half()): the emulation runs on those rounded values
+    pe = p if st == "bf16" else {k: v.half().float() for k, v in p.items()}
+    r = {"p": pe, "z": zr, "xt": xr, "Y": Y[ri].float().cpu(), "u8": u8[ri].cpu().numpy(),
          "attr": [a[ri].float().cpu() for a in attr], "blocks": [b[ri].float().cpu() for b in blocks]}
-    r["emu"] = aei_ref.aei_forward_bf16_storage(p, r["xt"], r["z"], backbone, nb, store=STORE[st])
+    r["emu"] = aei_ref.aei_forward_bf16_storage(pe, r["xt"], r["z"], backbone, nb, store=STORE[st])
     r["fp32"] = aei_ref.aei_forward(p, r["xt"], r["z"], backbone, nb)[0]
     _CACHE[key] = r
     return r

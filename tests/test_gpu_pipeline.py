@@ -201,3 +201,19 @@ def test_gather_pipeline_two_batches_in_flight(lib):
     assert len(got) == len(ref)
     for a, b in zip(got, ref):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dt,B", [(None, 1), (torch.bfloat16, 1), (torch.bfloat16, 4)])
+def test_graphed_swap_is_bit_identical(lib, dt, B):
+    """GraphedSwap (one HIP graph replay of the whole native plan, two-stream plan included) gives the
+    bytes of an eager swap_u8, for new inputs copied into the captured buffers on every call."""
+    from ghost_amd.inference import GraphedSwap
+    G, _p = model("unet", 2, dt)
+    g = GraphedSwap(G, B, DEV)
+    for seed in (3, 4):
+        crops = torch.from_numpy(aei_ref.make_u8_crops(B, seed)).to(DEV)
+        z = torch.randn(1, 512, generator=torch.Generator().manual_seed(seed)).to(DEV)
+        got = g(crops, z).clone()
+        ref = G.swap_u8(crops, z)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
