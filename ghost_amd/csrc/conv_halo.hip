@@ -656,243 +656,6 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
 }
 
 // ---------------------------------------------------------------------------
-// The 256 x 256 stage's 64 -> 64 conv (AADBlk8's first conv, AADLayer.py:64 inside AAD_ResBlk,
-// AEI_Net.py:137) as a four-deep DMA ring of 16 x 16 tiles.
-//
-// The 16 x 32 persistent kernel above keeps ONE stage (39 KB of halo) in flight beside the resident
-// 72 KB of weights: every stage computes for ~2 us and then waits for a DMA issued only one stage
-// earlier, which under load takes longer than that (measured: 12 us per tile against 4.6 us of
-// MFMA).  Here a tile is 16 x 16 (an 18 x 18 halo: 21 KB per channel block), four waves each own
-// 4 rows x 16 pixels x 64 channels, and four stage buffers are in flight: the DMA of stage s + 3 is
-// issued at the top of stage s, three stages (~3 us of MFMA) before it is read.
-//   LDS: 4 x 21 KB halo stages + 72 KB resident weights + 0.5 KB tables = 160,256 B (one WG per CU)
-//   top of stage s (s = 2 tile + channel block):
-//     s_waitcnt vmcnt(N)   N = the VM ops this wave issued after DMA(s), static from stage 4 on
-//                          (6 DMAs per stage — past the end repeats —, 8 W16 stores + 1 partials
-//                          store per tile end: 2*6 + 2*9 before a tile's first stage, 2*6 + 9 before
-//                          its second); vmcnt(0) in the four peeled first stages
-//     lgkmcnt(0) + raw s_barrier (every wave's DMA(s) landed; buffer (s - 1) % 4 free)
-//     issue DMA(s + 3) -> buffer (s + 3) % 4
-//     9 taps x 16 MFMA;  second block of a tile -> epilogue (+ InstanceNorm partials)
-// Every wave issues exactly 6 halo DMAs per stage (21 pieces of 16 pixels over 4 waves: the three
-// waves with 5 repeat their fifth piece, same source and destination) so the counts are uniform.
-// ---------------------------------------------------------------------------
-template <typename T, bool STATS>
-__global__ void __launch_bounds__(256) conv3x3_ring_kernel(const HaloArgs a) {
-  const T* __restrict__ ax_ = reinterpret_cast<const T*>(a.x);
-  const T* __restrict__ aw_ = reinterpret_cast<const T*>(a.w);
-  T* __restrict__ ay_ = reinterpret_cast<T*>(a.y);
-  constexpr int TH = 16, TW = 16, HWW = 18, HP = HWW * (TH + 2), NW = 4;
-  constexpr int HPIECES = (HP + 15) / 16, HPW = (HPIECES + NW - 1) / NW, WPIECES = 36, WPW = WPIECES / NW;
-  constexpr int STAGE_B = HPIECES * 1024, WBLK_B = 9 * 64 * 64;
-  constexpr int NEP = 8 + (STATS ? 1 : 0);   // VM ops of a tile's epilogue per wave
-  static_assert(HPIECES == 21 && HPW == 6 && WPIECES % NW == 0, "ring geometry");
-  __shared__ __attribute__((aligned(1024))) unsigned char lds0[STAGE_B];
-  __shared__ __attribute__((aligned(1024))) unsigned char lds1[STAGE_B];
-  __shared__ __attribute__((aligned(1024))) unsigned char lds2[STAGE_B];
-  __shared__ __attribute__((aligned(1024))) unsigned char lds3[STAGE_B];
-  __shared__ __attribute__((aligned(1024))) unsigned char ldsw[2 * WBLK_B];
-  __shared__ __attribute__((aligned(16))) float s_sc[64], s_sh[64];
-  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
-  const int prow = lane >> 2, slot = lane & 3;
-  if (tid < 64) {
-    s_sc[tid] = a.scale ? a.scale[tid] : 1.f;
-    s_sh[tid] = a.shift ? a.shift[tid] : 0.f;
-  }
-#if defined(__HIP_DEVICE_COMPILE__)
-  // both channel blocks' 9 x 64 weight rows, resident for the kernel
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int j = 0; j < WPW; ++j) {
-      const int piece = wid + j * NW;
-      const int tap = piece / 4, n = (piece % 4) * 16 + prow;
-      __builtin_amdgcn_global_load_lds(aw_ + n * a.Kpad + cb * 288 + tap * 32 + ((slot ^ hswz(n)) * 8),
-                                       ldsw + cb * WBLK_B + piece * 1024, 16, 0, 0);
-    }
-#endif
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const int G_ = gridDim.x;
-  const int xt = xcd_tile(blockIdx.x, G_);
-  const int nmine = a.ntiles > xt ? (a.ntiles - xt + G_ - 1) / G_ : 0;
-  if (nmine == 0) return;
-  const int nst = 2 * nmine;
-  struct Tile { long base; int y0, x0; };
-  auto tile_of = [&](int k) {
-    int t = k * G_ + xt;
-    Tile r;
-    const int tx = t % a.tiles_x;
-    t /= a.tiles_x;
-    const int ty = t % a.tiles_y;
-    r.base = (long)(t / a.tiles_y) * a.H * a.W;
-    r.y0 = ty * TH;
-    r.x0 = tx * TW;
-    return r;
-  };
-  // this lane's halo DMA: element offset from the tile's sample base per piece (bit j of h_ok = inside
-  // the image) and the LDS piece it lands in (a repeat of piece j = 4 for the waves with five)
-  int h_off[HPW], h_dst[HPW];
-  unsigned h_ok = 0u;
-  long dma_base = 0;
-  auto set_dma_tile = [&](const Tile& t) {
-    dma_base = t.base * a.ldx;
-    h_ok = 0u;
-#pragma unroll
-    for (int j = 0; j < HPW; ++j) {
-      int piece = wid + j * NW;
-      if (piece >= HPIECES) piece -= NW;
-      const int P = piece * 16 + prow;
-      const int hy = P / HWW, hx = P - hy * HWW;
-      const int iy = t.y0 - 1 + hy, ix = t.x0 - 1 + hx;
-      const bool ok = P < HP && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-      h_off[j] = ok ? (iy * a.W + ix) * a.ldx + ((slot ^ hswz(P)) * 8) : 0;
-      h_dst[j] = piece * 1024;
-      h_ok |= (ok ? 1u : 0u) << j;
-    }
-  };
-  auto issue = [&](unsigned char* buf, int cb) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const T* __restrict__ xs = ax_ + dma_base + cb * 32;
-#pragma unroll
-    for (int j = 0; j < HPW; ++j) {
-      const void* src = ((h_ok >> j) & 1u) ? (const void*)(xs + h_off[j]) : (const void*)g_halo_zero;
-      __builtin_amdgcn_global_load_lds(src, buf + h_dst[j], 16, 0, 0);
-    }
-#endif
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: stages 0, 1 (tile 0) and 2 (tile 1, block 0); the launch gives every WG >= 2 tiles
-  set_dma_tile(tile_of(0));
-  issue(lds0, 0);
-  issue(lds1, 1);
-  set_dma_tile(tile_of(1));
-  issue(lds2, 0);
-  Tile cur = tile_of(0);
-  // steady: the counted wait (every DMA and epilogue of the three stages before was issued)
-  auto step = [&](int s, auto jt, bool steady) {
-    constexpr int J = decltype(jt)::value, cb = J & 1;
-    unsigned char* buf = J == 0 ? lds0 : J == 1 ? lds1 : J == 2 ? lds2 : lds3;
-    unsigned char* nbuf = J == 0 ? lds3 : J == 1 ? lds0 : J == 2 ? lds1 : lds2;   // (J + 3) % 4
-    // gfx9 simm16: vm[3:0] exp[6:4] lgkm[11:8] vm[5:4]@[15:14]
-    constexpr int N = cb == 0 ? 2 * HPW + 2 * NEP : 2 * HPW + NEP;
-    static_assert(N < 64, "vmcnt range");
-    if (steady)
-      __builtin_amdgcn_s_waitcnt(((N >> 4) << 14) | 0x0F70 | (N & 15));
-    else
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-    // DMA(s + 3), unconditionally: past the last stage it repeats the last tile's block into a buffer no
-    // stage reads again, so that every path into a stage carries the same VM ops (hipcc's own wait
-    // analysis then finds the counted wait sufficient and inserts no drain of its own)
-    if constexpr (cb == 1) {
-      if (s + 3 < nst) set_dma_tile(tile_of((s + 3) >> 1));
-    }
-    issue(nbuf, cb ^ 1);
-    if constexpr (cb == 0) cur = tile_of(s >> 1);
-    const unsigned char* wb = ldsw + cb * WBLK_B;
-    v8_t<T> wf[2][4], pf[2][4];
-    auto load_frags = [&](int tap, v8_t<T> (&w)[4], v8_t<T> (&p)[4]) {
-      const int dy = tap / 3, dx = tap - dy * 3;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = j * 16 + lr;
-        w[j] = *reinterpret_cast<const v8_t<T>*>(wb + (tap * 64 + n) * 64 + ((lq ^ hswz(n)) * 16));
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int P = (wid * 4 + i + dy) * HWW + lr + dx;   // the wave's row i, column lr
-        p[i] = *reinterpret_cast<const v8_t<T>*>(buf + P * 64 + ((lq ^ hswz(P)) * 16));
-      }
-    };
-    load_frags(0, wf[0], pf[0]);
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      asm volatile("" ::: "memory");
-      if (tap + 1 < 9) load_frags(tap + 1, wf[(tap + 1) & 1], pf[(tap + 1) & 1]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[j][i] = mfma16x16x32<T>(wf[tap & 1][j], pf[tap & 1][i], acc[j][i]);
-    }
-    if constexpr (cb == 0) return;
-    // epilogue: 8 sixteen-byte stores per wave (+ 1 partials record): lanes lq and lq ^ 1 exchange the
-    // channel fragment the partner completes (as in conv3x3_halo_pp_kernel's W16 epilogue)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int oy = cur.y0 + wid * 4 + i, ox = cur.x0 + lr;
-      const long pix = cur.base + (long)oy * a.W + ox;
-      uint2 ov[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = j * 16 + lq * 4;
-        const f32x4 tsc = *reinterpret_cast<const f32x4*>(s_sc + n);
-        const f32x4 tsh = *reinterpret_cast<const f32x4*>(s_sh + n);
-        T* oe = reinterpret_cast<T*>(&ov[j]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = fmaf(acc[j][i][r], tsc[r], tsh[r]);
-          v = v > 0.f ? v : v * a.slope;
-          oe[r] = (T)v;
-          acc[j][i][r] = STATS ? (float)oe[r] : 0.f;   // the stored (rounded) value, for the statistics
-        }
-      }
-      const bool odd = (lq & 1) != 0;
-      const uint2 sa = odd ? ov[0] : ov[1], sb = odd ? ov[2] : ov[3];
-      uint2 ga, gb;
-      ga.x = (unsigned)__shfl_xor((int)sa.x, 16, 64);
-      ga.y = (unsigned)__shfl_xor((int)sa.y, 16, 64);
-      gb.x = (unsigned)__shfl_xor((int)sb.x, 16, 64);
-      gb.y = (unsigned)__shfl_xor((int)sb.y, 16, 64);
-      const uint2 a0 = odd ? ga : ov[0], a1 = odd ? ov[1] : ga;
-      const uint2 b0 = odd ? gb : ov[2], b1 = odd ? ov[3] : gb;
-      T* yp = ay_ + pix * a.ldy + (lq & 2) * 4;
-      *reinterpret_cast<u32x4*>(yp + (odd ? 16 : 0)) = u32x4{a0.x, a0.y, a1.x, a1.y};
-      *reinterpret_cast<u32x4*>(yp + (odd ? 48 : 32)) = u32x4{b0.x, b0.y, b1.x, b1.y};
-    }
-    if constexpr (STATS) {
-      float S1, S2;
-      tile_stats64(acc, lr, S1, S2);
-      const int c = (lr >> 2) * 16 + lq * 4 + (lr & 3);
-      const int tile = (cur.y0 / TH) * a.tiles_x + cur.x0 / TW;
-      const long b = cur.base / ((long)a.H * a.W);
-      float* dst = a.in_part + ((((b * a.tiles_x * a.tiles_y) + tile) * NW + wid) * 64L + c) * 2;
-      *reinterpret_cast<float2*>(dst) = make_float2(S1, S2);
-    }
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  // stages 0..3 peeled (waits for 0), then whole periods of four stages (the loop header is reached only
-  // after a whole period: the same VM ops in flight on every entry), then a last odd tile
-  step(0, I0{}, false);
-  step(1, I1{}, false);
-  step(2, I2{}, false);
-  step(3, I3{}, false);
-  int s = 4;
-  for (; s + 4 <= nst; s += 4) {
-    step(s, I0{}, true);
-    step(s + 1, I1{}, true);
-    step(s + 2, I2{}, true);
-    step(s + 3, I3{}, true);
-  }
-  if (s < nst) {
-    step(s, I0{}, true);
-    step(s + 1, I1{}, true);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// ---------------------------------------------------------------------------
 // ConvTranspose2d 4x4/s2/p1 (AEI_Net.py:27-41, the encoder's deconv layers) on the same plan:
 // a workgroup owns an 8 x 16 tile of INPUT pixels (= a 16 x 32 output tile: four sub-pixel
 // phases) and BN output channels.  Per block of 32 input channels it DMAs the 10 x 18 input
@@ -1232,52 +995,27 @@ bool conv3x3_pp_takes(const ConvDesc& d, int* nrec) {
   // -11 %, 32x32 512->512 -6 %, 32x32 1024->256 -8 %: +3 % frames/s end to end)
   const bool cin_ok = d.Cin == 64 || d.Cin == 128 || d.Cin == 192 || d.Cin == 256 || d.Cin == 512 || d.Cin == 1024;
   const bool ok = wide && pp && d.N <= 512 && d.N % 64 == 0 && cin_ok && d.Cin <= max_cin && !d.tanh_out;
-  // records per sample: one per wave and tile = 64 pixels each (16 x 32 tiles x 8 waves, or the ring's
-  // 16 x 16 tiles x 4 waves: the same count)
+  // records per sample: one per wave and tile = 64 pixels each (16 x 32 tiles x 8 waves)
   if (ok && nrec) *nrec = (d.Hi / HaloWide::TH) * (d.Wi / HaloWide::TW) * 8;
   return ok;
-}
-
-// the four-deep ring (conv3x3_ring_kernel): 64 -> 64 channels, no residual, whole 16 x 16 tiles, the
-// persistent kernel's other conditions (16-byte stores) — the generator's 256 x 256 conv
-static bool ring_takes(const ConvDesc& d) {
-  static const int on = GHOST_KNOB("GHOST_HALO_RING", 0);
-  return on && d.Cin == 64 && d.N == 64 && !d.res && d.Hi % 16 == 0 && d.Wi % 16 == 0 && d.Hi >= 64 &&
-         conv3x3_pp_takes(d, nullptr);
-}
-
-template <typename T>
-static int ring_launch(const ConvDesc& d, hipStream_t s) {
-  HaloArgs a{};
-  a.x = d.x; a.w = d.w; a.y = d.y;
-  a.scale = d.scale; a.shift = d.shift;
-  a.H = d.Hi; a.W = d.Wi; a.Cin = d.Cin; a.ldx = d.ldx; a.N = d.N; a.Kpad = d.Kpad;
-  a.ldy = d.ldy; a.slope = d.slope;
-  a.tiles_x = d.Wi / 16; a.tiles_y = d.Hi / 16; a.nNt = 1;
-  a.ntiles = d.B * a.tiles_x * a.tiles_y;
-  a.in_part = d.in_part;
-  const int g = a.ntiles / 2 < num_cus() ? a.ntiles / 2 : num_cus();   // >= 2 tiles per WG (the prologue)
-  if (g < 1) return -1;
-  if (a.in_part)
-    hipLaunchKernelGGL((conv3x3_ring_kernel<T, true>), dim3((unsigned)g), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv3x3_ring_kernel<T, false>), dim3((unsigned)g), dim3(256), 0, s, a);
-  return (int)hipGetLastError();
 }
 
 template <typename T>
 static int conv3x3_halo_t(const ConvDesc& d, hipStream_t s) {
   if (halo_img8(d)) return conv3x3_pp_takes(d, nullptr) ? halo_pp_launch<T, HaloImg8>(d, s) : -1;
-  if (ring_takes(d)) return ring_launch<T>(d, s);
   if (conv3x3_pp_takes(d, nullptr)) return halo_pp_launch<T, HaloWide>(d, s);
   if (d.in_part) return -1;   // only the persistent 16 x 32 kernel writes InstanceNorm partials
   static const int pp = GHOST_KNOB("GHOST_HALO_PP", 1);
   const int ncb = d.Cin / 32;
   if (pp && pp_small(d) && d.N <= 512 && d.Cin % 64 == 0 &&
       (ncb == 2 || ncb == 4 || ncb == 6 || ncb == 8 || ncb == 16 || ncb == 32)) {
-    // two samples per tile (HaloPair) when the batch pairs up: every weight stage serves both
-    static const int pair = GHOST_KNOB("GHOST_HALO_PAIR", 0);
-    if (pair && d.B % 2 == 0 && d.N <= 256) return halo_pp_launch<T, HaloPair>(d, s);
+    // two samples per tile (HaloPair) when the batch pairs up: every weight stage serves both.  Measured
+    // (ArcFace iresnet100 bf16, per conv): it wins wherever the paired grid still has a work item per CU —
+    // B = 128: 14x14 51.2 -> 40.8 us, 28x28 63.9 -> 51.2, 56x56 107.7 -> 83.8; B = 64: 28x28 35.3 -> 29.2,
+    // 56x56 59.4 -> 46.6 — and loses below that (B = 64 at 14x14, 128 items: 28.8 -> 36.2 us)
+    static const int pair = GHOST_KNOB("GHOST_HALO_PAIR", 1);
+    const long pair_items = (long)(d.B / 2) * ((d.Wi + 15) / 16) * ((d.Hi + 15) / 16) * (d.N / 64);
+    if (pair && d.B % 2 == 0 && d.N <= 256 && pair_items >= num_cus()) return halo_pp_launch<T, HaloPair>(d, s);
     return halo_pp_launch<T, HaloSmall>(d, s);
   }
   if (halo_exact_wide(d)) return halo_launch<T, HaloWide>(d, s);

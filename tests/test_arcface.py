@@ -156,17 +156,20 @@ def _stage_close(g, r, what):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("arch", ["iresnet18", "iresnet100"])
-def test_bf16_each_stage_matches_storage_emulation(arch):
-    """Bisection by construction: each stage from the GPU's own stored inputs (ghost_arc_set_taps)."""
+@pytest.mark.parametrize("arch,B", [("iresnet18", 2), ("iresnet100", 2), ("iresnet100", 128)])
+def test_bf16_each_stage_matches_storage_emulation(arch, B):
+    """Bisection by construction: each stage from the GPU's own stored inputs (ghost_arc_set_taps).  B = 128
+    runs the two-sample halo window (HaloPair) at 56x56 / 28x28 / 14x14; two of its rows are checked."""
     m = net(arch, compute_dtype=torch.bfloat16)
     layers, p = A.LAYERS[arch], weights(arch)
-    x = torch.from_numpy(np.random.Generator(np.random.PCG64(6)).uniform(-1, 1, (2, 3, 112, 112)).astype(np.float32))
+    x = torch.from_numpy(np.random.Generator(np.random.PCG64(6)).uniform(-1, 1, (B, 3, 112, 112)).astype(np.float32))
     emb, taps = m.forward_taps(x.to(DEV))
     torch.cuda.synchronize()
-    emb = emb.cpu()
+    rows = torch.tensor([0, 1] if B == 2 else [0, 77])
+    x = x[rows]
+    emb = emb[rows.to(DEV)].cpu()
     assert emb.dtype == torch.float32 and taps[0][0].dtype == torch.bfloat16
-    taps = [(a.float().cpu(), b.float().cpu()) for a, b in taps]
+    taps = [(a[rows.to(DEV)].float().cpu(), b[rows.to(DEV)].float().cpu()) for a, b in taps]
     nb = A.next_bn_names(layers)
     with torch.no_grad():
         X, XB = A.stem_storage(p, x.bfloat16().float(), torch.bfloat16, nb[0])
@@ -209,3 +212,17 @@ def test_match_faces_vs_oracle():
     assert best.cpu().tolist() == rb.tolist()
     assert torch.allclose(sim.cpu(), rs, atol=1e-5)
     assert ok.cpu().tolist() == rok.tolist()
+
+
+@pytest.mark.gpu
+def test_embed_batch_permutation_is_exact():
+    """All 128 rows: a permuted batch gives the permuted embeddings bit for bit (the paired halo window,
+    overhanging tiles and per-sample records must not mix rows)."""
+    m = net(compute_dtype=torch.bfloat16)
+    crops = torch.from_numpy(np.random.Generator(np.random.PCG64(12)).integers(0, 256, (128, 224, 224, 3),
+                                                                              dtype=np.uint8)).to(DEV)
+    perm = torch.randperm(128, generator=torch.Generator().manual_seed(2)).to(DEV)
+    e = m.embed_u8(crops)
+    ep = m.embed_u8(crops[perm].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(ep, e[perm])

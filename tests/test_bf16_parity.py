@@ -177,12 +177,19 @@ def test_swap_batch_permutation_is_exact(st):
     outp = G.swap_u8(crops[perm].contiguous(), z[perm].contiguous())
     torch.cuda.synchronize()
     assert torch.equal(outp, out[perm])
-    # and a batch of 1 reproduces its row of the batch of 64 (per-sample arithmetic; the kernels differ
-    # for B = 1, so allow the 1-LSB truncation flips of faceshifter_run.py:20-21)
+    # and a batch of 1 reproduces its row of the batch of 64 up to 16-bit storage noise: B = 1 runs other
+    # kernels (split-K GEMMs, the generic AAD path), whose different fp32 summation order flips 16-bit
+    # roundings that compound through 8 InstanceNorm'd blocks (measured up to 34 LSB in
+    # bf16).  Yardstick: the B = 64 row's own distance from the fp32 oracle.
     one = G.swap_u8(crops[7:8].contiguous(), z[7:8].contiguous())
     torch.cuda.synchronize()
-    d = (one[0].int() - out[7].int()).abs()
-    assert int(d.max()) <= 3 and float((d > 0).float().mean()) < 0.02
+    d = (one[0].int() - out[7].int()).abs().cpu().numpy()
+    xt = aei_ref.transform_target(crops[7:8].cpu().numpy())
+    ref = aei_ref.y_to_u8_bgr(aei_ref.aei_forward(_p, xt, z[7:8].float().cpu())[0])[0].astype(np.int16)
+    d32 = np.abs(out[7].cpu().numpy().astype(np.int16) - ref)
+    k = max(1, d.size // 200)
+    assert d.mean() <= 1.25 * d32.mean() + 0.02, (float(d.mean()), float(d32.mean()))
+    assert np.sort(d, axis=None)[-k:].mean() <= 1.3 * np.sort(d32, axis=None)[-k:].mean() + 1.0
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
