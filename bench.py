@@ -77,7 +77,29 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_substr):
+_MANGLED_TYPES = {"__bf16": "DF16b", "_Float16": "DF16_", "float": "f"}
+
+
+def mangle(kname):
+    """'aad_v5_kernel<__bf16, 64, 2, true, 2, true>' -> 'aad_v5_kernelIDF16bLi64ELi2ELb1ELi2ELb1EE' (the Itanium
+    template-argument part of the symbol rocprofv3 records)."""
+    import re
+    m = re.match(r"(\w+)<(.*)>", kname)
+    if not m:
+        return None
+    base, targs = m.group(1), [t.strip() for t in m.group(2).split(",")]
+    enc = []
+    for t in targs:
+        if t in _MANGLED_TYPES:
+            enc.append(_MANGLED_TYPES[t])
+        elif t in ("true", "false"):
+            enc.append("Lb1E" if t == "true" else "Lb0E")
+        else:
+            enc.append(f"Li{t}E")
+    return base + "I" + "".join(enc) + "E"
+
+
+def pmc_traffic(kname):
     """HBM bytes per launch of a kernel from the committed PMC summary (tools/pmc_traffic.py over
     separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 FETCH x2 correction)."""
     import glob
@@ -90,8 +112,9 @@ def pmc_traffic(kernel_substr):
     except (OSError, ValueError):
         return None
     rel = os.path.relpath(path, REPO)
+    key = mangle(kname) or kname
     for k in data.get("kernels", []):
-        if kernel_substr in k["kernel"] and k.get("hbm_bytes"):
+        if key in k["kernel"] and k.get("hbm_bytes"):
             return {"bytes_per_launch": k["hbm_bytes"], "read": k["read_bytes"], "write": k["write_bytes"],
                     "source": rel + " (" + data.get("source", "rocprofv3 --pmc") + ")"}
     return None
@@ -103,12 +126,9 @@ def rocprof_avg_us(kname):
     (profiles/rNN_kernel_stats_1stream.csv).  kname: the demangled 'aad_v5_kernel<64, 2, true, 2>'."""
     import csv
     import glob
-    import re
-    m = re.match(r"(\w+)<(.*)>", kname)
-    if not m:
+    mangled = mangle(kname)
+    if not mangled:
         return None
-    base, targs = m.group(1), [t.strip() for t in m.group(2).split(",")]
-    mangled = base + "I" + "".join(("Lb1E" if t == "true" else "Lb0E" if t == "false" else f"Li{t}E") for t in targs) + "E"
     out = {}
     for key, pat in (("timed", "r[0-9][0-9]_kernel_stats.csv"), ("isolated", "r[0-9][0-9]_kernel_stats_1stream.csv")):
         files = sorted(glob.glob(os.path.join(REPO, "profiles", pat)))
@@ -646,7 +666,9 @@ def main():
             zp = G.get_option("tap_partials") if a.dtype == "bf16" else 0
             per_launch_min, n_part, zpm = aad_v4_min_bytes(B, ca8, nl, a.num_blocks, zp)
             v5 = G.kernel_variant("aad_dual_256") == "v5"
-            kname = (f"aad_v5_kernel<{ca8}, {nl}, true, {zpm}>" if v5 else f"aad_v4_kernel<{ca8}, {nl}, true, true, {zpm}>")
+            # the launched instantiation (aad_v3.hip aad_v3_t): v5 <T, Ca, L, RELU, ZPM, ASMW = ZPM != 0>
+            kname = (f"aad_v5_kernel<__bf16, {ca8}, {nl}, true, {zpm}, {'true' if zpm else 'false'}>" if v5
+                     else f"aad_v4_kernel<{ca8}, {nl}, true, true, {zpm}>")
             # the kernel's own execution span (first workgroup start -> last wave end, its wall-clock stamps),
             # live in the timed region; the event bracket only if the clock recorded nothing
             clocked = clk_n > 0

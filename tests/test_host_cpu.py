@@ -182,3 +182,12 @@ def test_bench_roofline_bytes_follow_the_stored_outputs():
     assert bench.aad_v4_min_bytes(64, 64, 2, 2, 1)[1:] == (0, 0)          # mode 1: partials in the later layer
     assert bench.aad_v4_min_bytes(64, 32, 2, 1, 2)[1:] == (2, 3)          # nb = 1: both layers feed the RGB conv
     assert bench.aad_v4_min_bytes(64, 32, 2, 1, 1)[1:] == (1, 1)
+
+
+def test_bench_profile_lookups_match_the_launched_symbol():
+    """bench.py finds the roofline kernel's rows in the committed rocprof / PMC summaries by its Itanium
+    symbol (the launched instantiation carries the storage type and the ASMW flag)."""
+    import bench
+    assert bench.mangle("aad_v5_kernel<__bf16, 64, 2, true, 2, true>") == "aad_v5_kernelIDF16bLi64ELi2ELb1ELi2ELb1EE"
+    assert bench.mangle("aad_v4_kernel<64, 2, true, true, 2>") == "aad_v4_kernelILi64ELi2ELb1ELb1ELi2EE"
+    assert bench.mangle("k<_Float16, false>") == "kIDF16_Lb0EE"
