@@ -12,14 +12,17 @@ value = N*B*K / max-over-ranks wall time of the K timed steps.  ``--identities 4
 rows).
 
 Besides the JSON line's throughput, rank 0 at N = 1 reports
-* roofline: the dominant AAD kernel, aad_v4_kernel<64,2,true> (the two AADLayers of AADBlk8 that read
-  the same h_in / z_attr at 256x256, h_in sampled through the bilinear x2 upsample of AADBlk7's
-  128x128 output), HBM-bound.  ``achieved`` = the bytes that fused kernel must move at minimum (the
-  128x128 source of h_in once, z_attr8 once, the two 256x256 outputs: 2.147 GB at B = 64) / its
-  average launch time, timed with HIP events recorded on the launch stream around each of its
-  launches inside the timed region; ``traffic`` = its PMC-measured HBM bytes per launch
-  (the newest profiles/rNN_traffic.json); ``formula_frac`` keeps SURVEY.md §8d's per-layer formula
-  (|h_in|+|z_attr|+|out| per AADLayer, 3.22 GB), which counts bytes the fused kernel never moves;
+* roofline: the dominant AAD kernel, aad_v5_kernel<__bf16,64,2,true,2,true> (the two AADLayers of AADBlk8
+  that read the same h_in / z_attr at 256x256, h_in sampled through the bilinear x2 upsample of AADBlk7's
+  128x128 output; one of them writes the 3x3 RGB conv's tap partials), HBM-bound.  ``achieved`` = the bytes
+  that fused kernel must move at minimum (the 128x128 source of h_in once, z_attr8 once, its outputs as
+  stored: 1.476 GB at B = 64) / its average launch duration in the timed configuration — the committed
+  rocprofv3 trace row of that symbol (profiles/rNN_kernel_stats.csv, tools/profile_round.sh runs this same
+  command under rocprofv3), with the live in-kernel clock of the timed region beside it (live_clock_us);
+  ``traffic`` = its PMC-measured HBM bytes per launch (profiles/rNN_traffic.json); ``fractions`` gives the
+  minimum-bytes, physical (PMC) and SURVEY.md §8d per-layer-formula (|h_in|+|z_attr|+|out| per AADLayer,
+  3.22 GB: bytes the fused kernel never moves) fractions side by side; ``isolated`` the same kernel one
+  batch at a time (live clock and the one-stream trace row);
 * roofline_conv3x3 (MFMA-bound, all generator 3x3 convs) and aad_decoder_gbs (SURVEY.md §8d
   definition: AADLayer bytes / total AAD kernel time);
 * legs: the D2H-inclusive config 2 (pinned host output, copy overlapped with the next batch), config 5
@@ -669,13 +672,21 @@ def main():
             # the launched instantiation (aad_v3.hip aad_v3_t): v5 <T, Ca, L, RELU, ZPM, ASMW = ZPM != 0>
             kname = (f"aad_v5_kernel<__bf16, {ca8}, {nl}, true, {zpm}, {'true' if zpm else 'false'}>" if v5
                      else f"aad_v4_kernel<{ca8}, {nl}, true, true, {zpm}>")
-            # the kernel's own execution span (first workgroup start -> last wave end, its wall-clock stamps),
-            # live in the timed region; the event bracket only if the clock recorded nothing
+            # duration per launch: the committed rocprofv3 --kernel-trace --stats average of this exact symbol in the
+            # timed configuration (profiles/rNN_kernel_stats.csv, written by tools/profile_round.sh from this bench
+            # command) when the summary has its row — so every fraction below can be recomputed from profiles/ —
+            # else the kernel's own live execution span (in-kernel clock: first workgroup start -> last wave end);
+            # the live clock is always reported beside it (live_clock_us) with its ratio to the rocprof row
             clocked = clk_n > 0
-            per_launch_s = clk_us / clk_n / 1e6 if clocked else ev_s
-            ach = per_launch_min / per_launch_s / 1e9
+            live_s = clk_us / clk_n / 1e6 if clocked else ev_s
             tr = pmc_traffic(kname)
             rp = rocprof_avg_us(kname)
+            use_rp = bool(rp and rp.get("timed_avg_us"))
+            per_launch_s = rp["timed_avg_us"] / 1e6 if use_rp else live_s
+            ach = per_launch_min / per_launch_s / 1e9
+
+            def fr(nbytes, t):
+                return round(nbytes / t / 1e9 / HBM_PEAK_GBS, 4)
             res["roofline"] = {
                 "kernel": f"{kname}: AADBlk8's block-input AAD kernel at 256x256, {nl} AADLayer(s) sharing h_in/"
                           "z_attr, h_in = bilinear x2 of the 128x128 block output sampled in-kernel (IN-normalise, "
@@ -684,18 +695,20 @@ def main():
                 "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4),
                 "traffic": tr["bytes_per_launch"] if tr else None,
-                "avg_launch_us": round(per_launch_s * 1e6, 2), "launches_timed": clk_n if clocked else c["launches"],
-                "duration_source": ("in-kernel wall clock (earliest workgroup start to latest wave end, "
-                                    "s_memrealtime stamps) of every launch in the timed region" if clocked else
+                "avg_launch_us": round(per_launch_s * 1e6, 2),
+                "duration_source": (f"rocprofv3 kernel-trace average of this symbol in the timed configuration "
+                                    f"({rp['timed_source']}, {rp['timed_calls']} calls)" if use_rp else
+                                    "in-kernel wall clock (earliest workgroup start to latest wave end, s_memrealtime "
+                                    "stamps) of every launch in the timed region" if clocked else
                                     "HIP events on the launch stream around each launch in the timed region"),
+                "live_clock_us": round(live_s * 1e6, 2), "launches_timed": clk_n if clocked else c["launches"],
                 "bytes_per_launch": per_launch_min,
                 "bytes_note": "achieved = minimum bytes of the fused kernel (128x128 h_in source + z_attr8 + outputs "
                               "as stored: 64 bf16 channels, or 32 fp16 tap partials per pixel) / launch duration",
                 "fractions": {
-                    "minimum_bytes": round(ach / HBM_PEAK_GBS, 4),
-                    "physical_pmc": (round(tr["bytes_per_launch"] / per_launch_s / 1e9 / HBM_PEAK_GBS, 4)
-                                     if tr else None),
-                    "survey_8d_formula": round(per_launch_formula / per_launch_s / 1e9 / HBM_PEAK_GBS, 4),
+                    "minimum_bytes": fr(per_launch_min, per_launch_s),
+                    "physical_pmc": fr(tr["bytes_per_launch"], per_launch_s) if tr else None,
+                    "survey_8d_formula": fr(per_launch_formula, per_launch_s),
                     "formula_bytes_per_launch": per_launch_formula,
                     "pmc_source": tr["source"] if tr else None},
                 "timed_region_latency": {
@@ -706,20 +719,26 @@ def main():
             }
             if tr:
                 res["roofline"]["traffic_detail"] = tr
-            if rp and rp.get("timed_avg_us"):
-                res["roofline"]["rocprof_agreement"] = round(per_launch_s * 1e6 / rp["timed_avg_us"], 3)
+            if use_rp:
+                res["roofline"]["live_clock_vs_rocprof"] = round(live_s * 1e6 / rp["timed_avg_us"], 3)
             if iso.get("launches"):
-                # the same kernel with one batch on the GPU (untimed pass)
+                # the same kernel with one batch on the GPU (untimed pass): live in-kernel clock, and the
+                # one-stream trace row (profiles/rNN_kernel_stats_1stream.csv) beside it
                 iso_us, iso_n = clock["isolated"]
                 iso_s = iso_us / iso_n / 1e6 if iso_n else iso["ms"] / iso["launches"] / 1e3
+                rp_iso = rp.get("isolated_avg_us") if rp else None
                 res["roofline"]["isolated"] = {
                     "avg_launch_us": round(iso_s * 1e6, 2), "achieved": round(per_launch_min / iso_s / 1e9, 1),
-                    "frac": round(per_launch_min / iso_s / 1e9 / HBM_PEAK_GBS, 4),
-                    "formula_frac": round(per_launch_formula / iso_s / 1e9 / HBM_PEAK_GBS, 4),
-                    "physical_frac": (round(tr["bytes_per_launch"] / iso_s / 1e9 / HBM_PEAK_GBS, 4) if tr else None),
+                    "frac": fr(per_launch_min, iso_s),
+                    "formula_frac": fr(per_launch_formula, iso_s),
+                    "physical_frac": fr(tr["bytes_per_launch"], iso_s) if tr else None,
                     "event_avg_launch_us": round(iso["ms"] / iso["launches"] * 1e3, 2),
                     "launches": iso["launches"],
-                    "note": "one batch at a time (untimed pass); rocprof.isolated_avg_us is the one-stream trace row"}
+                    "rocprof_avg_us": rp_iso,
+                    "rocprof_frac": fr(per_launch_min, rp_iso / 1e6) if rp_iso else None,
+                    "live_vs_rocprof": round(iso_s * 1e6 / rp_iso, 3) if rp_iso else None,
+                    "note": "one batch at a time (untimed pass, in-kernel clock); rocprof_avg_us is the one-stream "
+                            "trace row (rocprof.isolated_source)"}
             cc = classes["conv3x3_all"]
             if cc["launches"]:
                 tf = cc["flops"] / (cc["ms"] / 1e3) / 1e12

@@ -850,11 +850,18 @@ int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream
   if (d.kind == CONV_FWD && (d.kh * d.kw > 64 || d.kh < 1 || d.kw < 1 || d.stride < 1)) return -1;   // 64-bit tap masks
   if (d.epi == EPI_AAD && (d.C_aad % 16 != 0 || d.N != 2 * d.C_aad || !d.hin || !d.stat || !d.idgb || !d.mask || !d.shift))
     return -1;
+#ifdef GHOST_TUNING
+  // plan listing for profiling (tuning builds only): one line per conv launch with its shape
+  static const int trace = GHOST_KNOB("GHOST_CONV_TRACE", 0);
+  if (trace)
+    fprintf(stderr, "[conv] kind=%d B=%d %dx%d Cin=%d N=%d k=%dx%d s=%d halo=%d\n", (int)d.kind, d.B, d.Hi, d.Wi, d.Cin,
+            d.N, d.kh, d.kw, d.stride, (int)conv3x3_halo_supported(d));
+#endif
   if (conv3x3_halo_supported(d)) return conv3x3_halo(d, stream);
   if (conv_first_supported(d)) return conv_first(d, ws, ws_bytes, stream);
   if (conv_stem3x3_supported(d)) return conv_stem3x3(d, stream);
   if (convT_halo_supported(d)) return convT_halo(d, stream);
-  if (conv4x4s2_patch_supported(d)) return conv4x4s2_patch(d, stream);
+  if (conv4x4s2_patch_supported(d) || conv3x3s2_patch_supported(d)) return conv_s2_patch(d, stream);
   Plan p = make_plan(d);
   if (p.NT > d.Npad) return -1;  // weight rows read by the last tile must exist
   const int K = d.kind == CONV_T4S2 ? 4 * d.Cin : d.kh * d.kw * d.Cin;

@@ -196,6 +196,12 @@ def test_conv4x4s2_patch_kernel(lib, cin, cout, H, B, xoff, yoff, bn):
     (512, 512, 512, 3, 1, 1, 7, "res_y2"),    # 7x7 stays on the implicit GEMM
     (3, 4, 64, 3, 1, 1, 112, "prelu_y2"),     # ArcFace stem (bf16: the 4-channel MFMA stem kernel)
     (3, 4, 64, 3, 1, 1, 9, "prelu_y2"),       # stem with a partial last 64-pixel chunk (B*81 = 162)
+    # 3x3/s2 on the LDS input-patch kernel in bf16 (conv_s2.hip, 8 x 16 output tiles overhanging 56/28/14)
+    (64, 64, 64, 3, 2, 1, 112, "res_y2"),     # layer1 block-0 conv2 112 -> 56
+    (128, 128, 128, 3, 2, 1, 56, "res_y2"),   # layer2 block-0 conv2 56 -> 28
+    (256, 256, 256, 3, 2, 1, 28, "res_y2"),   # layer3 block-0 conv2 28 -> 14
+    (64, 96, 64, 3, 2, 1, 32, "prelu_y2"),    # exact tiles, PReLU, padded input channels
+    (64, 64, 64, 3, 2, 1, 34, "relu"),        # 17 x 17 output: too much overhang, the implicit GEMM
 ])
 def test_conv2d_ex_epilogues(lib, dt, cin, ldx, cout, k, s, p, H, mode):
     """ghost_conv2d_ex_nhwc: residual-before-activation, per-channel PReLU and the dual output."""
