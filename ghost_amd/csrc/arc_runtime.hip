@@ -247,7 +247,16 @@ __global__ void __launch_bounds__(256) u8_max_kernel(const uint8_t* __restrict__
     const int t = __shfl_xor(m, o, 64);
     m = t > m ? t : m;
   }
-  if ((threadIdx.x & 63) == 0 && m > 0) atomicMax(out, m);
+  // one atomic per workgroup at most: same-address atomics serialise in one L2 channel (one per wave cost
+  // ~50 us at B = 128, 4096 of them), and the reader only asks max > 1, so a workgroup whose max is <= 1, or
+  // that already sees the flag above 1, adds nothing
+  __shared__ int wmax[4];
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+    if (m > 1 && __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= 1) atomicMax(out, m);
+  }
 }
 
 template <typename T>
