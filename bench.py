@@ -359,7 +359,8 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
          warp + mask composite on the device (blend.blend_swaps) from the device-resident swaps, D2H of
          the blended frames; copies on their own streams overlap the previous chunk's blend.
     The swap is resized 256 -> 224 as the reference does (cv2.resize INTER_LINEAR, on the device) before
-    the warp; landmarks / mask construction / the video writer stay on the host."""
+    the warp; the masks (face_mask_static: hull fill, erode, border fade, Gaussian blur) are built on the
+    device from per-frame landmarks; landmark detection and the video writer stay on the host."""
     from ghost_amd.inference.blend import blend_swaps
     from ghost_amd.inference.core import swap_identity_frames
     rng = np.random.Generator(np.random.PCG64(9))
@@ -379,9 +380,17 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
     mats[:, 1, 0], mats[:, 1, 1] = sc * np.sin(ang), sc * np.cos(ang)
     mats[:, 0, 2] = -(mats[:, 0, 0] * tx + mats[:, 0, 1] * ty)
     mats[:, 1, 2] = -(mats[:, 1, 0] * tx + mats[:, 1, 1] * ty)
-    yy, xx = np.mgrid[0:224, 0:224]
-    mask = np.clip(1.0 - (((yy - 112) / 96.0) ** 2 + ((xx - 112) / 83.0) ** 2), 0, 1).astype(np.float32)
-    masks_d = torch.from_numpy(np.broadcast_to(mask, (n_frames, 224, 224)).copy()).to(dev)
+    # 106 landmarks per frame as the landmark model would return them on the 224 x 224 swap (synthetic: a jaw /
+    # forehead contour + interior points, jittered per frame); face_mask_static's params from the first frame,
+    # reused for the identity's later frames (video_processing.py:219-223)
+    from ghost_amd.inference.masks import face_masks, mask_params
+    t_ = np.linspace(0.15 * np.pi, 0.85 * np.pi, 33) + np.pi
+    base = np.concatenate([np.stack([112 + 78 * np.cos(-t_), 118 + 92 * np.sin(-t_)], 1),
+                           np.stack([112 + rng.uniform(-60, 60, 73), 118 + rng.uniform(-70, 60, 73)], 1)])
+    lms = (base[None] + rng.normal(0, 1.5, (n_frames, 106, 2))).astype(np.float32)
+    lm_tgt = (base + rng.normal(0, 1.5, (106, 2))).astype(np.float32)
+    params = np.tile(np.array(mask_params(lms[0], lm_tgt), np.int32), (n_frames, 1))
+    masks_d = torch.empty(n_frames, 224, 224, dtype=torch.float32, device=dev)
     mats_d = torch.from_numpy(mats).to(dev)
     valid_d = torch.from_numpy(present.astype(np.int32)).to(dev)
     z = identity_rows(1, dev)
@@ -391,6 +400,7 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
     cur = torch.cuda.current_stream(dev)
 
     def run():
+        face_masks(lms, params, 224, 224, dev, out=masks_d)      # face_mask_static for every frame, on the GPU
         final, swaps_d = swap_identity_frames(crops, present, z, G, BS=BS, device=dev, return_device=True)
         # frame-indexed device swaps (faceless frames: a zero row, masked off by valid)
         idx = torch.from_numpy(np.maximum(np.cumsum(present) - 1, 0)).to(dev)
@@ -427,8 +437,8 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
     assert len(final) == n_frames and sum(1 for f in final if len(f)) == n_face
     return {"workload": f"config 3: {n_frames}-frame {W}x{H} video, 1 identity, {n_face} frames with a face; "
                         f"crops H2D -> swaps (BS={BS}, per-batch D2H) -> present re-insertion -> frames H2D -> "
-                        "device resize 256->224 + paste-back -> frames D2H (host detect/align/landmarks/mask/writer "
-                        "excluded)",
+                        "device face masks (face_mask_static from per-frame landmarks) + resize 256->224 + "
+                        "paste-back -> frames D2H (host detection/alignment/landmark model/writer excluded)",
             "frames_per_s": round(n_frames / el, 1), "seconds": round(el, 3),
             "host_bytes_moved": int(n_face * 196608 * 2 + 2 * n_frames * H * W * 3)}
 

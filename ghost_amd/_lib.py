@@ -62,6 +62,9 @@ _SIGS = {
     "ghost_blend_swaps_u8": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, i32, vp, i64, vp, vp, vp]),
     "ghost_resize_u8_linear": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, i32, vp]),
     "ghost_blend_image_u8": (i32, [vp, i32, i32, vp, i64, i32, i32, vp, i64, vp, vp]),
+    "ghost_mask_polygons": (i32, [vp, i32, i32, vp, vp, vp]),
+    "ghost_face_masks_workspace_bytes": (i64, [i32, i32, i32]),
+    "ghost_face_masks": (i32, [vp, vp, vp, i32, i32, i32, vp, i64, vp, i64, vp]),
     "ghost_conv2d_ex_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
                                    i32, vp, i64, vp]),
     "ghost_conv_transpose4x4s2_nhwc": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, vp, vp, f32, vp,

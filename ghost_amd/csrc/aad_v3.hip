@@ -950,7 +950,10 @@ static int v3_ppw(int HW, int C) { return (HW >= 65536 || C == 256) ? 1024 : 512
 // the v5 kernel's work items per workgroup if it takes this launch, else 0
 static int v5_takes(const AadV3Desc& d, int zpm) {
   static const int use_v5 = GHOST_KNOB("GHOST_AAD_V5", 1);
-  static const int ipw = GHOST_KNOB("GHOST_V5_IPW", 1);
+  // two 1024-pixel work items per workgroup (one prologue — statistics tables, weight rows — per 2048 pixels):
+  // measured B = 64 unet/2, same box: 384.8 -> 377.8 us one batch at a time, 11 084-11 172 -> 11 272 frames/s
+  // with two in flight (profiles/r03_ab_v5.txt; XCD-contiguous order neutral, the compiler-opaque DMA 3 % faster)
+  static const int ipw = GHOST_KNOB("GHOST_V5_IPW", 2);
   const bool up = d.up_H > 0;
   // OW / 8 column tiles must divide the 64 tiles of a 1024-pixel work item (OW in {64 .. 512}) and the
   // work items of an image must cover its H row tiles, IPW at a time

@@ -257,6 +257,18 @@ int ghost_resize_u8_linear(const uint8_t* src, int64_t src_stride, int F, int Hs
 int ghost_blend_image_u8(uint8_t* frame, int H, int W, const uint8_t* swaps, int64_t swap_stride, int J, int S,
                          const float* masks, int64_t mask_stride, const double* maps, void* stream);
 
+/* ---- face masks (face_mask_static, utils/inference/masks.py:38-107) ----
+ * Host, CPU only (no device pointers): for F frames of 106 float32 landmarks [F][106][2] and their
+ * (erode, sigmaX, sigmaY) params [F][3] (face_mask_static's, masks.py:43-65), expand_eyebrows on the int32
+ * landmarks (masks.py:5-20) and the convex hull (masks.py:31): poly [F][128][2] int32 vertices, nv[F] counts. */
+int ghost_mask_polygons(const float* landmarks, int F, int npts, const int32_t* params, int32_t* poly, int32_t* nv);
+/* Device: poly / nv / params as above (device copies) -> masks [F][H][W] f32 (frame f at f*mask_stride floats):
+ * cv2.fillConvexPoly(255), cv2.erode / dilate with the k x k box, the 2*sigmaY border fade, cv2.GaussianBlur
+ * (0, 0, sigmaX, sigmaY), / 255.  H*W <= 57344, H <= 256; ws >= ghost_face_masks_workspace_bytes(F, H, W). */
+int64_t ghost_face_masks_workspace_bytes(int F, int H, int W);
+int ghost_face_masks(const int32_t* poly, const int32_t* nv, const int32_t* params, int F, int H, int W, float* masks,
+                     int64_t mask_stride, void* ws, int64_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
