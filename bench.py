@@ -72,7 +72,8 @@ def parse():
     ap.add_argument("--video", type=int, default=900, help="frames of the config-3 video leg")
     ap.add_argument("--cpu-batches", default="1,64", help="CPU baseline batch sizes ('' = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
-    ap.add_argument("--arc-batch", type=int, default=128, help="faces per ArcFace embedding batch in its leg")
+    ap.add_argument("--arc-batch", default="256,128",
+                    help="faces per ArcFace embedding launch in its leg (comma list; the first is the leg's headline)")
     ap.add_argument("--streams", type=int, default=2,
                     help="batches in flight on the GPU (dp.GatherPipeline streams; 1 = one batch at a time)")
     ap.add_argument("--opt", action="append", default=[],
@@ -777,9 +778,13 @@ def main():
             res["legs"]["config5"] = config5_leg(dev, B, a.steps, 3, nstreams=pipe.nstreams)
         if "latency" in legs:
             res["legs"]["config1_latency"] = latency_leg(dev)
-        if "arcface" in legs and a.arc_batch > 0:
+        arc_batches = [int(b) for b in str(a.arc_batch).split(",") if b]
+        if "arcface" in legs and arc_batches:
             # one batch at a time: two in flight measured neutral (the persistent 3x3 convs hold every CU)
-            res["legs"]["arcface"] = arcface_leg(dev, a.arc_batch, max(3, a.steps // 2), 1)
+            runs = [arcface_leg(dev, n, max(3, a.steps // 2), 1) for n in arc_batches]
+            res["legs"]["arcface"] = dict(runs[0])
+            res["legs"]["arcface"]["by_batch"] = {str(r["batch"]): {k: r[k] for k in ("ms_per_batch", "embeddings_per_s",
+                                                                                     "mfma_frac")} for r in runs}
         batches = [int(b) for b in a.cpu_batches.split(",") if b]
         if world == 1 and batches:
             res["cpu_baseline"] = cpu_baseline(a.backbone, a.num_blocks, batches)
