@@ -627,8 +627,12 @@ Plan make_plan(const ConvDesc& d) {
   // (only grids that need split-K: with >= 256 tiles of 128 x 128 the two-workgroup register-staged
   // kernel measured faster, e.g. the 8x8 AAD GEMM 55 vs 74 us)
   const long tiles128 = (long)((p.M + 127) / 128) * ((d.N + 127) / 128) * p.npar;
-  if (deep > 0 && bf && p.fast && d.to == d.ti && p.M <= 8192 && d.N >= 256 && d.Kpad >= 1024 &&
-      d.N % 128 == 0 && tiles128 < 256) {
+  // very deep K (>= 4096: IResNet's 7 x 7 512 -> 512 convs) keeps the ring up to two rounds of workgroups:
+  // at B = 256 (M = 12 544, 392 tiles) 175 -> 167 us per conv against the register-staged 64 x 128 tile (the
+  // second, partial round of 136 tiles costs what the ring saves; at B = 128 the ring with split-K: 63 us)
+  const bool deep_k = p.M <= 16384 && d.Kpad >= 4096 && tiles128 < 512;
+  if (deep > 0 && bf && p.fast && d.to == d.ti && d.N >= 256 && d.Kpad >= 1024 && d.N % 128 == 0 &&
+      ((p.M <= 8192 && tiles128 < 256) || deep_k)) {
     p.BM = 128; p.BN = 128; p.BK = 32; p.stages = deep;
   }
 #ifdef GHOST_TUNING

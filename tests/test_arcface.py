@@ -156,16 +156,17 @@ def _stage_close(g, r, what):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("arch,B", [("iresnet18", 2), ("iresnet100", 2), ("iresnet100", 128)])
+@pytest.mark.parametrize("arch,B", [("iresnet18", 2), ("iresnet100", 2), ("iresnet100", 128), ("iresnet100", 256)])
 def test_bf16_each_stage_matches_storage_emulation(arch, B):
     """Bisection by construction: each stage from the GPU's own stored inputs (ghost_arc_set_taps).  B = 128
-    runs the two-sample halo window (HaloPair) at 56x56 / 28x28 / 14x14; two of its rows are checked."""
+    runs the two-sample halo window (HaloPair) at 56x56 / 28x28 / 14x14, B = 256 also the deep LDS-DMA ring at
+    7x7 (M = 12 544); two rows of each are checked."""
     m = net(arch, compute_dtype=torch.bfloat16)
     layers, p = A.LAYERS[arch], weights(arch)
     x = torch.from_numpy(np.random.Generator(np.random.PCG64(6)).uniform(-1, 1, (B, 3, 112, 112)).astype(np.float32))
     emb, taps = m.forward_taps(x.to(DEV))
     torch.cuda.synchronize()
-    rows = torch.tensor([0, 1] if B == 2 else [0, 77])
+    rows = torch.tensor([0, 1] if B == 2 else [0, 77] if B == 128 else [0, 201])
     x = x[rows]
     emb = emb[rows.to(DEV)].cpu()
     assert emb.dtype == torch.float32 and taps[0][0].dtype == torch.bfloat16

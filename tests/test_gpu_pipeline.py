@@ -203,7 +203,7 @@ def test_gather_pipeline_two_batches_in_flight(lib):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("dt,B", [(None, 1), (torch.bfloat16, 1), (torch.bfloat16, 4)])
+@pytest.mark.parametrize("dt,B", [(None, 1), (torch.bfloat16, 1), (torch.bfloat16, 4), (torch.float16, 2)])
 def test_graphed_swap_is_bit_identical(lib, dt, B):
     """GraphedSwap (one HIP graph replay of the whole native plan, two-stream plan included) gives the
     bytes of an eager swap_u8, for new inputs copied into the captured buffers on every call."""
