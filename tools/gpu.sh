@@ -49,14 +49,16 @@ for step in "$@"; do
       IFS=';' read -ra specs <<< "${step#knobs:}"
       for v in "${specs[@]}"; do
         for st in 1 2; do
-          eval env GHOST_TUNING=1 $v timeout -k 10 200 python -u bench.py $Q --streams $st $BENCH_ARGS > /tmp/o.log 2>&1; must $?
+          eval env GHOST_TUNING=1 $v timeout -k 10 200 python -u bench.py $Q --streams $st $BENCH_ARGS > /tmp/o.log 2>&1
+          rc=$?; [ $rc -eq 0 ] || cp /tmp/o.log gpurun_out/knobs_fail.log; must $rc
           last /tmp/o.log "$v streams=$st" >> gpurun_out/ab_knobs.txt
         done
       done ;;
     streams:*)
       IFS=',' read -ra ns <<< "${step#streams:}"
       for st in "${ns[@]}"; do
-        eval timeout -k 10 200 python -u bench.py $Q --streams $st --steps 40 $BENCH_ARGS > /tmp/o.log 2>&1; must $?
+        eval timeout -k 10 200 python -u bench.py $Q --streams $st --steps 40 $BENCH_ARGS > /tmp/o.log 2>&1
+        rc=$?; [ $rc -eq 0 ] || cp /tmp/o.log gpurun_out/streams_fail.log; must $rc
         last /tmp/o.log "streams=$st" >> gpurun_out/ab_streams.txt
       done ;;
     arc:*)
