@@ -400,8 +400,20 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
     s_in, s_out = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     cur = torch.cuda.current_stream(dev)
 
+    ev_times = {"masks": [], "blend": []}
+
+    def bracket(kind):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev_times[kind].append((e0, e1))
+        return e0, e1
+
     def run():
+        for v in ev_times.values():
+            v.clear()
+        e0, e1 = bracket("masks")
+        e0.record(cur)
         face_masks(lms, params, 224, 224, dev, out=masks_d)      # face_mask_static for every frame, on the GPU
+        e1.record(cur)
         final, swaps_d = swap_identity_frames(crops, present, z, G, BS=BS, device=dev, return_device=True)
         # frame-indexed device swaps (faceless frames: a zero row, masked off by valid)
         idx = torch.from_numpy(np.maximum(np.cumsum(present) - 1, 0)).to(dev)
@@ -417,7 +429,10 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
                 loaded = torch.cuda.Event()
                 loaded.record(s_in)
             cur.wait_event(loaded)
+            e0, e1 = bracket("blend")
+            e0.record(cur)
             blend_swaps(b[:f1 - f0], swaps_f[f0:f1], masks_d[f0:f1], mats_d[f0:f1], valid_d[f0:f1], resize_to=224)
+            e1.record(cur)
             blended = torch.cuda.Event()
             blended.record(cur)
             with torch.cuda.stream(s_out):
@@ -441,7 +456,10 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
                         "device face masks (face_mask_static from per-frame landmarks) + resize 256->224 + "
                         "paste-back -> frames D2H (host detection/alignment/landmark model/writer excluded)",
             "frames_per_s": round(n_frames / el, 1), "seconds": round(el, 3),
-            "host_bytes_moved": int(n_face * 196608 * 2 + 2 * n_frames * H * W * 3)}
+            "host_bytes_moved": int(n_face * 196608 * 2 + 2 * n_frames * H * W * 3),
+            # device time of the paste-back pieces (HIP events on the compute stream, recorded after the wait for each
+            # chunk's H2D copy; the blend brackets include the 256 -> 224 resize)
+            "device_ms": {k: round(sum(a.elapsed_time(b) for a, b in v), 3) for k, v in ev_times.items()}}
 
 
 def latency_leg(dev, n=20):
