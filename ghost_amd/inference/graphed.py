@@ -38,7 +38,10 @@ class GraphedSwap:
         cur.wait_stream(side)
         torch.cuda.synchronize(dev)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # a capture stream of its own: the module's workspace cache is keyed by stream, so the captured workspace
+        # (allocated in the graph's private pool) is never handed to an eager call or to another GraphedSwap
+        self._capture_stream = torch.cuda.Stream(dev)
+        with torch.cuda.graph(self.graph, stream=self._capture_stream):
             G.swap_u8(self.crops, self.z, out=self.out)
         torch.cuda.synchronize(dev)
 
