@@ -944,8 +944,15 @@ static bool v5_pairing_ok(const Up2xSrc& u) {
   return true;
 }
 
-// pixels per workgroup: one sample's block; C = 256 stages its weights once per 1024 pixels
-static int v3_ppw(int HW, int C) { return (HW >= 65536 || C == 256) ? 1024 : 512; }
+// pixels per workgroup: one sample's block; C = 256 stages its weights once per 1024 pixels, and so may the
+// C = 128 layers (128 x 128 stage: GHOST_V3_PPW128, A/B knob)
+static int v3_ppw(int HW, int C) {
+  if (C == 128) {
+    static const int p128 = GHOST_KNOB("GHOST_V3_PPW128", 512);
+    if ((p128 == 1024 || p128 == 2048) && HW % p128 == 0) return p128;
+  }
+  return (HW >= 65536 || C == 256) ? 1024 : 512;
+}
 
 // the v5 kernel's work items per workgroup if it takes this launch, else 0
 static int v5_takes(const AadV3Desc& d, int zpm) {
