@@ -84,7 +84,8 @@ def run(backbone, nb, B=64, rows=ROWS, st="bf16"):
     r = {"p": pe, "z": zr, "xt": xr, "Y": Y[ri].float().cpu(), "u8": u8[ri].cpu().numpy(),
          "attr": [a[ri].float().cpu() for a in attr], "blocks": [b[ri].float().cpu() for b in blocks]}
     r["emu"] = aei_ref.aei_forward_bf16_storage(pe, r["xt"], r["z"], backbone, nb, store=STORE[st])
-    r["fp32"] = aei_ref.aei_forward(p, r["xt"], r["z"], backbone, nb)[0]
+    r["fp32"], a32 = aei_ref.aei_forward(p, r["xt"], r["z"], backbone, nb)
+    r["fp32_attr"] = [a.float() for a in a32]
     _CACHE[key] = r
     return r
 
@@ -116,11 +117,30 @@ def check_blocks(r, backbone, nb, st="bf16"):
 @pytest.mark.parametrize("st", ["bf16", "fp16"])
 @pytest.mark.parametrize("backbone,nb", CASES)
 def test_encoder_maps_match_emulation(backbone, nb, st):
+    """The attribute encoder's eight maps (unet / linknet: conv4x4 + deconv4x4 chains) against the storage
+    emulation."""
     r = run(backbone, nb, st=st)
     for i, (g, e) in enumerate(zip(r["attr"], r["emu"][1]), 1):
         d = (g - e).abs()
         assert float(d.max()) <= 2 * ulp(float(e.abs().max()), st), (i, float(d.max()))
         assert float(d.mean()) <= 2e-3 * float(e.abs().mean()), (i, float(d.mean()))
+
+
+@pytest.mark.parametrize("st", ["bf16", "fp16"])
+def test_resnet_encoder_maps_within_storage_error(st):
+    """MLAttrEncoderResnet (resnet.py:81-149): its deepest map z_attr1 sits behind two 7x7 convs and 12 Bottlenecks
+    (36 convs, 12 residual adds), so a summation-order flip early in the chain reaches the maps a few ulps wide
+    (measured: outside the 2-ulp gate the conv4x4 chains pass): its maps are
+    gated end to end like Y — per map, the GPU's error against the fp32 oracle within 1.25x (mean) / 1.3x (top
+    0.5 %) of the emulated 16-bit arithmetic's own error."""
+    r = run("resnet", 2, 4, list(range(4)), st=st)
+    for i, (g, e, f) in enumerate(zip(r["attr"], r["emu"][1], r["fp32_attr"]), 1):
+        dg, de = (g - f).abs().flatten(), (e.float() - f).abs().flatten()
+        tol = ulp(float(f.abs().max()), st) / 64
+        assert float(dg.mean()) <= 1.25 * float(de.mean()) + tol, (i, float(dg.mean()), float(de.mean()))
+        k = max(1, dg.numel() // 200)
+        tg, te = float(dg.topk(k).values.mean()), float(de.topk(k).values.mean())
+        assert tg <= 1.3 * te + tol, (i, tg, te)
 
 
 @pytest.mark.parametrize("st", ["bf16", "fp16"])
@@ -131,7 +151,8 @@ def test_each_decoder_block_matches_emulation(backbone, nb, st):
 
 
 @pytest.mark.parametrize("st", ["bf16", "fp16"])
-@pytest.mark.parametrize("backbone,nb,B", [("unet", 2, 1), ("linknet", 3, 2), ("unet", 1, 4), ("unet", 3, 2)])
+@pytest.mark.parametrize("backbone,nb,B", [("unet", 2, 1), ("linknet", 3, 2), ("unet", 1, 4), ("unet", 3, 2),
+                                           ("resnet", 2, 4)])
 def test_small_batch_blocks_match_emulation(backbone, nb, B, st):
     """Small batches take other kernels (split-K GEMMs, the generic AAD path): same per-stage gates."""
     check_blocks(run(backbone, nb, B, list(range(B)), st=st), backbone, nb, st)
