@@ -66,9 +66,10 @@ def parse():
     ap.add_argument("--num-blocks", type=int, default=2)
     ap.add_argument("--identities", type=int, default=1, help="source identities mixed in every batch (config 5: 4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--legs", default="d2h,fp16,config5,video,latency,arcface",
-                    help="side measurements at N=1 (comma list of d2h, fp16, config5, video, latency, arcface; "
-                         "'' = none)")
+    ap.add_argument("--legs", default="config5_multi,d2h,fp16,config5,video,latency,arcface",
+                    help="side measurements (comma list of config5_multi (every N), d2h, fp16, config5, video, latency, "
+                         "arcface (N = 1 only); '' = none)")
+    ap.add_argument("--c5-frames", type=int, default=120, help="video frames per GPU of the config5_multi leg")
     ap.add_argument("--video", type=int, default=900, help="frames of the config-3 video leg")
     ap.add_argument("--cpu-batches", default="1,64", help="CPU baseline batch sizes ('' = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
@@ -122,6 +123,31 @@ def pmc_traffic(kname):
             return {"bytes_per_launch": k["hbm_bytes"], "read": k["read_bytes"], "write": k["write_bytes"],
                     "source": rel + " (" + data.get("source", "rocprofv3 --pmc") + ")"}
     return None
+
+
+def mfma_profile(match=None):
+    """The newest committed MFMA-utilisation summary (profiles/rNN_mfma.json, tools/pmc_mfma.sh: rocprofv3 --pmc
+    SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_MFMA / SQ_INSTS_VALU / GRBM_GUI_ACTIVE ... over this bench's one-stream
+    configuration and the ArcFace leg).  match: a kernel-name substring -> that kernel's rows only."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]_mfma.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+    except (OSError, ValueError):
+        return None
+    out = {"source": os.path.relpath(files[-1], REPO), "definition": d.get("definitions", {}).get("mfma_busy")}
+    for part in ("generator", "arcface"):
+        if part not in d:
+            continue
+        rows = d[part]["kernels"]
+        if match:
+            rows = [r for r in rows if match in r["kernel"]]
+        out[part] = {"totals": d[part]["totals"],
+                     "kernels": [{k: r.get(k) for k in ("kernel", "grid", "dispatches", "mfma_busy", "valu_per_mfma",
+                                                        "wait_frac", "eff_clock_ghz")} for r in rows[:12]]}
+    return out
 
 
 def rocprof_avg_us(kname):
@@ -349,6 +375,63 @@ def config5_leg(dev, B, steps, warmup, n_ident=4, nstreams=1):
                         f"num_blocks=3 bf16, u8 in -> u8 out, {ns} batch(es) in flight",
             "frames_per_s": round(B * steps / el, 1),
             "ms_per_batch": round(el * 1e3 / steps, 3)}
+
+
+def config5_multi_leg(dev, world, frames_per_gpu=120, n_ident=4, BS=64, reps=3, G=None, crop=224):
+    """BASELINE config 5 as one pipeline on every rank (N = 1..8): a synthetic video of frames_per_gpu * N frames
+    with n_ident target identities (each present in ~90 % of the frames), per identity its crop_frames (224x224
+    uint8 crops or []) and a source embedding; ``dp.model_inference_multi`` (core.py:56-88 over all identities at
+    once): resize_frames on the device, the identities' present crops as one sequence sharded contiguously over
+    the ranks, mixed-identity batches (per-sample embedding rows) with two in flight, each batch gathered to rank 0
+    (RCCL gather at N > 1), rank 0 assembling final_frames_list.  Timed: ``reps`` calls after one warm-up, each
+    bracketed by a barrier + device sync, max over ranks; output 'device' (rank 0 holds the swapped crops in HBM)
+    and 'host' (rank 0 also copies them to pinned host memory, overlapped per batch).  ``G`` / ``crop``: a stand-in
+    swap and 256-px crops for the gloo test of the N > 1 reporting (tests/test_dp_cpu.py)."""
+    from ghost_amd.inference.dp import model_inference_multi
+    own = G is None
+    if own:
+        G = make_model("linknet", 3, torch.bfloat16, dev)
+    nf = frames_per_gpu * world
+    rng = np.random.Generator(np.random.PCG64(55))
+    pool = rng.integers(0, 256, size=(48, crop, crop, 3), dtype=np.uint8)    # distinct crops, reused by reference
+    present = rng.random((n_ident, nf)) > 0.1
+    embeds = identity_rows(n_ident, torch.device("cpu"))
+    idents = []
+    for q in range(n_ident):
+        cf = [pool[(q * 7 + i) % len(pool)] if present[q, i] else [] for i in range(nf)]
+        idents.append((cf, embeds[q:q + 1]))
+    n_crops = int(present.sum())
+    out = {"workload": f"config 5 as one pipeline: {nf}-frame video ({frames_per_gpu} per GPU), {n_ident} identities, "
+                       f"{n_crops} face crops (224x224 crop_frames -> device resize_frames -> mixed-identity "
+                       f"linknet/3 bf16 batches of {BS}, two in flight, sharded over {world} GPU(s), gathered to "
+                       "rank 0 -> final_frames_list)", "crops": n_crops, "frames": nf}
+    for mode in ("device", "host"):
+        res = model_inference_multi(idents, G, BS=BS, device=dev, collect="rank0", output=mode)   # warm-up
+        del res
+        ts = []
+        for _ in range(reps):
+            if world > 1:
+                dist.barrier()
+            device_sync(dev)
+            t0 = time.perf_counter()
+            res = model_inference_multi(idents, G, BS=BS, device=dev, collect="rank0", output=mode)
+            device_sync(dev)
+            if world > 1:
+                dist.barrier()
+            ts.append(time.perf_counter() - t0)
+            if res is not None:
+                assert len(res) == n_ident and all(len(r) == nf for r in res)
+            del res
+        el = float(np.median(ts))
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        out[mode] = {"crops_per_s": round(n_crops / el, 1), "seconds": round(el, 4)}
+    if own:
+        del G
+        torch.cuda.empty_cache()
+    return out
 
 
 def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
@@ -680,6 +763,11 @@ def main():
         clock["isolated"] = G.profile_clock()
         G.profile(0)
 
+    # legs every rank runs (N >= 1): config 5 as one multi-identity pipeline, gathered to rank 0
+    multi_legs = {}
+    if "config5_multi" in [s for s in a.legs.split(",") if s] and a.c5_frames > 0:
+        pipe.drain()
+        multi_legs["config5_multi"] = config5_multi_leg(dev, world, a.c5_frames)
     if rank == 0:
         res = headline_record(world, B, a.steps, a.warmup, el, a.backbone, a.num_blocks, a.identities, a.dtype,
                               pipe.nstreams)
@@ -748,8 +836,16 @@ def main():
             }
             if tr:
                 res["roofline"]["traffic_detail"] = tr
+            # this run's own fraction (minimum bytes / the live in-kernel clock of the timed region), flagged when it
+            # departs from the committed trace row by more than 10 %
+            res["roofline"]["frac_live"] = fr(per_launch_min, live_s)
             if use_rp:
-                res["roofline"]["live_clock_vs_rocprof"] = round(live_s * 1e6 / rp["timed_avg_us"], 3)
+                ratio = live_s * 1e6 / rp["timed_avg_us"]
+                res["roofline"]["live_clock_vs_rocprof"] = round(ratio, 3)
+                res["roofline"]["live_departs_from_committed_row"] = bool(abs(ratio - 1.0) > 0.10)
+            mp = mfma_profile(mangle(kname) or kname)
+            if mp and mp.get("generator", {}).get("kernels"):
+                res["roofline"]["issue_counters"] = mp["generator"]["kernels"][0] | {"source": mp["source"]}
             if iso.get("launches"):
                 # the same kernel with one batch on the GPU (untimed pass): live in-kernel clock, and the
                 # one-stream trace row (profiles/rNN_kernel_stats_1stream.csv) beside it
@@ -773,6 +869,13 @@ def main():
                 tf = cc["flops"] / (cc["ms"] / 1e3) / 1e12
                 res["roofline_conv3x3"] = {"bound": "mfma", "achieved": round(tf, 1), "peak": BF16_PEAK_TFLOPS,
                                            "unit": "TFLOP/s", "frac": round(tf / BF16_PEAK_TFLOPS, 4)}
+                mp = mfma_profile("conv3x3_halo")
+                if mp and "generator" in mp:
+                    # PMC MFMA utilisation of the halo 3x3 convs (committed rocprofv3 --pmc rows) and the whole step
+                    res["roofline_conv3x3"]["mfma_counters"] = {
+                        "source": mp["source"], "definition": mp["definition"],
+                        "step_mfma_busy": mp["generator"]["totals"].get("mfma_busy"),
+                        "kernels": mp["generator"]["kernels"]}
             aad = classes["aad_all"]
             if aad["ms"]:
                 # SURVEY.md §8d definition: sum over AADLayers of |h_in|+|z_attr|+|out| / AAD kernel time
@@ -784,8 +887,8 @@ def main():
                                               "untimed one-batch-at-a-time pass with every class bracketed by "
                                               "HIP events")
         legs = [s for s in a.legs.split(",") if s] if world == 1 else []
-        if legs:
-            res["legs"] = {}
+        if legs or multi_legs:
+            res["legs"] = dict(multi_legs)
         if "d2h" in legs:
             res["legs"]["d2h"] = d2h_leg(G, crops, z, a.steps, pipe.nstreams)
         if "fp16" in legs:

@@ -113,9 +113,11 @@ __global__ void __launch_bounds__(256) resize_u8_linear_kernel(const uint8_t* __
 }
 
 // get_final_image (image_processing.py:51-76): the full frame, and per identity j in order a 224x224 uint8 swap
-// warped by cv2.warpAffine(swap, invertAffineTransform(tfm), BORDER_REPLICATE) and its float mask warped with
-// the default constant 0 border, composited as final = mask_t*swap_t + (1-mask_t)*final in float32 (numpy's
-// order, one rounding per operation, no FMA), one uint8 cast at the end.  warpAffine's fixed point (imgwarp.cpp):
+// warped by cv2.warpAffine(swap, invertAffineTransform(tfm), BORDER_REPLICATE) and its mask warped with the
+// default constant 0 border, composited as final = mask_t*swap_t + (1-mask_t)*final, one uint8 cast at the end.
+// The mask is face_mask_static's ``mask/255`` (masks.py:83-85): a float64 array, so cv2 warps it with float table
+// weights and double accumulation (remapBilinear<Cast<double,double>, float>) and numpy composites in float64:
+// all of that in double here (one rounding per operation, no FMA, numpy's order).  warpAffine's fixed point (imgwarp.cpp):
 // the map A (the double inverse of the given matrix, host-side) sampled at X = (rint((A1 y + A2) 1024) + 16 +
 // rint(A0 x 1024)) >> 5: pixel X >> 5, sub-pixel X & 31; bilinear weights from the 32 x 32 grid (15-bit integers
 // for uint8 with (sum + 2^14) >> 15, floats for the mask).
@@ -140,7 +142,7 @@ __device__ CvWarp cv_warp_pos(const double* A, int x, int y) {
 struct ImageBlendArgs {
   uint8_t* frame; int H, W;
   const uint8_t* swaps; long sstride;   // [J][224][224][3]
-  const float* masks; long mstride;     // [J][224][224]
+  const double* masks; long mstride;    // [J][224][224] float64 (mask/255)
   const double* maps;                   // [J][6] warpAffine's effective dst -> src map
   int J, S;
 };
@@ -150,21 +152,21 @@ __global__ void __launch_bounds__(256) blend_image_kernel(const ImageBlendArgs a
   if (p >= (long)a.H * a.W) return;
   const int y = (int)(p / a.W), x = (int)(p - (long)y * a.W);
   uint8_t* fr = a.frame + p * 3;
-  float fin[3] = {(float)fr[0], (float)fr[1], (float)fr[2]};
+  double fin[3] = {(double)fr[0], (double)fr[1], (double)fr[2]};
   const int S = a.S;
   for (int j = 0; j < a.J; ++j) {
     const CvWarp w = cv_warp_pos(a.maps + j * 6, x, y);
     const float wx[2] = {__fsub_rn(1.f, w.wx1), w.wx1}, wy[2] = {__fsub_rn(1.f, w.wy1), w.wy1};
     const uint8_t* sw = a.swaps + j * a.sstride;
-    const float* mk = a.masks + j * a.mstride;
+    const double* mk = a.masks + j * a.mstride;
     int acc[3] = {0, 0, 0};
-    float ms = 0.f;
+    double ms = 0.0;
     bool any = false;
 #pragma unroll
     for (int ky = 0; ky < 2; ++ky)
 #pragma unroll
       for (int kx = 0; kx < 2; ++kx) {
-        const float wf = __fmul_rn(wy[ky], wx[kx]);
+        const float wf = __fmul_rn(wy[ky], wx[kx]);          // the float interpolation table entry
         const int wi = (int)rintf(__fmul_rn(wf, 32768.f));
         const int tx = w.sx + kx, ty = w.sy + ky;
         const bool in = tx >= 0 && tx < S && ty >= 0 && ty < S;
@@ -173,15 +175,15 @@ __global__ void __launch_bounds__(256) blend_image_kernel(const ImageBlendArgs a
         const long o = (long)cy * S + cx;
 #pragma unroll
         for (int c = 0; c < 3; ++c) acc[c] += (int)sw[o * 3 + c] * wi;
-        ms = __fadd_rn(ms, __fmul_rn(in ? mk[o] : 0.f, wf));                  // constant 0 border
+        ms = __dadd_rn(ms, __dmul_rn(in ? mk[o] : 0.0, (double)wf));          // constant 0 border
       }
-    const float mt = any ? ms : 0.f;
-    const float omt = __fsub_rn(1.f, mt);
+    const double mt = any ? ms : 0.0;
+    const double omt = __dsub_rn(1.0, mt);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       int v = (acc[c] + (1 << 14)) >> 15;
       v = v < 0 ? 0 : (v > 255 ? 255 : v);
-      fin[c] = __fadd_rn(__fmul_rn(mt, (float)v), __fmul_rn(omt, fin[c]));
+      fin[c] = __dadd_rn(__dmul_rn(mt, (double)v), __dmul_rn(omt, fin[c]));
     }
   }
 #pragma unroll
@@ -204,7 +206,7 @@ extern "C" int ghost_resize_u8_linear(const uint8_t* src, int64_t src_stride, in
 }
 
 extern "C" int ghost_blend_image_u8(uint8_t* frame, int H, int W, const uint8_t* swaps, int64_t swap_stride, int J,
-                                    int S, const float* masks, int64_t mask_stride, const double* maps, void* stream) {
+                                    int S, const double* masks, int64_t mask_stride, const double* maps, void* stream) {
   if (!frame || (J > 0 && (!swaps || !masks || !maps)))
     return ghost::set_last_error(GHOST_EINVAL, "ghost_blend_image_u8: null argument");
   if (H <= 0 || W <= 0 || J < 0 || S <= 0 || (J > 0 && (swap_stride < (int64_t)S * S * 3 || mask_stride < (int64_t)S * S)))

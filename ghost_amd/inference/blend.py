@@ -6,7 +6,8 @@
   ``(mask_t*swap_t + (1-mask_t)*frame).type(uint8)``, in place on device-resident uint8 frames.
 * ``blend_image`` — get_final_image (utils/inference/image_processing.py:51-76), the image-to-image path:
   cv2.resize to 224, cv2.warpAffine with BORDER_REPLICATE for the swap and a constant 0 border for the
-  mask, identities accumulated in float32 and cast to uint8 once.
+  mask, identities accumulated in float64 (the mask is ``mask/255`` of a uint8 array: numpy float64) and cast
+  to uint8 once.
 Producing the masks (landmark model + cv2 erode/blur, masks.py) stays on the host as in the reference;
 the masks are inputs here.  cv2 / kornia are absent in this container: the kernels follow restatements
 of their published algorithms (oracle/blend_ref.py), parity unpinned.
@@ -84,8 +85,9 @@ def cv_warp_map(tfm: np.ndarray) -> np.ndarray:
 def blend_image(full_frame: torch.Tensor, swaps: torch.Tensor, masks: torch.Tensor,
                 tfms: Sequence[np.ndarray]) -> torch.Tensor:
     """get_final_image on the device: full_frame u8 [H,W,3] (modified in place and returned), swaps u8
-    [J,256,256,3] (or already 224), masks f32 [J,224,224] (face_mask_static's, host-made), tfms J crop <-
-    frame [2,3] matrices (estimate_norm's, float64)."""
+    [J,256,256,3] (or already 224), masks [J,224,224] — face_mask_static's float64 ``mask/255`` as the reference
+    returns it, or the float32 masks of ``masks.face_masks`` (q/255 of a uint8 q, rebuilt exactly as q/255.0 in
+    float64) — tfms J crop <- frame [2,3] matrices (estimate_norm's, float64)."""
     _lib.require_gpu(full_frame, "blend_image")
     dev = full_frame.device
     if full_frame.dtype != torch.uint8 or full_frame.ndim != 3 or full_frame.shape[2] != 3 or \
@@ -95,7 +97,10 @@ def blend_image(full_frame: torch.Tensor, swaps: torch.Tensor, masks: torch.Tens
     swaps = swaps.to(dev).contiguous()
     if tuple(swaps.shape[1:3]) != (224, 224):
         swaps = resize_u8(swaps, (224, 224))          # image_processing.py:63
-    masks = masks.to(dev, torch.float32).contiguous()
+    masks = torch.as_tensor(masks).to(dev)
+    if masks.dtype != torch.float64:      # q/255 in float32 -> the float64 q/255.0 numpy computes
+        masks = torch.round(masks.to(torch.float64) * 255.0) / 255.0
+    masks = masks.contiguous()
     if tuple(masks.shape) != (J, 224, 224) or len(tfms) != J:
         raise RuntimeError("ghost_amd: blend_image needs J masks [224,224] and J transforms")
     maps = torch.from_numpy(np.stack([cv_warp_map(t) for t in tfms]).reshape(J, 6) if J else

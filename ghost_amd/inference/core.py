@@ -1,8 +1,14 @@
 """Per-identity swap loop of model_inference (utils/inference/core.py:13-26, :57-88).
 
 Only the per-frame part is here: crops in, swapped crops out with the reference's
-``present`` bookkeeping (frames without a face yield ``[]``).  Detection, alignment,
-landmarks and blending stay on the host pipeline of the reference (out of scope).
+``present`` bookkeeping (frames without a face yield ``[]``).  Detection, alignment and
+landmarks stay on the host pipeline of the reference (out of scope).
+
+* ``resize_frames`` — video_processing.py:174-188 on the device: the 224x224 aligned crops of one identity
+  (``[]`` where no face was found) -> ``present`` and the 256x256 crops, resized by the cv2 INTER_LINEAR
+  fixed-point kernel (``ghost_resize_u8_linear``) instead of one cv2.resize per frame on the host;
+* ``swap_identity_frames`` — core.py:57-88 for one identity on already-resized crops (host or device);
+* ``swap_crop_frames`` — both: crop_frames of one identity in, the per-frame list out.
 """
 from __future__ import annotations
 
@@ -32,11 +38,51 @@ def transform_target_to_torch(resized_frs: np.ndarray, half: bool = True, device
     return y.permute(0, 3, 1, 2)
 
 
-def swap_identity_frames(resized_frs: np.ndarray, present: Sequence[int], source_embed: torch.Tensor, G,
+def resize_frames(crop_frames: Sequence, new_size=(256, 256), device=None):
+    """video_processing.py:174-188 with the resize on the device.  ``crop_frames``: one entry per video frame,
+    a uint8 [h, w, 3] crop (crop_frames_and_get_transforms' 224x224 warpAffine output) or ``[]`` where the
+    identity had no face (cv2.resize raises on it and the reference marks the frame absent).  Returns
+    (resized device uint8 [n, 256, 256, 3] of the present frames in frame order, present: float64 [F] of 1/0,
+    as ``np.ones`` then ``present[i] = 0`` make it).  All crops of one call must share one size (the reference's
+    crops are all crop_size x crop_size)."""
+    device = torch.device(device or "cuda")
+    present = np.ones(len(crop_frames))
+    keep = []
+    for i, fr in enumerate(crop_frames):
+        a = np.asarray(fr) if not isinstance(fr, list) else None
+        if a is None or a.ndim != 3 or a.size == 0:
+            present[i] = 0
+        else:
+            keep.append(a)
+    Wd, Hd = new_size
+    if not keep:
+        return torch.empty(0, Hd, Wd, 3, dtype=torch.uint8, device=device), present
+    shapes = {k.shape for k in keep}
+    if len(shapes) != 1 or keep[0].dtype != np.uint8 or keep[0].shape[2] != 3:
+        raise RuntimeError(f"ghost_amd: resize_frames needs uint8 crops of one [h,w,3] shape, got {sorted(shapes)}")
+    host = torch.from_numpy(np.stack(keep))
+    src = host.pin_memory().to(device, non_blocking=True)
+    if tuple(src.shape[1:3]) == (Hd, Wd):
+        return src, present
+    from .blend import resize_u8
+    return resize_u8(src, (Wd, Hd)), present
+
+
+def swap_crop_frames(crop_frames: Sequence, source_embed: torch.Tensor, G, BS: int = 60, device=None,
+                     return_device: bool = False):
+    """core.py:57-88 for one identity from its crop_frames: ``resize_frames`` on the device (224 -> 256, the
+    ``present`` vector), then ``swap_identity_frames`` on the device-resident crops.  Returns the per-frame list
+    (swapped uint8 crop, or ``[]``), plus the device swaps with ``return_device``."""
+    crops, present = resize_frames(crop_frames, device=device)
+    return swap_identity_frames(crops, present, source_embed, G, BS=BS, device=device, return_device=return_device)
+
+
+def swap_identity_frames(resized_frs, present: Sequence[int], source_embed: torch.Tensor, G,
                          BS: int = 60, device=None, return_device: bool = False):
     """core.py:57-88 for one identity: batched swap of the present crops, then re-insert ``[]``
     for frames without a face so the result is indexed by frame (bit-exact crop indices).
 
+    ``resized_frs``: host uint8 [n,256,256,3] (numpy) or a device tensor of them (``resize_frames``' output).
     The crops go to the device once (core.py:63 transfers the identity's frames at once); each
     batch of BS is swapped into a device buffer and copied to pinned host memory on a copy stream
     while the next batch is swapped (the reference's per-batch ``.cpu()``, faceshifter_run.py:22,
@@ -47,8 +93,10 @@ def swap_identity_frames(resized_frs: np.ndarray, present: Sequence[int], source
     if n == 0:
         final = reinsert_present(np.zeros((0, 256, 256, 3), np.uint8), present)
         return (final, None) if return_device else final
-    host_in = torch.from_numpy(np.ascontiguousarray(resized_frs))
-    crops = host_in.pin_memory().to(device, non_blocking=True)
+    if torch.is_tensor(resized_frs):
+        crops = resized_frs.to(device)
+    else:
+        crops = torch.from_numpy(np.ascontiguousarray(resized_frs)).pin_memory().to(device, non_blocking=True)
     z = source_embed.to(device)
     out = torch.empty(n, 256, 256, 3, dtype=torch.uint8, device=device)
     host = torch.empty(n, 256, 256, 3, dtype=torch.uint8, pin_memory=True)

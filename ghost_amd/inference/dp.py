@@ -94,6 +94,155 @@ def model_inference_dp(resized_frs: np.ndarray, present: Sequence[int], source_e
     return reinsert_present(gathered.cpu().numpy(), present)
 
 
+def _identity_crops(ident):
+    """One identity of model_inference_multi -> (host crops of its present frames in frame order (a list of
+    uint8 arrays or one [n,h,w,3] array), present, source embedding, whether the crops still need resize_frames'
+    224 -> 256 resize)."""
+    if len(ident) == 3:                       # (resized_frs, present, source_embed): resize_frames already ran
+        resized, present, emb = ident
+        return resized, np.asarray(present), emb, False
+    if len(ident) == 2:                       # (crop_frames, source_embed): crop_frames_and_get_transforms' lists
+        crop_frames, emb = ident
+        present = np.ones(len(crop_frames))
+        keep = []
+        for i, fr in enumerate(crop_frames):
+            a = None if isinstance(fr, list) else np.asarray(fr)
+            if a is None or a.ndim != 3 or a.size == 0:
+                present[i] = 0
+            else:
+                keep.append(a)
+        return keep, present, emb, True
+    raise ValueError("ghost_amd: an identity is (crop_frames, source_embed) or (resized_frs, present, source_embed)")
+
+
+def model_inference_multi(identities: Sequence, G, BS: int = 64, device=None, group=None, collect: str = "rank0",
+                          output: str = "host", streams: int = 2):
+    """The identity loop of model_inference (utils/inference/core.py:56-88) for every identity of a video at once,
+    data-parallel over the group (BASELINE config 5: several source -> target identities in one video).
+
+    ``identities``: per identity either ``(crop_frames, source_embed)`` — crop_frames_and_get_transforms' list for
+    that identity, one 224x224 uint8 crop or ``[]`` per video frame; resize_frames (video_processing.py:174-188)
+    runs here, its cv2.resize on the device — or ``(resized_frs, present, source_embed)`` after resize_frames.
+
+    Every identity's present crops form one sequence in identity-major, frame order; rank r of W swaps the
+    contiguous block ``shard_bounds(N, W, r)`` of it in batches of BS.  A batch may hold crops of several
+    identities: each crop carries its identity's embedding row (per-sample z_id rows, ``swap_mixed_identities``).
+    Batches run through a ``GatherPipeline`` (``streams`` batches in flight; each batch gathered to rank 0 —
+    ``collect="rank0"``, the video mux rank — or to every rank with ``collect="all"``, while the next batch is
+    swapped).  The receiving rank places every rank's rows at their sequence positions, copies them to pinned host
+    memory batch by batch on a copy stream (``output="host"``), and returns ``final_frames_list`` as core.py:88
+    builds it: per identity one entry per video frame, the swapped uint8 crop or ``[]``.  ``output="device"``
+    returns the same lists holding device tensor views instead (no host copy).  Ranks that receive nothing return
+    ``None``."""
+    if collect not in ("rank0", "all"):
+        raise ValueError(f"ghost_amd: collect must be 'rank0' or 'all', got {collect!r}")
+    if output not in ("host", "device"):
+        raise ValueError(f"ghost_amd: output must be 'host' or 'device', got {output!r}")
+    device = torch.device(device or "cuda")
+    gpu = device.type == "cuda"
+    dist_on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if dist_on else 1
+    rank = dist.get_rank(group) if dist_on else 0
+    idents = [_identity_crops(i) for i in identities]
+    counts = [len(c) for c, _, _, _ in idents]
+    n = sum(counts)
+    offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    start, end, per = shard_bounds(n, world, rank)
+    # the per-crop shape every rank agrees on (all ranks hold the host lists): 256x256 after resize_frames
+    fshape = (256, 256, 3)
+    for crops, _, _, needs in idents:
+        if len(crops) and not needs:
+            fshape = tuple(np.asarray(crops[0]).shape)
+            break
+    # this rank's crops (host -> device once, per identity part; crop_frames parts resized 224 -> 256 on the device,
+    # video_processing.py:184) and their identity rows
+    parts, ids = [], []
+    for q, (crops, _, _, needs) in enumerate(idents):
+        a, b = max(start, int(offs[q])), min(end, int(offs[q + 1]))
+        if a >= b:
+            continue
+        part = crops[a - offs[q]:b - offs[q]]
+        host = torch.from_numpy(np.ascontiguousarray(np.stack(part) if isinstance(part, list) else np.asarray(part)))
+        dpart = host.pin_memory().to(device, non_blocking=True) if gpu else host.to(device)
+        if needs and tuple(dpart.shape[1:3]) != (256, 256):
+            from .blend import resize_u8
+            dpart = resize_u8(dpart, (256, 256))
+        parts.append(dpart)
+        ids.append(np.full(b - a, q, np.int64))
+    embeds = torch.stack([torch.as_tensor(e).reshape(-1) for _, _, e, _ in idents]).to(device) if idents else None
+    if parts:
+        local = parts[0] if len(parts) == 1 else torch.cat(parts)
+        if tuple(local.shape[1:]) != fshape:
+            raise ValueError(f"ghost_amd: identities' crops differ in shape ({tuple(local.shape[1:])} vs {fshape})")
+        z_all = embeds.index_select(0, torch.from_numpy(np.concatenate(ids)).to(device))
+        try:
+            pdt = next(G.parameters()).dtype
+        except (AttributeError, StopIteration):
+            pdt = None
+        if pdt == torch.float16:
+            z_all = z_all.half()                            # core.py:65-66 (a .half() module)
+    else:
+        local = torch.empty((0,) + fshape, dtype=torch.uint8, device=device)
+        z_all = None
+    nb = (per + BS - 1) // BS if per else 0
+    B = max(1, min(BS, per))
+    zb = [None]
+    streams = max(1, streams) if gpu else 1
+    pipe = GatherPipeline(lambda c, o: G.swap_u8(c, zb[0], out=o), (B,) + fshape, device, group=group,
+                          depth=2 * streams, streams=streams, dst=0 if collect == "rank0" else None)
+    receiver = pipe.receiver
+    out_all = torch.empty((n,) + fshape, dtype=torch.uint8, device=device) if receiver else None
+    host_all = (torch.empty((n,) + fshape, dtype=torch.uint8, pin_memory=True)
+                if receiver and output == "host" and gpu else None)
+    copy = torch.cuda.Stream(device) if host_all is not None else None
+    cur = torch.cuda.current_stream(device) if gpu else None
+    bounds = [shard_bounds(n, world, r)[:2] for r in range(world)]
+
+    def place(k, ticket):
+        g = pipe.result(ticket)                              # caller's stream waits for the batch
+        if g is None:
+            return
+        row = 0
+        for r, (s0, e0) in enumerate(bounds):
+            a = s0 + k * B
+            c = max(0, min(B, e0 - a))
+            if c:
+                out_all[a:a + c].copy_(g[row:row + c])
+                if copy is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(cur)
+                    with torch.cuda.stream(copy):
+                        copy.wait_event(ev)
+                        host_all[a:a + c].copy_(out_all[a:a + c], non_blocking=True)
+            row += c
+
+    pending = []
+    for k in range(nb):
+        a = k * B
+        c = max(0, min(B, (end - start) - a))
+        kc = [max(0, min(B, e0 - s0 - a)) for s0, e0 in bounds]
+        zb[0] = z_all[a:a + c] if c else None
+        pending.append((k, pipe.submit(local[a:a + c], counts=kc)))
+        if len(pending) > pipe.depth - 1:                   # consume a slot before it is reused
+            place(*pending.pop(0))
+    for kt in pending:
+        place(*kt)
+    pipe.drain()
+    if not receiver:
+        if gpu:
+            torch.cuda.current_stream(device).synchronize()
+        return None
+    if copy is not None:
+        copy.synchronize()
+        out_all.record_stream(copy)
+        rows = host_all.numpy()
+    elif output == "host":
+        rows = out_all.numpy()           # CPU tensors (gloo tests)
+    else:
+        rows = out_all
+    return [reinsert_present(rows[offs[q]:offs[q + 1]], present) for q, (_, present, _, _) in enumerate(idents)]
+
+
 def swap_mixed_identities(crops: torch.Tensor, identity_index: torch.Tensor, source_embeds: torch.Tensor, G,
                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Config 5 (several identities in one batch): each crop carries the index of its source

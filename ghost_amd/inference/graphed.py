@@ -9,8 +9,11 @@ replays it with one ``hipGraphLaunch``.  The inputs are copied into the graph's 
 the result is read from its output buffer, so the replay runs the same kernels on the same weights: the
 output bytes are identical to ``swap_u8``'s (tests/test_gpu_pipeline.py).
 
-The graph holds the module's packed weights and workspace as they were at capture: after
-``load_state_dict`` / ``.to`` / an in-place parameter change, build a new ``GraphedSwap``.
+The graph holds the module's packed weights and workspace as they were at capture, and the ``GraphedSwap``
+keeps that runtime (its packed weight tensors, native handle and workspace) alive for as long as it lives.  A
+replay after the module was re-packed (``load_state_dict``, ``.to`` / ``.half``, an in-place parameter change,
+a replaced parameter — anything ``PackedModule`` invalidates on) raises instead of running the stale plan:
+build a new ``GraphedSwap`` then.
 """
 from __future__ import annotations
 
@@ -44,6 +47,8 @@ class GraphedSwap:
         with torch.cuda.graph(self.graph, stream=self._capture_stream):
             G.swap_u8(self.crops, self.z, out=self.out)
         torch.cuda.synchronize(dev)
+        # the captured kernels read the packed weights of this runtime (and its handle / workspace): hold it
+        self._rt = G._rt
 
     def __call__(self, crops_u8: torch.Tensor, z_id: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """swap_u8(crops_u8, z_id): inputs copied into the graph's buffers, one graph launch on the current
@@ -55,6 +60,10 @@ class GraphedSwap:
         if tuple(z.shape) != tuple(self.z.shape):
             raise RuntimeError(f"ghost_amd: GraphedSwap was captured for z_id {tuple(self.z.shape)}, got "
                                f"{tuple(z_id.shape)}")
+        if not self.G._pack_current(self._rt):
+            raise RuntimeError("ghost_amd: the module was re-packed (load_state_dict / .to / .half / a parameter "
+                               "change) after this GraphedSwap was captured; its graph would replay the old weights. "
+                               "Capture a new GraphedSwap.")
         self.crops.copy_(crops_u8, non_blocking=True)
         self.z.copy_(z, non_blocking=True)
         self.graph.replay()

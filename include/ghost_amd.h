@@ -251,11 +251,13 @@ int ghost_resize_u8_linear(const uint8_t* src, int64_t src_stride, int F, int Hs
 /* get_final_image (utils/inference/image_processing.py:51-76) for one full frame [H,W,3] u8, in place: for
  * each identity j in order, swap_t = cv2.warpAffine(swaps[j] (S x S, already resized), invertAffineTransform
  * (tfm_j), BORDER_REPLICATE), mask_t = the same warp of masks[j] with the constant 0 border, final =
- * mask_t*swap_t + (1-mask_t)*final in float32; one uint8 cast at the end.  maps[j] = the [2][3] double
+ * mask_t*swap_t + (1-mask_t)*final; one uint8 cast at the end.  masks are float64 [J][S][S] (face_mask_static
+ * returns mask/255 of a uint8 array, masks.py:83-85: numpy float64), so the mask warp (float table weights, double
+ * accumulation, as cv2 does for CV_64F) and the composite run in double as numpy does.  maps[j] = the [2][3] double
  * matrix warpAffine samples with (the inverse of invertAffineTransform(tfm_j), computed on the host as
  * OpenCV does: ghost_amd.inference.blend.cv_warp_map). */
 int ghost_blend_image_u8(uint8_t* frame, int H, int W, const uint8_t* swaps, int64_t swap_stride, int J, int S,
-                         const float* masks, int64_t mask_stride, const double* maps, void* stream);
+                         const double* masks, int64_t mask_stride, const double* maps, void* stream);
 
 /* ---- face masks (face_mask_static, utils/inference/masks.py:38-107) ----
  * Host, CPU only (no device pointers): for F frames of 106 float32 landmarks [F][106][2] and their

@@ -72,7 +72,7 @@ def paste_back(full_frame_u8: np.ndarray, swap_u8: np.ndarray, mask: np.ndarray,
     return final.numpy()
 
 
-def make_case(seed: int, H: int = 270, W: int = 480, S: int = 224):
+def make_case(seed: int, H: int = 270, W: int = 480, S: int = 224, scale_range=(1.2, 2.5)):
     """A synthetic frame, swapped crop, soft mask and an estimate_norm-like similarity transform
     (frame -> crop: scale, rotation, translation) that puts the face inside the frame."""
     g = np.random.Generator(np.random.PCG64(seed))
@@ -81,7 +81,7 @@ def make_case(seed: int, H: int = 270, W: int = 480, S: int = 224):
     yy, xx = np.mgrid[0:S, 0:S].astype(np.float32)
     r = np.sqrt((yy - S / 2) ** 2 + (xx - S / 2) ** 2) / (S / 2)
     mask = np.clip(1.3 - r, 0.0, 1.0).astype(np.float32)   # 1 in the centre, 0 near the border
-    scale = g.uniform(1.2, 2.5)
+    scale = g.uniform(*scale_range)
     ang = g.uniform(-0.4, 0.4)
     cx, cy = g.uniform(0.35 * W, 0.65 * W), g.uniform(0.35 * H, 0.65 * H)
     c, s = scale * np.cos(ang), scale * np.sin(ang)
@@ -160,10 +160,11 @@ def warp_affine_map(m_dst_to_src_given: np.ndarray) -> np.ndarray:
 
 
 def warp_affine_cv(src: np.ndarray, M: np.ndarray, dsize, border: str) -> np.ndarray:
-    """cv2.warpAffine(src, M, dsize=(W, H), INTER_LINEAR, border) for uint8 [H, W, 3] or float32 [H, W]
+    """cv2.warpAffine(src, M, dsize=(W, H), INTER_LINEAR, border) for uint8 [H, W, 3] or float32 / float64 [H, W]
     (border 'replicate' or 'constant' with 0).  Fixed point as imgwarp.cpp: X = (round(M1*y + M2)*1024 + 16 +
     round(M0*x*1024)) >> 5 (sub-pixel index X & 31, pixel X >> 5), 32 x 32 bilinear table; uint8: 15-bit
-    integer weights, (sum + 2^14) >> 15; float: float weights, left-to-right float sum."""
+    integer weights, (sum + 2^14) >> 15; float32 / float64: the float table weights, a left-to-right sum in the
+    source's type (remapBilinear's work type: float for CV_32F, double for CV_64F)."""
     W, H = dsize
     A = warp_affine_map(M)
     x = np.arange(W, dtype=np.float64)
@@ -184,7 +185,8 @@ def warp_affine_cv(src: np.ndarray, M: np.ndarray, dsize, border: str) -> np.nda
     is_u8 = src.dtype == np.uint8
     C = src.shape[2] if src.ndim == 3 else 1
     s = src.reshape(Hs, Ws, C)
-    acc = np.zeros((H, W, C), np.int64 if is_u8 else np.float32)
+    ft = np.float64 if src.dtype == np.float64 else np.float32
+    acc = np.zeros((H, W, C), np.int64 if is_u8 else ft)
     inside_any = np.zeros((H, W), bool)
     for ky in range(2):
         for kx in range(2):
@@ -200,7 +202,7 @@ def warp_affine_cv(src: np.ndarray, M: np.ndarray, dsize, border: str) -> np.nda
                 wi = _cv_round(w * np.float32(1 << REMAP_COEF_BITS))
                 acc = acc + v.astype(np.int64) * wi[..., None]
             else:
-                acc = (acc + v.astype(np.float32) * w[..., None]).astype(np.float32)
+                acc = (acc + v.astype(ft) * w[..., None].astype(ft)).astype(ft)
     if is_u8:
         out = np.clip((acc + (1 << (REMAP_COEF_BITS - 1))) >> REMAP_COEF_BITS, 0, 255).astype(np.uint8)
     else:
@@ -214,16 +216,21 @@ def get_final_image(final_frames, full_frame: np.ndarray, tfm_arrays, masks) -> 
     """image_processing.py:51-76 (get_final_image) with the masks given (face_mask_static needs the
     landmark model, absent here): per identity i, frame = cv2.resize(swap_i, 224); swap_t = warpAffine
     (frame, invertAffineTransform(tfm_i), BORDER_REPLICATE); mask_t = warpAffine(mask_i, ..., constant 0);
-    final = mask_t*swap_t + (1-mask_t)*final in float32, identities in order; one uint8 cast at the end."""
+    final = mask_t*swap_t + (1-mask_t)*final, identities in order; one uint8 cast at the end.  The mask is
+    face_mask_static's ``mask/255`` (masks.py:83-85) of a uint8 array — numpy float64 — so the mask warp and the
+    composite are float64, as numpy promotes them (``masks`` given as uint8 are divided here; float arrays are
+    taken as they are)."""
     H, W = full_frame.shape[:2]
     final = full_frame.copy()
     for sw, tfm, mask in zip(final_frames, tfm_arrays, masks):
+        mask = np.asarray(mask)
+        if mask.dtype == np.uint8:
+            mask = mask / 255
         frame = resize_linear_u8(sw, (224, 224))
         mat_rev = invert_affine_cv(tfm)
         swap_t = warp_affine_cv(frame, mat_rev, (W, H), "replicate")
-        mask_t = warp_affine_cv(mask.astype(np.float32), mat_rev, (W, H), "constant")[..., None]
-        final = (mask_t * swap_t.astype(np.float32) + (np.float32(1.0) - mask_t) * final.astype(np.float32))
-        final = final.astype(np.float32)
+        mask_t = warp_affine_cv(mask, mat_rev, (W, H), "constant")[..., None]
+        final = mask_t * swap_t + (1 - mask_t) * final
     return np.array(final, dtype="uint8")
 
 

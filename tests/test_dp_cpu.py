@@ -323,3 +323,136 @@ def test_gather_pipeline_dst_rank0_gloo():
     for k in range(4):
         expect = torch.cat([fake_swap(torch.full((2, 4, 4, 3), 10 * k + rr, dtype=torch.uint8)) for rr in range(world)])
         assert np.array_equal(outs0[k], expect.numpy()), k
+
+
+class _FakeGz(_FakeG):
+    """Stand-in swap that also depends on each row's identity embedding (z[:, 0] added to the bytes)."""
+
+    def swap_u8(self, crops, z, out=None):
+        zz = z.reshape(z.shape[0], -1)[:, 0].round().to(torch.int64)
+        y = ((fake_swap(crops).to(torch.int64) + zz.view(-1, 1, 1, 1)) % 256).to(torch.uint8)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+
+MULTI_PRESENT = [[1, 1, 0, 1, 1, 1, 0], [0, 1, 1, 1, 0, 0, 1], [1, 0, 0, 0, 0, 1, 1]]
+
+
+def _multi_case():
+    """Three identities of one 7-frame video: identity 0 as crop_frames (a crop or [] per frame), 1 and 2 after
+    resize_frames (present crops + present vector); embeddings 7*q + 3."""
+    g = np.random.Generator(np.random.PCG64(21))
+    idents, crops_of = [], []
+    for q, pres in enumerate(MULTI_PRESENT):
+        crops = g.integers(0, 256, size=(sum(pres), 256, 256, 3), dtype=np.uint8)
+        emb = torch.full((1, 512), 7.0 * q + 3)
+        crops_of.append(crops)
+        if q == 0:
+            it = iter(crops)
+            idents.append(([next(it) if p else [] for p in pres], emb))
+        else:
+            idents.append((crops, np.array(pres, np.float64), emb))
+    return idents, crops_of
+
+
+def _multi_worker(rank, world, port, collect, bs, q):
+    from ghost_amd.inference import dp
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        idents, _ = _multi_case()
+        out = dp.model_inference_multi(idents, _FakeGz(), BS=bs, device="cpu", collect=collect)
+        q.put((rank, None if out is None else [[f if isinstance(f, list) else f.copy() for f in fl] for fl in out]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _multi_expect():
+    _, crops_of = _multi_case()
+    exp = []
+    for q, (pres, crops) in enumerate(zip(MULTI_PRESENT, crops_of)):
+        sw = ((fake_swap(torch.from_numpy(crops)).to(torch.int64) + (7 * q + 3)) % 256).to(torch.uint8).numpy()
+        exp.append(reinsert_present(sw, pres))
+    return exp
+
+
+def _same_lists(got, exp):
+    assert len(got) == len(exp)
+    for fl, el in zip(got, exp):
+        assert len(fl) == len(el)
+        for a, b in zip(fl, el):
+            if isinstance(b, list):
+                assert isinstance(a, list) and a == []
+            else:
+                assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("world,collect,bs", [(1, "rank0", 4), (2, "rank0", 2), (2, "all", 3), (3, "rank0", 5)])
+def test_model_inference_multi_gloo(world, collect, bs):
+    """model_inference_multi (core.py:56-88 over every identity at once, config 5) on gloo:
+    identities' present crops in one identity-major sequence, contiguous shards, batches that mix identities
+    through per-sample embedding rows, gathered to rank 0 (or all) — rank 0 returns final_frames_list equal to the
+    single-process per-identity result, the other ranks None (rank0) or the same lists (all)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_multi_worker, args=(r, world, port, collect, bs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = _multi_expect()
+    _same_lists(res[0], exp)
+    for r in range(1, world):
+        if collect == "rank0":
+            assert res[r] is None
+        else:
+            _same_lists(res[r], exp)
+
+
+def _c5_bench_worker(rank, world, port, q):
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = []
+
+        class G(_FakeGz):
+            def swap_u8(self, crops, z, out=None):
+                calls.append(crops.shape[0])
+                return super().swap_u8(crops, z, out)
+        leg = bench.config5_multi_leg(torch.device("cpu"), world, frames_per_gpu=6, n_ident=4, BS=4, reps=2, G=G(),
+                                      crop=256)
+        q.put((rank, leg, calls))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_config5_multi_leg_reporting_gloo():
+    """bench.py's config-5 pipeline leg runs on every rank at N > 1 (gloo world 2, stand-in
+    swap): the video grows with N (frames_per_gpu * N), every rank swaps about half of the crops, the reported
+    times are the max over ranks (identical on both ranks) for both output modes."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c5_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (leg, calls) for r, leg, calls in (q.get(timeout=180) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (l0, c0), (l1, c1) = res[0], res[1]
+    assert l0["frames"] == 12 and l0["crops"] == l1["crops"]
+    for mode in ("device", "host"):
+        assert l0[mode] == l1[mode] and l0[mode]["crops_per_s"] > 0
+    per = (l0["crops"] + 1) // 2               # rank 0's contiguous shard
+    # 2 output modes x (1 warm-up + 2 timed) = 6 pipeline calls, each swapping the rank's whole shard
+    assert sum(c0) == 6 * per and sum(c1) == 6 * (l0["crops"] - per), (sum(c0), sum(c1), per)

@@ -217,3 +217,73 @@ def test_graphed_swap_is_bit_identical(lib, dt, B):
         ref = G.swap_u8(crops, z)
         torch.cuda.synchronize()
         assert torch.equal(got, ref)
+
+
+def test_graphed_swap_refuses_a_repacked_module(lib):
+    """after the module is re-packed (here load_state_dict), a replay would read the old runtime's
+    weights; GraphedSwap keeps that runtime alive and raises instead of returning bytes."""
+    from ghost_amd.inference import GraphedSwap
+    G, p = model("unet", 2, torch.bfloat16)
+    g = GraphedSwap(G, 1, DEV)
+    crops = torch.from_numpy(aei_ref.make_u8_crops(1, 5)).to(DEV)
+    z = torch.randn(1, 512, generator=torch.Generator().manual_seed(5)).to(DEV)
+    g(crops, z)
+    G.load_state_dict(p)
+    G.swap_u8(crops, z)                      # the eager call re-packs
+    with pytest.raises(RuntimeError, match="re-packed"):
+        g(crops, z)
+
+
+def test_resize_frames_on_device(lib):
+    """video_processing.py:174-188 on the device: present from the [] entries, the 224 -> 256 cv2 INTER_LINEAR
+    resize bit-exact against the OpenCV fixed-point restatement (oracle/blend_ref.resize_linear_u8; cv2 itself is
+    absent: parity against cv2 unpinned), and swap_crop_frames == swap_identity_frames on those crops."""
+    from oracle import blend_ref as R
+    from ghost_amd.inference.core import resize_frames, swap_crop_frames, swap_identity_frames
+    g = np.random.default_rng(12)
+    crops224 = g.integers(0, 256, (sum(PRESENT), 224, 224, 3), dtype=np.uint8)
+    it = iter(crops224)
+    crop_frames = [next(it) if p else [] for p in PRESENT]
+    dev_crops, present = resize_frames(crop_frames, device=DEV)
+    assert present.tolist() == [float(p) for p in PRESENT]
+    ref = np.stack([R.resize_linear_u8(c, (256, 256)) for c in crops224])
+    assert np.array_equal(dev_crops.cpu().numpy(), ref)
+    G, _ = model("unet", 2, torch.bfloat16)
+    _, z = aei_ref.make_inputs(1, 12)
+    a = swap_crop_frames(crop_frames, z.to(DEV), G, BS=3)
+    b = swap_identity_frames(ref, present, z.to(DEV), G, BS=3)
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        assert (x == [] and y == []) if isinstance(y, list) else np.array_equal(x, y)
+
+
+def test_model_inference_multi_rccl_one_rank(lib):
+    """dp.model_inference_multi (core.py:56-88 for three identities at once: mixed-identity
+    batches through per-sample embedding rows, one-rank RCCL gather to rank 0, final_frames_list) against
+    swap_identity_frames run identity by identity (fp32: batch composition moves bytes by at most 1 LSB)."""
+    import torch.distributed as dist
+    from ghost_amd.inference.core import swap_identity_frames
+    from ghost_amd.inference.dp import model_inference_multi
+    G, _ = model("unet", 2)
+    pres = [[1, 1, 0, 1, 1], [0, 1, 1, 1, 0], [1, 0, 1, 0, 1]]
+    g = np.random.default_rng(13)
+    idents, refs = [], []
+    for q, pr in enumerate(pres):
+        crops = g.integers(0, 256, (sum(pr), 256, 256, 3), dtype=np.uint8)
+        _, z = aei_ref.make_inputs(1, 100 + q)
+        idents.append((crops, np.array(pr, np.float64), z))
+        refs.append(swap_identity_frames(crops, pr, z.to(DEV), G, BS=4))
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        for mode in ("host", "device"):
+            got = model_inference_multi(idents, G, BS=4, device=DEV, output=mode)
+            assert len(got) == 3
+            for fl, rl in zip(got, refs):
+                assert len(fl) == len(rl)
+                for x, y in zip(fl, rl):
+                    if isinstance(y, list):
+                        assert isinstance(x, list) and x == []
+                    else:
+                        u8_close(x if mode == "host" else x.cpu().numpy(), y, max_lsb=1, frac=1e-3)
+    finally:
+        dist.destroy_process_group()

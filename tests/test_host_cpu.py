@@ -191,3 +191,44 @@ def test_bench_profile_lookups_match_the_launched_symbol():
     assert bench.mangle("aad_v5_kernel<__bf16, 64, 2, true, 2, true>") == "aad_v5_kernelIDF16bLi64ELi2ELb1ELi2ELb1EE"
     assert bench.mangle("aad_v4_kernel<64, 2, true, true, 2>") == "aad_v4_kernelILi64ELi2ELb1ELb1ELi2EE"
     assert bench.mangle("k<_Float16, false>") == "kIDF16_Lb0EE"
+
+
+def test_pack_invalidation_rules():
+    """_packed.PackedModule: the cached pack survives plain calls and is dropped by every edit it claims to see
+    (in-place edits, parameter / buffer / submodule replacement anywhere in the tree, .to/.half of a submodule,
+    load_state_dict); ADVICE r03."""
+    import copy
+
+    from ghost_amd.network import AEI_Net
+    G = AEI_Net("unet", num_blocks=1, c_id=512)
+    dev = torch.device("cpu")
+    built = []
+
+    def get():
+        return G._cached_runtime(dev, torch.float32, lambda sd: built.append(object()) or built[-1])
+
+    def _inplace(p, v):
+        with torch.no_grad():
+            p.add_(v)
+
+    rt = get()
+    assert get() is rt and len(built) == 1
+    cases = [
+        lambda: _inplace(G.generator.up1.weight, 0.0),                      # in-place: version counter
+        lambda: setattr(G.encoder.conv1[0], "weight", torch.nn.Parameter(torch.zeros_like(G.encoder.conv1[0].weight))),
+        lambda: G.encoder.conv1[1].register_buffer("running_mean", torch.zeros_like(G.encoder.conv1[1].running_mean)),
+        lambda: G.generator.AADBlk1.to(torch.float64),                     # .to on a submodule only
+        lambda: G.to(torch.float32),
+        lambda: setattr(G.encoder, "conv1", copy.deepcopy(G.encoder.conv1)),   # submodule replaced
+        lambda: _inplace(G.encoder.conv1[0].weight, 0.0),                # ... and the new one is owned
+        lambda: G.load_state_dict(G.state_dict()),
+    ]
+    for i, edit in enumerate(cases):
+        edit()
+        rt2 = get()
+        assert rt2 is not rt, f"edit {i} did not invalidate the pack"
+        rt = rt2
+        assert get() is rt
+    assert G._pack_current(rt) and not G._pack_current(object())
+    G.invalidate_pack()
+    assert get() is not rt
