@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--legs", default="config5_multi,d2h,fp16,config5,video,latency,arcface",
                     help="side measurements (comma list of config5_multi (every N), d2h, fp16, config5, video, latency, "
                          "arcface (N = 1 only); '' = none)")
-    ap.add_argument("--c5-frames", type=int, default=120, help="video frames per GPU of the config5_multi leg")
+    ap.add_argument("--c5-frames", type=int, default=240, help="video frames per GPU of the config5_multi leg")
     ap.add_argument("--video", type=int, default=900, help="frames of the config-3 video leg")
     ap.add_argument("--cpu-batches", default="1,64", help="CPU baseline batch sizes ('' = skip)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")

@@ -24,6 +24,34 @@ int set_last_error(int rc, const char* msg);
 
 namespace {
 
+// One rounding per operation, never fused: HIP's __fmul_rn / __dadd_rn ... are plain operators compiled with the
+// translation unit's contraction mode, so after inlining the compiler fuses a*b + c into an FMA.  These carry no
+// contract flag (the pragma applies to the operations written in their bodies).
+__device__ __forceinline__ float f_mul(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float f_add(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+__device__ __forceinline__ float f_sub(float a, float b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
+__device__ __forceinline__ double d_mul(double a, double b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ double d_add(double a, double b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+__device__ __forceinline__ double d_sub(double a, double b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
+
 struct BlendArgs {
   uint8_t* frames; long fstride; int H, W;
   const uint8_t* swaps; long sstride; int Hs, Ws;
@@ -80,14 +108,14 @@ __device__ RzTap rz_tap(int d, int src_n, int dst_n) {
   const double scale = 1.0 / ((double)dst_n / (double)src_n);
   float f = (float)(((double)d + 0.5) * scale - 0.5);
   int s0 = (int)floorf(f);
-  f = __fsub_rn(f, (float)s0);
+  f = f_sub(f, (float)s0);
   if (s0 < 0) { f = 0.f; s0 = 0; }
   if (s0 >= src_n - 1) { f = 0.f; s0 = src_n - 1; }
   RzTap t;
   t.s0 = s0;
   t.s1 = min(s0 + 1, src_n - 1);
-  t.w0 = (int)rintf(__fmul_rn(__fsub_rn(1.f, f), 2048.f));
-  t.w1 = (int)rintf(__fmul_rn(f, 2048.f));
+  t.w0 = (int)rintf(f_mul(f_sub(1.f, f), 2048.f));
+  t.w1 = (int)rintf(f_mul(f, 2048.f));
   return t;
 }
 
@@ -126,10 +154,10 @@ struct CvWarp {
   float wx1, wy1;        // sub-pixel weights (multiples of 1/32)
 };
 __device__ CvWarp cv_warp_pos(const double* A, int x, int y) {
-  const long adelta = __double2ll_rn(__dmul_rn(__dmul_rn(A[0], (double)x), 1024.0));
-  const long bdelta = __double2ll_rn(__dmul_rn(__dmul_rn(A[3], (double)x), 1024.0));
-  const long X0 = __double2ll_rn(__dmul_rn(__dadd_rn(__dmul_rn(A[1], (double)y), A[2]), 1024.0)) + 16;
-  const long Y0 = __double2ll_rn(__dmul_rn(__dadd_rn(__dmul_rn(A[4], (double)y), A[5]), 1024.0)) + 16;
+  const long adelta = __double2ll_rn(d_mul(d_mul(A[0], (double)x), 1024.0));
+  const long bdelta = __double2ll_rn(d_mul(d_mul(A[3], (double)x), 1024.0));
+  const long X0 = __double2ll_rn(d_mul(d_add(d_mul(A[1], (double)y), A[2]), 1024.0)) + 16;
+  const long Y0 = __double2ll_rn(d_mul(d_add(d_mul(A[4], (double)y), A[5]), 1024.0)) + 16;
   const long X = (X0 + adelta) >> 5, Y = (Y0 + bdelta) >> 5;
   CvWarp w;
   w.sx = (int)(X >> 5);
@@ -156,7 +184,7 @@ __global__ void __launch_bounds__(256) blend_image_kernel(const ImageBlendArgs a
   const int S = a.S;
   for (int j = 0; j < a.J; ++j) {
     const CvWarp w = cv_warp_pos(a.maps + j * 6, x, y);
-    const float wx[2] = {__fsub_rn(1.f, w.wx1), w.wx1}, wy[2] = {__fsub_rn(1.f, w.wy1), w.wy1};
+    const float wx[2] = {f_sub(1.f, w.wx1), w.wx1}, wy[2] = {f_sub(1.f, w.wy1), w.wy1};
     const uint8_t* sw = a.swaps + j * a.sstride;
     const double* mk = a.masks + j * a.mstride;
     int acc[3] = {0, 0, 0};
@@ -166,8 +194,8 @@ __global__ void __launch_bounds__(256) blend_image_kernel(const ImageBlendArgs a
     for (int ky = 0; ky < 2; ++ky)
 #pragma unroll
       for (int kx = 0; kx < 2; ++kx) {
-        const float wf = __fmul_rn(wy[ky], wx[kx]);          // the float interpolation table entry
-        const int wi = (int)rintf(__fmul_rn(wf, 32768.f));
+        const float wf = f_mul(wy[ky], wx[kx]);          // the float interpolation table entry
+        const int wi = (int)rintf(f_mul(wf, 32768.f));
         const int tx = w.sx + kx, ty = w.sy + ky;
         const bool in = tx >= 0 && tx < S && ty >= 0 && ty < S;
         any |= in;
@@ -175,15 +203,15 @@ __global__ void __launch_bounds__(256) blend_image_kernel(const ImageBlendArgs a
         const long o = (long)cy * S + cx;
 #pragma unroll
         for (int c = 0; c < 3; ++c) acc[c] += (int)sw[o * 3 + c] * wi;
-        ms = __dadd_rn(ms, __dmul_rn(in ? mk[o] : 0.0, (double)wf));          // constant 0 border
+        ms = d_add(ms, d_mul(in ? mk[o] : 0.0, (double)wf));          // constant 0 border
       }
     const double mt = any ? ms : 0.0;
-    const double omt = __dsub_rn(1.0, mt);
+    const double omt = d_sub(1.0, mt);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       int v = (acc[c] + (1 << 14)) >> 15;
       v = v < 0 ? 0 : (v > 255 ? 255 : v);
-      fin[c] = __dadd_rn(__dmul_rn(mt, (double)v), __dmul_rn(omt, fin[c]));
+      fin[c] = d_add(d_mul(mt, (double)v), d_mul(omt, fin[c]));
     }
   }
 #pragma unroll

@@ -22,6 +22,12 @@ import torch
 from .. import _lib
 
 
+def _fstride(t: torch.Tensor) -> int:
+    """Elements between consecutive items of dim 0; for a single item any stride is valid (numpy's a[None] and
+    torch's size-1 dims may report 0), so report the dense size the native checks expect."""
+    return t.stride(0) if t.shape[0] > 1 else int(np.prod(t.shape[1:]))
+
+
 def resize_u8(src: torch.Tensor, size=(224, 224)) -> torch.Tensor:
     """cv2.resize(src, size) INTER_LINEAR for uint8 [F,H,W,3] device images -> [F,size[1],size[0],3]."""
     _lib.require_gpu(src, "resize_u8")
@@ -32,7 +38,7 @@ def resize_u8(src: torch.Tensor, size=(224, 224)) -> torch.Tensor:
     Wd, Hd = size
     dst = torch.empty(F_, Hd, Wd, 3, dtype=torch.uint8, device=src.device)
     if F_:
-        _lib.check(_lib.load().ghost_resize_u8_linear(src.data_ptr(), src.stride(0), F_, Hs, Ws, dst.data_ptr(),
+        _lib.check(_lib.load().ghost_resize_u8_linear(src.data_ptr(), _fstride(src), F_, Hs, Ws, dst.data_ptr(),
                                                       dst.stride(0), Hd, Wd, _lib.stream_ptr(src.device)), "resize_u8")
     return dst
 
@@ -61,8 +67,8 @@ def blend_swaps(frames: torch.Tensor, swaps: torch.Tensor, masks: torch.Tensor, 
     m = m.to(dev, torch.float32).reshape(F_, 6).contiguous()
     v = None if valid is None else valid.to(dev, torch.int32).contiguous()
     lib = _lib.load()
-    _lib.check(lib.ghost_blend_swaps_u8(frames.data_ptr(), frames.stride(0), F_, H, W, swaps.data_ptr(),
-                                        swaps.stride(0), S_h, S_w, masks.data_ptr(), masks.stride(0), m.data_ptr(),
+    _lib.check(lib.ghost_blend_swaps_u8(frames.data_ptr(), _fstride(frames), F_, H, W, swaps.data_ptr(),
+                                        _fstride(swaps), S_h, S_w, masks.data_ptr(), _fstride(masks), m.data_ptr(),
                                         None if v is None else v.data_ptr(), _lib.stream_ptr(dev)), "blend_swaps")
     return frames
 
@@ -99,7 +105,10 @@ def blend_image(full_frame: torch.Tensor, swaps: torch.Tensor, masks: torch.Tens
         swaps = resize_u8(swaps, (224, 224))          # image_processing.py:63
     masks = torch.as_tensor(masks).to(dev)
     if masks.dtype != torch.float64:      # q/255 in float32 -> the float64 q/255.0 numpy computes
-        masks = torch.round(masks.to(torch.float64) * 255.0) / 255.0
+        # a 256-entry table of numpy's correctly rounded q / 255 (torch's device division by a scalar multiplies by
+        # the reciprocal, which is not), indexed by the recovered q
+        lut = torch.from_numpy(np.arange(256, dtype=np.float64) / 255).to(dev)
+        masks = lut[torch.round(masks.to(torch.float32) * 255.0).clamp_(0, 255).to(torch.int64)]
     masks = masks.contiguous()
     if tuple(masks.shape) != (J, 224, 224) or len(tfms) != J:
         raise RuntimeError("ghost_amd: blend_image needs J masks [224,224] and J transforms")
@@ -107,7 +116,7 @@ def blend_image(full_frame: torch.Tensor, swaps: torch.Tensor, masks: torch.Tens
                             np.zeros((0, 6))).to(dev, torch.float64).contiguous()
     H, W = full_frame.shape[:2]
     _lib.check(_lib.load().ghost_blend_image_u8(full_frame.data_ptr(), H, W, swaps.data_ptr(),
-                                                swaps.stride(0) if J else 0, J, 224, masks.data_ptr(),
-                                                masks.stride(0) if J else 0, maps.data_ptr(),
+                                                _fstride(swaps) if J else 0, J, 224, masks.data_ptr(),
+                                                _fstride(masks) if J else 0, maps.data_ptr(),
                                                 _lib.stream_ptr(dev)), "blend_image")
     return full_frame

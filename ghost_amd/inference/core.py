@@ -33,7 +33,8 @@ def transform_target_to_torch(resized_frs: np.ndarray, half: bool = True, device
     dt = torch.float16 if half else torch.float32
     y = torch.empty(B, H, W, 3, dtype=dt, device=device)
     lib = _lib.load()
-    _lib.check(lib.ghost_crops_to_input_nhwc(crops.data_ptr(), crops.stride(0), B, H, W, _lib.gdtype(dt),
+    cstride = crops.stride(0) if B > 1 else H * W * 3
+    _lib.check(lib.ghost_crops_to_input_nhwc(crops.data_ptr(), cstride, B, H, W, _lib.gdtype(dt),
                                              y.data_ptr(), _lib.stream_ptr(device)), "transform_target_to_torch")
     return y.permute(0, 3, 1, 2)
 

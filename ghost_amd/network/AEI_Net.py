@@ -342,7 +342,8 @@ class AEI_Net(PackedModule):
         lib = rt.lib
         stream = _lib.stream_ptr(dev)
         ws = rt.workspace("swap", B, dev, stream)
-        _lib.check(lib.ghost_aei_swap_u8(rt.h, crops_u8.data_ptr(), crops_u8.stride(0), B, z.data_ptr(),
+        cstride = crops_u8.stride(0) if B > 1 else 256 * 256 * 3     # a single crop: any dim-0 stride (a[None])
+        _lib.check(lib.ghost_aei_swap_u8(rt.h, crops_u8.data_ptr(), cstride, B, z.data_ptr(),
                                          _lib.gdtype(z.dtype), zrs, out.data_ptr(), ws.data_ptr(), ws.numel(),
                                          stream), "AEI_Net.swap_u8")
         return out
