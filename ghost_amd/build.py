@@ -43,8 +43,12 @@ def _compile(src: str, force: bool) -> str:
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj
     cmd = [HIPCC] + CFLAGS + ["-c", src, "-o", obj]
+    if os.path.exists(obj):
+        os.remove(obj)            # a failed compile must not leave the old object looking current
     r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
+    # hipcc can report an assembler failure of the device pass ("failed to execute") with exit status 0:
+    # trust the object file, not the status alone
+    if r.returncode != 0 or not os.path.exists(obj) or "failed to execute" in r.stderr:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-4000:]}")
     return obj
 

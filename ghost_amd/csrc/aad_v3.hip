@@ -48,6 +48,7 @@ struct AadV3ArgsT {
   unsigned long long* tclk;
   int v5_xcd;   // v5: blocks in XCD-contiguous order
   int v5_ipw;   // v5: 1024-pixel work items per workgroup
+  int v5_flags; // v5, tuning build only: epilogue A/B (aad_v5_kernel)
 };
 
 static constexpr int kWaves = 8;
@@ -134,13 +135,17 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
   __shared__ __attribute__((aligned(16))) float s_b[L * CT * 128];
   __shared__ __attribute__((aligned(16))) float s_rs[C];
   __shared__ __attribute__((aligned(16))) float s_nm[C];
-  __shared__ __attribute__((aligned(16))) float s_cf[L * C];     // wh * rstd
+  // mask rows: cf_l = wh_l * rstd split in three 16-bit parts (hi, mid, lo), the logits as MFMAs over the h
+  // fragments (see aad_v5_kernel: the split keeps cf to ~2^-26 through the cancellation against s_k)
+  __shared__ __attribute__((aligned(16))) T s_mA[L * 3 * C];
   __shared__ float s_k[L];                                        // sum_c wh * (-mu * rstd)
   __shared__ __attribute__((aligned(16))) float s_gi[L * C];
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
   __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
 
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
+  const int mrow = (lr & 3) == 3 ? 0 : (lr & 3);   // mask A row: part lr & 3 of the split (row 3 repeats hi)
+  const bool relu = a.slope == 0.f;                // the ReLU after every generator AADLayer: one packed max
   const long p_begin = (long)blockIdx.x * a.PPW;
   const int b = (int)(p_begin / a.HW);     // PPW divides HW: one sample per workgroup
   zp_stage_weights<T, L, ZPM, NWV * 64>(a, s_wz, tid);
@@ -152,10 +157,21 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
       *reinterpret_cast<u32x4*>(&s_w[(l * CT * 128 + row) * WLD + kc * 8]) =
           *reinterpret_cast<const u32x4*>(a.w3[l] + (long)row * CA + kc * 8);
     }
-    for (int idx = tid; idx < CT * 128; idx += NWV * 64) s_b[l * CT * 128 + idx] = a.b3[l][idx];
+    // GEMM bias with the identity path folded in: row rho of tile ct (pack_aad_v3) starts from b3 - gi (gamma
+    // rows) or b3 - bi (beta rows) of its channel, so out = I + (1 - M) (D_gamma hh + D_beta)
+    for (int idx = tid; idx < CT * 128; idx += NWV * 64) {
+      const int ct = idx >> 7, rho = idx & 127, i = rho >> 4;
+      const int c = ct * 64 + 32 * ((i >> 1) & 1) + 8 * ((rho >> 2) & 3) + 4 * (i & 1) + (rho & 3);
+      s_b[l * CT * 128 + idx] = a.b3[l][idx] - a.idgb[l][(long)b * a.id_ld + (i < 4 ? c : C + c)];
+    }
     for (int c = tid; c < C; c += NWV * 64) {
-      const float rs = a.stat[((long)b * C + c) * 2 + 1];
-      s_cf[l * C + c] = a.wh[l][c] * rs;
+      const float cf = a.wh[l][c] * a.stat[((long)b * C + c) * 2 + 1];
+      const T hi = (T)cf;
+      const float r1 = cf - (float)hi;
+      const T mid = (T)r1;
+      s_mA[(l * 3) * C + c] = hi;
+      s_mA[(l * 3 + 1) * C + c] = mid;
+      s_mA[(l * 3 + 2) * C + c] = (T)(r1 - (float)mid);
       s_gi[l * C + c] = a.idgb[l][(long)b * a.id_ld + c];
       s_bi[l * C + c] = a.idgb[l][(long)b * a.id_ld + C + c];
     }
@@ -212,32 +228,28 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
         hc[j] = *reinterpret_cast<const u32x4*>(a.hin + p * a.ldh + (j >> 1) * 64 + (j & 1) * 32 + lq * 8);
     }
 
-    // mask partials of every layer over this lane's 8*NH channels, then across the 4 lanes of the pixel
-    float ms[L];
-#pragma unroll
-    for (int l = 0; l < L; ++l) ms[l] = 0.f;
-#pragma unroll
-    for (int j = 0; j < NH; ++j) {
-      const int c0 = (j >> 1) * 64 + (j & 1) * 32 + lq * 8;
-      const T* hv = reinterpret_cast<const T*>(&hc[j]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-#pragma unroll
-        for (int l = 0; l < L; ++l) ms[l] = fmaf(s_cf[l * C + c0 + e], (float)hv[e], ms[l]);
-    }
+    // mask logits: per layer NH MFMAs over the h fragments (chunk j is the B operand of K step j: lane (lr, lq)
+    // holds channels 32 j + 8 lq .. +7 of pixel lr); lane (lr, lq) gets rows 4 lq .. +3 = (hi, mid, lo, hi) . h
     float Mk[L];
 #pragma unroll
     for (int l = 0; l < L; ++l) {
-      float sm = ms[l];
-      sm += __shfl_xor(sm, 16, 64);
-      sm += __shfl_xor(sm, 32, 64);
-      Mk[l] = sigmoidf_ref(sm + bh[l]);
+      f32x4 mac = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < NH; ++j) {
+        v8_t<T> bfr;
+        __builtin_memcpy(&bfr, &hc[j], 16);
+        const v8_t<T> afr = *reinterpret_cast<const v8_t<T>*>(&s_mA[(l * 3 + mrow) * C + j * 32 + lq * 8]);
+        mac = mfma16x16x32<T>(afr, bfr, mac);
+      }
+      Mk[l] = sigmoidf_ref((mac[0] + mac[1]) + mac[2] + bh[l]);
     }
 
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       asm volatile("" ::: "memory");   // one layer's accumulators live at a time
       v8_t<T> xf[2];
+      const float om = 1.f - Mk[l];
+      const f32x2 om2 = {om, om};
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         const T* W = s_w + (l * CT + ct) * 128 * WLD;
@@ -265,23 +277,24 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
           }
           const int j = ct * 2 + sh;
           const int c0 = ct * 64 + sh * 32 + lq * 8;
-          const T* hv = reinterpret_cast<const T*>(&hc[j]);
-          float o[8];
+          u32x4 ow;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float hh = fmaf((float)hv[e], s_rs[c0 + e], s_nm[c0 + e]);
-            const float g = acc[e >> 2][e & 3];
-            const float be = acc[2 + (e >> 2)][e & 3];
-            const float A = fmaf(g, hh, be);
-            const float I = fmaf(s_gi[l * C + c0 + e], hh, s_bi[l * C + c0 + e]);
-            const float v = fmaf(Mk[l], I - A, A);
-            o[e] = v > 0.f ? v : v * a.slope;
+          for (int kk = 0; kk < 4; ++kk) {   // channels c0 + 2kk, c0 + 2kk + 1
+            const int c = c0 + 2 * kk;
+            const f32x2 h2 = fma2(unpack2<T>(hc[j][kk]), *reinterpret_cast<const f32x2*>(&s_rs[c]),
+                                  *reinterpret_cast<const f32x2*>(&s_nm[c]));
+            const f32x2 gg = {acc[kk >> 1][(2 * kk) & 3], acc[kk >> 1][(2 * kk + 1) & 3]};
+            const f32x2 be = {acc[2 + (kk >> 1)][(2 * kk) & 3], acc[2 + (kk >> 1)][(2 * kk + 1) & 3]};
+            const f32x2 D = fma2(gg, h2, be);
+            const f32x2 I = fma2(*reinterpret_cast<const f32x2*>(&s_gi[l * C + c]), h2,
+                                 *reinterpret_cast<const f32x2*>(&s_bi[l * C + c]));
+            const f32x2 v = fma2(om2, D, I);
+            ow[kk] = relu ? relu_pack2<T>(v) : pack2<T>(v.x > 0.f ? v.x : v.x * a.slope, v.y > 0.f ? v.y : v.y * a.slope);
           }
           if (ZPM && ((ZPM >> l) & 1)) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) xf[sh][e] = (T)o[e];
+            __builtin_memcpy(&xf[sh], &ow, 16);
           } else {
-            store16_f(a.out[l] + p * a.ldo[l] + c0, o);
+            *reinterpret_cast<u32x4*>(a.out[l] + p * a.ldo[l] + c0) = ow;
           }
         }
       }
@@ -608,6 +621,17 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 GHOST_DEV void asm_dma16(const void* gp, uint32_t lds_base) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(gp), "s"(lds_base) : "memory", "m0");
 }
+// the same with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset (the saddr form): no
+// 64-bit address arithmetic per lane
+GHOST_DEV void asm_dma16_s(const void* base, uint32_t voff, uint32_t lds_base) {
+  // the base through readfirstlane so that the "s" operand is an SGPR pair (a value the compiler cannot prove
+  // uniform would be handed over in VGPRs)
+  const uint64_t bp = (uint64_t)(uintptr_t)base;
+  const uint64_t sbase = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(bp >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bp);
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" : : "v"(voff), "s"(sbase), "s"(lds_base)
+               : "memory", "m0");
+}
 GHOST_DEV u32x4 asm_lds16(uint32_t addr) {
   u32x4 v;
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
@@ -626,8 +650,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   __shared__ __attribute__((aligned(16))) float s_b[L * 128];
   __shared__ __attribute__((aligned(16))) float s_rs[C];
   __shared__ __attribute__((aligned(16))) float s_nm[C];
-  __shared__ __attribute__((aligned(16))) float s_cf[L * C];
+  // mask rows (round 4): the logits sum_c (wh_c rs_c) h_c of a layer as MFMAs over the tile's h fragments.  Layer
+  // l's rows 3l .. 3l+2 hold cf_l = wh_l rs split into three 16-bit parts: hi = T(cf), mid = T(cf - hi), lo =
+  // T(cf - hi - mid) (each residual exact in fp32): the sum carries cf to ~2^-26, as the fp32 FMA chain did.  Two
+  // parts (~2^-17) were not enough: sum_c cf_c h_c cancels against the mean term k, and the error showed in the
+  // uint8 output.  A row lr reads part lr & 3 of its layer (row 3 repeats part 0), so every lane group gets all
+  // three sums;
+  // every product of two 16-bit values is exact in the fp32 accumulation.
+  __shared__ __attribute__((aligned(16))) T s_mA[L * 3 * C];
   __shared__ float s_k[L];
+  __shared__ __attribute__((aligned(16))) int s_rt[kWaves * 2 * 8];   // per wave its <= 2 row tiles (RowT)
   __shared__ __attribute__((aligned(16))) float s_gi[L * C];
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hA[kWaves * SLOT_B];
@@ -641,6 +673,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, lr = lane & 15,
             lq = lane >> 4;
   if (a.tclk && tid == 0) a.tclk[blockIdx.x] = (unsigned long long)wall_clock64();
+#ifdef GHOST_TUNING
+  // A/B of the round-4 epilogue (tuning build only): bit 0 mask logits by MFMA (else the per-lane FMA chain),
+  // bit 1 the identity path folded into the GEMM bias (else A + M (I - A))
+  const bool mm = (a.v5_flags & 1) != 0, di = (a.v5_flags & 2) != 0;
+  __shared__ __attribute__((aligned(16))) float s_cf[L * C];
+#else
+  constexpr bool mm = true, di = true;
+#endif
   const int H = a.up.H, W = a.up.W, OW = 2 * W;
   const int NCT = OW / 8;                      // 8-column tiles per row tile
   const int RT = 64 / NCT;                     // row tiles per workgroup (host: 1, 2, 4 or 8)
@@ -656,13 +696,31 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       *reinterpret_cast<u32x4*>(&s_w[widx(l * 128 + row, kc * 8)]) =
           *reinterpret_cast<const u32x4*>(a.w3[l] + (long)row * CA + kc * 8);
     }
-    for (int idx = tid; idx < 128; idx += kWaves * 64) s_b[l * 128 + idx] = a.b3[l][idx];
+    // the GEMM bias with the identity path folded in (round 4): row rho (pack_aad_v3: i = rho >> 4 row tile,
+    // gamma for i < 4, channel 32 ((i >> 1) & 1) + 8 ((rho >> 2) & 3) + 4 (i & 1) + (rho & 3)) starts from
+    // b3 - gi (gamma) or b3 - bi (beta), so the accumulators are D = (gamma - gi, beta - bi) and
+    // out = A + M (I - A) = I + (1 - M) (D_gamma hh + D_beta)
+    for (int idx = tid; idx < 128; idx += kWaves * 64) {
+      const int i = idx >> 4, c = 32 * ((i >> 1) & 1) + 8 * ((idx >> 2) & 3) + 4 * (i & 1) + (idx & 3);
+      s_b[l * 128 + idx] = a.b3[l][idx] - (di ? a.idgb[l][(long)b * a.id_ld + (i < 4 ? c : C + c)] : 0.f);
+    }
     for (int c = tid; c < C; c += kWaves * 64) {
-      const float rs = a.stat[((long)b * C + c) * 2 + 1];
-      s_cf[l * C + c] = a.wh[l][c] * rs;
       s_gi[l * C + c] = a.idgb[l][(long)b * a.id_ld + c];
       s_bi[l * C + c] = a.idgb[l][(long)b * a.id_ld + C + c];
+#ifdef GHOST_TUNING
+      s_cf[l * C + c] = a.wh[l][c] * a.stat[((long)b * C + c) * 2 + 1];
+#endif
     }
+  }
+  for (int idx = tid; idx < L * C; idx += kWaves * 64) {
+    const int l = idx / C, c = idx - l * C;
+    const float cf = a.wh[l][c] * a.stat[((long)b * C + c) * 2 + 1];
+    const T hi = (T)cf;
+    const float r1 = cf - (float)hi;
+    const T mid = (T)r1;
+    s_mA[(l * 3) * C + c] = hi;
+    s_mA[(l * 3 + 1) * C + c] = mid;
+    s_mA[(l * 3 + 2) * C + c] = (T)(r1 - (float)mid);
   }
   for (int c = tid; c < C; c += kWaves * 64) {
     const float mu = a.stat[((long)b * C + c) * 2], rs = a.stat[((long)b * C + c) * 2 + 1];
@@ -684,42 +742,76 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 
   const T* src = a.hin + (long)b * H * W * a.ldh;
   const long pimg = (long)b * a.HW;
+  // per-sample bases (wave-uniform, 64-bit once): every per-tile address below is a 32-bit offset inside the
+  // sample (HW * ld < 2^31), so the loop issues no 64-bit multiplies
+  const T* __restrict__ za_b = a.za + pimg * a.lda;
+
   const int ri = lr >> 3, col = lr & 7;        // this lane's pixel: row ri of the row tile, column col
+  const int mrow = (lr & 3) == 3 ? 0 : (lr & 3);   // mask A row: part lr & 3 of the split (row 3 repeats hi)
   const int rtl = wid % RT;                    // this wave's row tile inside a work item
   const int nw = 8 * IPW;                      // tiles per wave: 8 per work item
   const int ox_w = 8 * (wid / RT), ox_step = 64 / RT;   // wave's first column, column step between its tiles
   // row tile of the wave's tile i (item i / 8): q = 0 -> output rows {0, 2H-1}, q >= 1 -> {2q-1, 2q}; its
   // source rows (scalar): sA = y0(oyA); sB = y1(oyA) for a pair, y0(oyB) for the edge tile; and this lane's
   // row: output row offset, y taps as slot rows (top / bottom) and weight
+  // Every field is wave-uniform (SGPRs); a lane's own row (ri) selects between the A / B forms at use.
   struct RowT {
-    int sA, sB, top, bot;
-    long prow, prowA, prowB;   // this lane's output row, the row tile's two rows (pixel offsets)
-    float fly1;
+    int sA, sB;                // the two source rows in the slot (top slot row 0, bottom 1)
+    int prowA, prowB;          // the row tile's two output rows (pixel offsets in the sample)
+    float flyA, flyB;          // y weight of rows A / B
+    int tbA, tbB;              // slot rows of (y0, y1) for rows A / B: bit 0 = top, bit 1 = bottom
   };
-  auto row_tile = [&](int i) {
+  auto row_tile = [&](int g) {   // g: the wave's work item (row tile (g0 + g) * RT + rtl)
     RowT r;
-    const int q = (g0 + (i >> 3)) * RT + rtl;
+    const int q = (g0 + g) * RT + rtl;
     const int oyA = q == 0 ? 0 : 2 * q - 1, oyB = q == 0 ? 2 * H - 1 : 2 * q;
     float rA = a.up.sh * (float)oyA, rB = a.up.sh * (float)oyB;
     asm volatile("" : "+v"(rA), "+v"(rB));
     const int y0A = __builtin_amdgcn_readfirstlane((int)rA), y0B = __builtin_amdgcn_readfirstlane((int)rB);
     r.sA = y0A;
     r.sB = q == 0 ? y0B : y0A + (y0A < H - 1 ? 1 : 0);
-    const int oy = ri ? oyB : oyA;
-    float ry = ri ? rB : rA;
-    const int y0 = (int)ry, y1 = y0 + (y0 < H - 1 ? 1 : 0);
-    r.fly1 = ry - (float)y0;
-    r.top = y0 == r.sA ? 0 : 1;
-    r.bot = y1 == r.sA ? 0 : (y1 == r.sB ? 1 : r.top);
-    r.prow = pimg + (long)oy * OW;
-    r.prowA = pimg + (long)oyA * OW;
-    r.prowB = pimg + (long)oyB * OW;
+    r.flyA = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rA - (float)y0A)));
+    r.flyB = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(rB - (float)y0B)));
+    auto tb = [&](int y0) {
+      const int y1 = y0 + (y0 < H - 1 ? 1 : 0);
+      const int top = y0 == r.sA ? 0 : 1;
+      const int bot = y1 == r.sA ? 0 : (y1 == r.sB ? 1 : top);
+      return top | (bot << 1);
+    };
+    r.tbA = tb(y0A);
+    r.tbB = tb(y0B);
+    r.prowA = oyA * OW;
+    r.prowB = oyB * OW;
+    return r;
+  };
+  // a wave walks at most two row tiles (IPW <= 2, v5_takes): both computed once, selected per tile by the
+  // uniform i >> 3
+  // the wave's (at most two, IPW <= 2) row tiles, computed once into LDS (8 words each) and read back per tile:
+  // holding them in registers across the loop spills, recomputing them costs ~20 VALU per use
+  // (row_tile's readfirstlane needs a wave-uniform argument: one call per row tile, lane 0 stores it)
+  for (int g = 0; g < IPW; ++g) {
+    const RowT r = row_tile(g);
+    if (lane == 0) {
+      int* d = s_rt + (wid * 2 + g) * 8;
+      d[0] = r.sA; d[1] = r.sB; d[2] = r.prowA; d[3] = r.prowB;
+      d[4] = __float_as_int(r.flyA); d[5] = __float_as_int(r.flyB); d[6] = r.tbA; d[7] = r.tbB;
+    }
+  }
+  auto rt_of = [&](int i) -> RowT {
+    const int* d = s_rt + (wid * 2 + (i >> 3)) * 8;
+    const int4 u0 = *reinterpret_cast<const int4*>(d), u1 = *reinterpret_cast<const int4*>(d + 4);
+    RowT r;
+    r.sA = __builtin_amdgcn_readfirstlane(u0.x); r.sB = __builtin_amdgcn_readfirstlane(u0.y);
+    r.prowA = __builtin_amdgcn_readfirstlane(u0.z); r.prowB = __builtin_amdgcn_readfirstlane(u0.w);
+    r.flyA = __int_as_float(__builtin_amdgcn_readfirstlane(u1.x));
+    r.flyB = __int_as_float(__builtin_amdgcn_readfirstlane(u1.y));
+    r.tbA = __builtin_amdgcn_readfirstlane(u1.z); r.tbB = __builtin_amdgcn_readfirstlane(u1.w);
     return r;
   };
 
   // z fragments of tile i (registers) + its 2 x 6 source pixels (DMA into slot `slot` of this wave)
   auto issue = [&](int i, u32x4 (&zc)[KS], unsigned char* slot) {
-    const RowT rt = row_tile(i);
+    const RowT rt = rt_of(i);
     const int ox0 = ox_w + ox_step * (i & 7);
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (ASMW) {
@@ -731,11 +823,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       for (int k = 0; k < KS; ++k) {
         const int piece = k * 64 + lane, px = piece / CPX, c = piece % CPX;
         const int prx = px >> 3, pcx = px & 7;                  // pixel -> (row of the row tile, column)
-        const long pp = (prx ? rt.prowB : rt.prowA) + ox0 + pcx;
-        asm_dma16(a.za + pp * a.lda + ((c ^ (px & (CPX - 1))) * 8), zdst + k * 1024);
+        const int pp = (prx ? rt.prowB : rt.prowA) + ox0 + pcx;
+        asm_dma16_s(za_b, (uint32_t)(pp * a.lda + ((c ^ (px & (CPX - 1))) * 8)) * 2u, zdst + k * 1024);
       }
     } else {
-      const T* zt = a.za + (rt.prow + ox0 + col) * a.lda + lq * 8;
+      const T* zt = za_b + (((ri ? rt.prowB : rt.prowA) + ox0 + col) * a.lda + lq * 8);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) zc[ks] = *reinterpret_cast<const u32x4*>(zt + ks * 32);
     }
@@ -743,30 +835,30 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     float rx = a.up.sw * (float)ox0;
     asm volatile("" : "+v"(rx));
     const int x_lo = __builtin_amdgcn_readfirstlane((int)rx);
-    const T* rowA = src + (long)rt.sA * W * a.ldh;
-    const T* rowB = src + (long)rt.sB * W * a.ldh;
+    const int rowA = rt.sA * W, rowB = rt.sB * W;          // source row starts (pixels in the sample)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       if (k == 1 && lane >= 32) continue;                    // 12 slot pixels x 8 chunks = 96 pieces
       const int qs = k * 8 + (lane >> 3), cl = lane & 7;     // slot pixel / chunk position this lane fills
       const int sr = qs >= SPX, px = qs - (sr ? SPX : 0);
       const int sx = min(x_lo + px, W - 1);
-      const T* gp = (sr ? rowB : rowA) + sx * a.ldh + ((cl ^ (qs & 7)) * 8);
+      const int off = ((sr ? rowB : rowA) + sx) * a.ldh + ((cl ^ (qs & 7)) * 8);
       if constexpr (ASMW)
-        asm_dma16(gp, (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_off(dst + k * 1024)));
+        asm_dma16_s(src, (uint32_t)off * 2u, (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_off(dst + k * 1024)));
       else
-        __builtin_amdgcn_global_load_lds(gp, dst + k * 1024, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(src + off, dst + k * 1024, 16, 0, 0);
     }
 #endif
   };
   // tile i's h_in chunks out of its LDS slot through the bilinear x2
-  auto hload = [&](int i, const unsigned char* slot, u32x4 (&hc)[2], long& p) {
+  auto hload = [&](int i, const unsigned char* slot, u32x4 (&hc)[2], f32x2 (&hh)[8], int& p) {
     const unsigned char* hs = slot + wid * SLOT_B;
-    const RowT rt = row_tile(i);
+    const RowT rt = rt_of(i);
     const int ox0 = ox_w + ox_step * (i & 7);
-    p = rt.prow + ox0 + col;
-    const int top = rt.top, bot = rt.bot;
-    const f32x2 ly0 = {1.f - rt.fly1, 1.f - rt.fly1}, ly1 = {rt.fly1, rt.fly1};
+    p = (ri ? rt.prowB : rt.prowA) + ox0 + col;
+    const int tb = ri ? rt.tbB : rt.tbA, top = tb & 1, bot = tb >> 1;
+    const float fly1 = ri ? rt.flyB : rt.flyA;
+    const f32x2 ly0 = {1.f - fly1, 1.f - fly1}, ly1 = {fly1, fly1};
     float rx0 = a.up.sw * (float)ox0;
     asm volatile("" : "+v"(rx0));
     const int x_lo = __builtin_amdgcn_readfirstlane((int)rx0);
@@ -787,38 +879,62 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       };
       u32x4 r00 = ld(q00), r01 = ld(q01), r10 = ld(q10), r11 = ld(q11);
       if constexpr (ASMW) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r00), "+v"(r01), "+v"(r10), "+v"(r11));
-      T* hv = reinterpret_cast<T*>(&hc[j]);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const f32x2 tp = fma2(lx0, unpack2<T>(r00[k]), lx1 * unpack2<T>(r01[k]));
         const f32x2 bt = fma2(lx0, unpack2<T>(r10[k]), lx1 * unpack2<T>(r11[k]));
         const f32x2 v = fma2(ly0, tp, ly1 * bt);
-        hv[2 * k] = (T)v.x;
-        hv[2 * k + 1] = (T)v.y;
+        hc[j][k] = pack2<T>(v.x, v.y);
+      }
+      // hh = (h - mu) rs of the stored (T-rounded) h, once per tile for both layers
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = j * 32 + lq * 8 + 2 * k;
+        hh[j * 4 + k] = fma2(unpack2<T>(hc[j][k]), *reinterpret_cast<const f32x2*>(&s_rs[c]),
+                             *reinterpret_cast<const f32x2*>(&s_nm[c]));
       }
     }
   };
-  auto compute = [&](const long p, const u32x4 (&zc)[KS], const u32x4 (&hc)[2]) {
-    f32x2 ms[L];
-#pragma unroll
-    for (int l = 0; l < L; ++l) ms[l] = f32x2{0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c0 = j * 32 + lq * 8;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const f32x2 h2 = unpack2<T>(hc[j][k]);
-#pragma unroll
-        for (int l = 0; l < L; ++l) ms[l] = fma2(*reinterpret_cast<const f32x2*>(&s_cf[l * C + c0 + 2 * k]), h2, ms[l]);
-      }
-    }
+  auto compute = [&](const int p, const u32x4 (&zc)[KS], const u32x4 (&hc)[2], const f32x2 (&hh)[8]) {
+    // mask logits: per layer one MFMA per 32-channel half over the h fragments (B operand: lane (lr, lq) holds
+    // channels 32 j + 8 lq .. +7 of pixel lr, the z_attr layout); lane (lr, lq) gets rows 4 lq .. +3 =
+    // (hi, mid, lo, hi) . h of pixel lr (row 3 repeats hi and is not used)
     float Mk[L];
+    if (mm) {
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-      float sm = ms[l].x + ms[l].y;
-      sm += __shfl_xor(sm, 16, 64);
-      sm += __shfl_xor(sm, 32, 64);
-      Mk[l] = sigmoid_fast(sm + bh[l]);
+      for (int l = 0; l < L; ++l) {
+        f32x4 mac = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          v8_t<T> bfr;
+          __builtin_memcpy(&bfr, &hc[j], 16);
+          const v8_t<T> afr = *reinterpret_cast<const v8_t<T>*>(&s_mA[(l * 3 + mrow) * C + j * 32 + lq * 8]);
+          mac = mfma16x16x32<T>(afr, bfr, mac);
+        }
+        Mk[l] = sigmoid_fast((mac[0] + mac[1]) + mac[2] + bh[l]);
+      }
+    } else {
+#ifdef GHOST_TUNING
+      f32x2 ms[L];
+#pragma unroll
+      for (int l = 0; l < L; ++l) ms[l] = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f32x2 h2 = unpack2<T>(hc[j][k]);
+#pragma unroll
+          for (int l = 0; l < L; ++l)
+            ms[l] = fma2(*reinterpret_cast<const f32x2*>(&s_cf[l * C + j * 32 + lq * 8 + 2 * k]), h2, ms[l]);
+        }
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        float sm = ms[l].x + ms[l].y;
+        sm += __shfl_xor(sm, 16, 64);
+        sm += __shfl_xor(sm, 32, 64);
+        Mk[l] = sigmoid_fast(sm + bh[l]);
+      }
+#endif
     }
 #pragma unroll
     for (int l = 0; l < L; ++l) {
@@ -846,37 +962,41 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
           }
         }
         const int c0 = sh * 32 + lq * 8;
-        const f32x2 M2 = {Mk[l], Mk[l]};
-        float o[8];
+        const float om = 1.f - Mk[l];
+        const f32x2 om2 = {om, om};
+        u32x4 ow;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int c = c0 + 2 * k;
-          const f32x2 hh = fma2(unpack2<T>(hc[sh][k]), *reinterpret_cast<const f32x2*>(&s_rs[c]),
-                                *reinterpret_cast<const f32x2*>(&s_nm[c]));
+          const f32x2 h2 = hh[sh * 4 + k];
           const f32x2 gg = {acc[k >> 1][(2 * k) & 3], acc[k >> 1][(2 * k + 1) & 3]};
           const f32x2 be = {acc[2 + (k >> 1)][(2 * k) & 3], acc[2 + (k >> 1)][(2 * k + 1) & 3]};
-          const f32x2 A = fma2(gg, hh, be);
-          const f32x2 I = fma2(*reinterpret_cast<const f32x2*>(&s_gi[l * C + c]), hh,
+          const f32x2 D = fma2(gg, h2, be);
+          const f32x2 I = fma2(*reinterpret_cast<const f32x2*>(&s_gi[l * C + c]), h2,
                                *reinterpret_cast<const f32x2*>(&s_bi[l * C + c]));
-          const f32x2 v = fma2(M2, I - A, A);
+          f32x2 v;
+          if (di) {
+            v = fma2(om2, D, I);
+          } else {   // (tuning build) the A + M (I - A) form on an unfolded bias: D is A here
+            const f32x2 M2 = {Mk[l], Mk[l]};
+            v = fma2(M2, I - D, D);
+          }
           if constexpr (RELU) {
-            o[2 * k] = fmaxf(v.x, 0.f);
-            o[2 * k + 1] = fmaxf(v.y, 0.f);
+            ow[k] = relu_pack2<T>(v);
           } else {
-            o[2 * k] = v.x > 0.f ? v.x : v.x * a.slope;
-            o[2 * k + 1] = v.y > 0.f ? v.y : v.y * a.slope;
+            ow[k] = pack2<T>(v.x > 0.f ? v.x : v.x * a.slope, v.y > 0.f ? v.y : v.y * a.slope);
           }
         }
         if (ZPM && ((ZPM >> l) & 1)) {
           v8_t<T> xf;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) xf[e] = (T)o[e];
+          __builtin_memcpy(&xf, &ow, 16);
           zp_mfma_half(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, sh, zacc, lr, lq);
         } else {
-          store16_f(a.out[l] + p * a.ldo[l] + c0, o);
+          *reinterpret_cast<u32x4*>(a.out[l] + pimg * a.ldo[l] + (p * a.ldo[l] + c0)) = ow;
         }
       }
-      if (ZPM && ((ZPM >> l) & 1)) zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + p * 32, lq);
+      if (ZPM && ((ZPM >> l) & 1))
+        zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + pimg * 32 + p * 32, lq);
     }
   };
 
@@ -902,12 +1022,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       if constexpr (KS == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(zc[0]), "+v"(zc[1]));
       else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(zc[0]));
       u32x4 hc[2];
-      long p;
-      hload(i, cur, hc, p);
+      f32x2 hh[8];
+      int p;
+      hload(i, cur, hc, hh, p);
       asm volatile("" ::: "memory");
       if (i + 1 < nw) issue(i + 1, zn, nxt);
       asm volatile("" ::: "memory");
-      compute(p, zc, hc);
+      compute(p, zc, hc, hh);
     }
   } else {
     for (int i = 0; i < nw; ++i) {
@@ -915,12 +1036,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       unsigned char* nxt = (i & 1) ? s_hA : s_hB;
       asm volatile("" ::: "memory");
       u32x4 hc[2];
-      long p;
-      hload(i, cur, hc, p);
+      f32x2 hh[8];
+      int p;
+      hload(i, cur, hc, hh, p);
       asm volatile("" ::: "memory");
       if (i + 1 < nw) issue(i + 1, zn, nxt);
       asm volatile("" ::: "memory");
-      compute(p, zc, hc);
+      compute(p, zc, hc, hh);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) zc[ks] = zn[ks];
     }
@@ -968,7 +1090,7 @@ static int v5_takes(const AadV3Desc& d, int zpm) {
   if (!use_v5 || !up || d.C != 64 || v3_ppw(d.HW, d.C) != 1024 || d.ldh % 8 || d.up_W % 4 || rt < 1 || rt > 8 ||
       d.up_H % rt || d.up_H < 2 || ipw < 1 || (d.up_H / rt) % ipw || !v5_pairing_ok(up2x_src(d.up_H, d.up_W)))
     return 0;
-  if (!(d.Ca == 64 || d.Ca == 32) || (zpm && d.L != 2)) return 0;
+  if (!(d.Ca == 64 || d.Ca == 32) || (zpm && d.L != 2) || ipw > 2) return 0;   // the kernel holds <= 2 row tiles
   return ipw;
 }
 
@@ -1027,6 +1149,7 @@ static int aad_v3_t(const AadV3Desc& d, hipStream_t s) {
   a.tclk = d.tclk;
   a.v5_xcd = GHOST_KNOB("GHOST_V5_XCD", 1);
   a.v5_ipw = v5_takes(d, zpm);
+  a.v5_flags = GHOST_KNOB("GHOST_V5_FLAGS", 3);
   static const int v5_asm = GHOST_KNOB("GHOST_V5_ASM", 1);
   if (a.v5_ipw) {
     grid = dim3(grid.x / a.v5_ipw);

@@ -111,8 +111,27 @@ template <> GHOST_DEV f32x2 unpack2<_Float16>(unsigned w) {
 // two fp32 -> one 32-bit word of T (round to nearest even, as (T)v)
 template <typename T> GHOST_DEV unsigned pack2(float a, float b) {
   typedef __attribute__((ext_vector_type(2))) T t2;
-  const t2 v = {(T)a, (T)b};
+  // one vector conversion: a single v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32 (two scalar casts became two
+  // conversions and a v_perm_b32)
+  const t2 v = __builtin_convertvector(f32x2{a, b}, t2);
   return __builtin_bit_cast(unsigned, v);
+}
+
+// relu of two fp32 values rounded to T and packed: round first (v_cvt_pk_*), then one packed max on the
+// 16-bit halves — rounding keeps the sign, so relu(round(v)) == round(relu(v)).  bf16 as signed int16: every
+// negative value (and -0) is a negative integer, so max(x, 0) zeroes exactly those (v_pk_max_i16); fp16 with
+// v_pk_max_f16.
+template <typename T> GHOST_DEV unsigned relu_pack2(f32x2 v);
+template <> GHOST_DEV unsigned relu_pack2<bf16>(f32x2 v) {
+  typedef __attribute__((ext_vector_type(2))) short s16x2;
+  const s16x2 x = __builtin_bit_cast(s16x2, pack2<bf16>(v.x, v.y));
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(x, s16x2{0, 0}));
+}
+template <> GHOST_DEV unsigned relu_pack2<_Float16>(f32x2 v) {
+  typedef __attribute__((ext_vector_type(2))) short s16x2;
+  // fp16 as signed int16 orders the same way as bf16 (sign-magnitude with the sign in bit 15)
+  const s16x2 x = __builtin_bit_cast(s16x2, pack2<_Float16>(v.x, v.y));
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(x, s16x2{0, 0}));
 }
 
 // ghost dtype enum of a storage type
