@@ -88,31 +88,26 @@ in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chu
 // materialised bf16 upsample differs from it by storage rounding only.  One pass over the source,
 // ~10 VALU per source pixel and channel instead of ~44 for the four outputs it feeds.
 //
-// up2x_weights_kernel: the six tables (rows then columns) into wt[6][ld], ld >= max(H, W).
-__global__ void up2x_weights_kernel(const Up2xSrc u, float* __restrict__ wt, int ld) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  for (int dim = 0; dim < 2; ++dim) {
-    const int n = dim ? u.W : u.H;
-    const float sc = dim ? u.sw : u.sh;
-    if (s >= n) continue;
-    double w = 0.0, g0 = 0.0, g1 = 0.0;
-    for (int o = max(0, 2 * s - 4); o <= min(2 * n - 1, 2 * s + 4); ++o) {
-      float r = sc * (float)o;
-      asm volatile("" : "+v"(r));
-      const int i0 = (int)r;
-      const float l1 = r - (float)i0, l0 = 1.f - l1;
-      // a(o, i0) = l0, a(o, i0 + 1) = l1 (l1 = 0 at the last source index)
-      const double as = i0 == s ? (double)l0 : (i0 + 1 == s ? (double)l1 : 0.0);
-      const double an = i0 == s ? (double)l1 : 0.0;   // a(o, s + 1) beside a(o, s)
-      w += as;
-      g0 += as * as;
-      g1 += as * an;
-    }
-    float* t = wt + dim * 3 * ld;
-    t[s] = (float)w;
-    t[ld + s] = (float)g0;
-    t[2 * ld + s] = (float)g1;
+// up2x_tap_weights: the three table entries (w, g0, g1) of source index s along one axis of n source points
+// (scale sc).  Round 4: computed by in_stats_up_quad_kernel for its own rows and columns into LDS (a separate
+// table kernel was one more launch per block input).
+GHOST_DEV void up2x_tap_weights(float sc, int n, int s, float& wo, float& g0o, float& g1o) {
+  double w = 0.0, g0 = 0.0, g1 = 0.0;
+  for (int o = max(0, 2 * s - 4); o <= min(2 * n - 1, 2 * s + 4); ++o) {
+    float r = sc * (float)o;
+    asm volatile("" : "+v"(r));
+    const int i0 = (int)r;
+    const float l1 = r - (float)i0, l0 = 1.f - l1;
+    // a(o, i0) = l0, a(o, i0 + 1) = l1 (l1 = 0 at the last source index)
+    const double as = i0 == s ? (double)l0 : (i0 + 1 == s ? (double)l1 : 0.0);
+    const double an = i0 == s ? (double)l1 : 0.0;   // a(o, s + 1) beside a(o, s)
+    w += as;
+    g0 += as * as;
+    g1 += as * an;
   }
+  wo = (float)w;
+  g0o = (float)g0;
+  g1o = (float)g1;
 }
 
 // a workgroup: RB source rows x CPB = 512 / RB source columns of one sample (CPB = min(W, 128)),
@@ -122,21 +117,27 @@ __global__ void up2x_weights_kernel(const Up2xSrc u, float* __restrict__ wt, int
 // wave per SIMD, and the kernel ran at 1.9 TB/s)
 template <typename T>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
-in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, float* __restrict__ part, const Up2xSrc u,
-                        const float* __restrict__ wt, int ld) {
+in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, float* __restrict__ part,
+                        const Up2xSrc u) {
   __shared__ float red[2][32][65];
+  __shared__ float swx[3][128], swy[3][32];   // this workgroup's column / row tap-weight tables
   const int b = blockIdx.z, cg = blockIdx.y, ch = blockIdx.x;
   const int t = threadIdx.x, cc = t & 7, q = t >> 3;
   constexpr int VEC = Vec16<T>::N;
   static_assert(VEC == 8, "16-bit source");
   const int CPB = u.W < 128 ? u.W : 128, RB = 512 / CPB, nxb = u.W / CPB;
-  const int sy = (ch / nxb) * RB + q % RB, sx0 = (ch % nxb) * CPB + (q / RB) * 16;
+  const int cx0 = (ch % nxb) * CPB, ry0 = (ch / nxb) * RB;
+  if (t < CPB) {
+    up2x_tap_weights(u.sw, u.W, cx0 + t, swx[0][t], swx[1][t], swx[2][t]);
+  } else if (t >= 128 && t - 128 < RB) {
+    up2x_tap_weights(u.sh, u.H, ry0 + t - 128, swy[0][t - 128], swy[1][t - 128], swy[2][t - 128]);
+  }
+  __syncthreads();
+  const int sy = ry0 + q % RB, sx0 = cx0 + (q / RB) * 16;
   const T* xb = x + (long)b * u.H * u.W * ldx + cg * 64 + cc * 8;
   float K[8];
   load16_f(xb, K);
-  const float* wyt = wt;
-  const float* wxt = wt + 3 * ld;
-  const float wy = wyt[sy], g0y = wyt[ld + sy], g1y = wyt[2 * ld + sy];
+  const float wy = swy[0][q % RB], g0y = swy[1][q % RB], g1y = swy[2][q % RB];
   const int sy1 = sy + 1 < u.H ? sy + 1 : sy;   // g1y = 0 on the last row
   const T* r0 = xb + (long)sy * u.W * ldx;
   const T* r1 = xb + (long)sy1 * u.W * ldx;
@@ -165,7 +166,7 @@ in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, flo
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const int sx = sx0 + k0 + j;
-      const float wx = wxt[sx], g0x = wxt[ld + sx], g1x = wxt[2 * ld + sx], g1x2 = 2.f * g1x;
+      const float wx = swx[0][sx - cx0], g0x = swx[1][sx - cx0], g1x = swx[2][sx - cx0], g1x2 = 2.f * g1x;
       const T* e0 = reinterpret_cast<const T*>(&nr0[j]);
       const T* e1 = reinterpret_cast<const T*>(&nr1[j]);
 #pragma unroll
@@ -306,11 +307,7 @@ static void in_stats_launch(const T* x, int ldx, int B, int HW, int C, float* st
     if (up && in_stats_up2x_closed_form(gdt<T>(), u.H, u.W, C, ldx)) {
       // closed form over the source: (H / 4) * (W / 128) records <= the HW / 512 reserved
       const int nr = u.H * u.W / 512;   // workgroups of 512 source pixels
-      const int ld = u.H > u.W ? u.H : u.W;
-      float* wt = part + (size_t)B * nr * C * 2;   // 6 x ld floats after the records (workspace slack)
-      hipLaunchKernelGGL(up2x_weights_kernel, dim3((ld + 127) / 128), dim3(128), 0, s, u, wt, ld);
-      hipLaunchKernelGGL(in_stats_up_quad_kernel<T>, dim3(nr, C / 64, B), dim3(256), 0, s, x, ldx, C, nr, part, u, wt,
-                         ld);
+      hipLaunchKernelGGL(in_stats_up_quad_kernel<T>, dim3(nr, C / 64, B), dim3(256), 0, s, x, ldx, C, nr, part, u);
       hipLaunchKernelGGL(in_stats_final_kernel<T>, g2, dim3(256), 0, s, x, ldx, (long)u.H * u.W, B, HW, C, nr, part,
                          stat);
       return;

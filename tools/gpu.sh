@@ -20,6 +20,8 @@
 #   streams:LIST   bench.py quick at --streams N for N in the ','-list     -> gpurun_out/ab_streams.txt
 #   arc:LIST       tools/run_arc.py N for N in the ','-list (ArcFace)      -> gpurun_out/arc_batch.txt
 #   arctrace:N     kernel trace of tools/run_arc.py N (ArcFace)            -> gpurun_out/arc_kt_N.txt
+#   gtrace:DT      kernel trace of eager vs GraphedSwap at B = 1 (DT fp32/bf16) -> gpurun_out/gtrace_DT.txt
+#   mfma           MFMA / VALU PMC passes (tools/pmc_mfma.sh, ROUND=rNN)   -> gpurun_out/rNN_mfma.json
 # Extra bench.py arguments for quick/quick1/ab/knobs/streams: BENCH_ARGS="--opt tap_partials=1".
 # knobs needs the tuning library on the box (GHOST_TUNING=1 python -m ghost_amd.build; list the shipping
 # library in .gpurunignore for that call if the push should carry only one of them).
@@ -69,6 +71,12 @@ for step in "$@"; do
       rm -rf /tmp/at
       timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/at -o run -- python3 tools/run_arc.py $n 5 > "gpurun_out/arc_tr_$n.log" 2>&1; must $?
       python3 tools/kernel_table.py /tmp/at/run_results.db --top 24 > "gpurun_out/arc_kt_$n.txt" 2>&1 ;;
+    gtrace:*)
+      dt="${step#gtrace:}"
+      rm -rf /tmp/gtr
+      timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/gtr -o run -- python3 tools/graph_trace.py $dt > "gpurun_out/gtrace_$dt.txt" 2>&1; must $?
+      python3 tools/graph_trace.py --analyze /tmp/gtr/run_results.db >> "gpurun_out/gtrace_$dt.txt" 2>&1 ;;
+    mfma) bash tools/pmc_mfma.sh; must $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
