@@ -141,10 +141,6 @@ struct Ctx {
   int dev = 0;
   hipStream_t s_up = nullptr;
   char* scratch_up = nullptr;
-  // split-K tile counters (conv_igemm.hip splitk_fixup), one zeroed region per stream: zeroed once per call,
-  // each conv launch leaves them zero again
-  int* cnt = nullptr;
-  int* cnt_up = nullptr;
   int rc = 0;
   std::string where;
 
@@ -201,9 +197,6 @@ struct Ctx {
   }
 };
 
-// split-K tile counters per stream (the largest split grid of the plan: 8x8 stage, 128 x 128 tiles)
-constexpr int kTileCnt = 4096;
-
 // one conv launch (or its workspace accounting in the dry run)
 static const bool g_trace = GHOST_KNOB("GHOST_PLAN_TRACE", 0) != 0;   // one stderr line per launch (tuning builds)
 
@@ -221,8 +214,6 @@ void run_conv(Ctx& c, ConvDesc& d, int cls_all, int cls_big, double flops) {
   const bool big = d.Hi == 256 || d.Hi * (d.kind == CONV_T4S2 ? 2 : 1) == 256;
   int e_all = c.prof_begin(cls_all);
   int e_big = (big && cls_big >= 0) ? c.prof_begin(cls_big) : -1;
-  d.tile_cnt = c.cnt;
-  d.tile_cnt_cap = kTileCnt;
   c.check(conv_launch(d, c.scratch, c.scratch_cap, c.s), "conv_launch");
   double bytes = 0;
   if (d.epi == EPI_AAD) {
@@ -403,13 +394,11 @@ void encoder(Ctx& c, const void* xin, int B, void* const attr[8]) {
   hipStream_t s_main = c.s;
   char* scr_main = c.scratch;
   const bool dual = c.dual && !c.dry;
-  const bool switched = dual && c.ok();
-  if (switched) {
+  if (dual && c.ok()) {
     c.check((int)hipEventRecord(h->zev[0], c.s), "event record");
     c.check((int)hipStreamWaitEvent(c.s_up, h->zev[0], 0), "stream wait");
     c.s = c.s_up;
     c.scratch = c.scratch_up;
-    std::swap(c.cnt, c.cnt_up);
   }
   for (int i = 1; i <= 6; ++i) {
     int Cin, H, Cout, Ho;
@@ -438,7 +427,6 @@ void encoder(Ctx& c, const void* xin, int B, void* const attr[8]) {
     if (c.ok()) c.check((int)hipEventRecord(h->zev[8], c.s), "event record");
     c.s = s_main;
     c.scratch = scr_main;
-    if (switched) std::swap(c.cnt, c.cnt_up);
   }
 }
 
@@ -908,11 +896,6 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
   }
   // network input NHWC with a zero fourth channel: 8-byte (bf16) pixels for the first conv
   void* xin = c.alloc((size_t)B * 256 * 256 * 4 * es);
-  // split-K tile counters of both streams, zeroed here on the caller's stream (before the up path's stream
-  // joins it through zev[1])
-  c.cnt = (int*)c.alloc(2 * kTileCnt * sizeof(int));
-  c.cnt_up = c.cnt + kTileCnt;
-  if (!c.dry && c.ok()) c.check((int)hipMemsetAsync(c.cnt, 0, 2 * kTileCnt * sizeof(int), c.s), "counter memset");
   if (!c.dry && c.ok()) {
     if (mode == M_SWAP)
       c.check(crops_u8_to_input(io.crops, io.crop_bs, B, 256, 256, h->dt, xin, c.s, 4), "crops_u8_to_input");
@@ -937,14 +920,12 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
       if (c.ok()) c.check((int)hipStreamWaitEvent(c.s_up, h->zev[1], 0), "stream wait");
       c.s = c.s_up;
       c.scratch = c.scratch_up;
-      std::swap(c.cnt, c.cnt_up);
     }
     prologue();
     if (!c.dry) {
       if (c.ok()) c.check((int)hipEventRecord(h->zev[1], c.s), "event record");
       c.s = s_main;
       c.scratch = scr_main;
-      std::swap(c.cnt, c.cnt_up);
     }
   }
   encoder(c, xin, B, attr);

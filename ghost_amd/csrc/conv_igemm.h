@@ -59,11 +59,6 @@ struct ConvDesc {
   // it (conv3x3_pp_takes): per (sample, tile, wave, channel) the mean and centred sum of squares of
   // 64 pixels; in_stats_from_tiles() merges them in fp64 into [B][C][2] mean / rstd
   float* in_part = nullptr;
-  // optional split-K tile counters (zeroed ints, >= tiles of the launch; each launch leaves them zero again):
-  // the last split of a tile to finish reduces the partials and applies the epilogue itself (no
-  // splitk_reduce_kernel launch).  Null: the reduction kernel runs.
-  int* tile_cnt = nullptr;
-  int tile_cnt_cap = 0;
 };
 
 // bytes of fp32 split-K workspace the launch may use

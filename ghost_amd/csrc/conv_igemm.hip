@@ -48,8 +48,6 @@ struct ConvArgs {
   float slope;
   int tanh_out;
   int nmajor;           // 1: tiles ordered N-major, so each XCD's contiguous run of tiles shares weight rows
-  int* tile_cnt;        // split-K: per (parity, tile) arrival counters (null: splitk_reduce_kernel reduces)
-  int fix_aad;          // the fixup applies the AAD epilogue (else the standard one)
 };
 
 // ---------------------------------------------------------------------------
@@ -106,63 +104,6 @@ GHOST_DEV long out_pixel(const ConvArgs& a, long m, int py, int px) {
   const int r = (int)(m - (long)b * HW);
   const int qy = r / a.Wo, qx = r - qy * a.Wo;
   return ((long)b * (2 * a.Ho) + 2 * qy + py) * (2 * a.Wo) + 2 * qx + px;
-}
-
-// Split-K fixup (round 4): every split of a tile stores its fp32 partials, then the workgroup whose arrival on
-// the tile's counter is the last one sums all nsplit partials (in split order: deterministic, the bytes of
-// splitk_reduce_kernel) and applies the epilogue — no separate reduction launch.  Hand-off across workgroups
-// and XCDs as MI355X_MICROARCH.md prescribes: producers plain stores -> every storing wave s_waitcnt vmcnt(0) ->
-// barrier -> one lane: agent release fence, vmcnt(0), agent atomic add; the last one (its add returned
-// nsplit - 1): agent acquire fence, vmcnt(0), barrier -> plain loads.  It resets the counter for the next launch
-// on this stream.  tid / nthr: the workgroup's storing threads (the warp-specialised ring: its compute waves).
-template <typename TO>
-GHOST_DEV void splitk_fixup(const ConvArgs& a, int cnt_idx, int m0, int n0, int BM, int BN, int par, int tid,
-                            int nthr) {
-  __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int old = __hip_atomic_fetch_add(a.tile_cnt + cnt_idx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == a.nsplit - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  const int py = par >> 1, px = par & 1;
-  const long sstride = (long)a.M * a.NT;
-  const float* base = a.partial + (long)par * a.nsplit * sstride;
-  if (!a.fix_aad) {
-    for (int idx = tid; idx < BM * BN; idx += nthr) {
-      const int m = m0 + idx / BN, n = n0 + idx % BN;
-      if (m >= a.M || n >= a.N) continue;
-      float v = 0.f;
-      for (int sp = 0; sp < a.nsplit; ++sp) v += base[sp * sstride + (long)m * a.NT + n];
-      const long op = out_pixel(a, m, py, px);
-      store_std<TO>(a, epi_std<TO>(a, v, n, op), n, op);
-    }
-  } else {
-    const int nc = BN / 2;   // AAD channels of the tile: weight columns (gamma, beta) in runs of 16
-    for (int idx = tid; idx < BM * nc; idx += nthr) {
-      const int m = m0 + idx / nc, c = n0 / 2 + idx % nc;
-      if (m >= a.M || c >= a.C_aad) continue;
-      const int ng = (c >> 4) * 32 + (c & 15);
-      float ga = 0.f, ba = 0.f;
-      for (int sp = 0; sp < a.nsplit; ++sp) {
-        ga += base[sp * sstride + (long)m * a.NT + ng];
-        ba += base[sp * sstride + (long)m * a.NT + ng + 16];
-      }
-      ga += a.shift[ng];
-      ba += a.shift[ng + 16];
-      reinterpret_cast<TO*>(a.y)[(long)m * a.ldy + c] = from_f<TO>(epi_aad<TO>(a, ga, ba, c, m));
-    }
-  }
-  if (tid == 0) __hip_atomic_store(a.tile_cnt + cnt_idx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------
@@ -390,9 +331,6 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
         }
       }
     }
-  }
-  if constexpr (EPI == KEPI_SPLIT) {
-    if (a.tile_cnt) splitk_fixup<TO>(a, par * gridDim.x + tile, m0, n0, BM, BN, par, tid, 256);
   }
 }
 
@@ -626,9 +564,6 @@ __global__ void __launch_bounds__(WSL ? 512 : 256) conv_glds_kernel(const ConvAr
       }
     }
   }
-  if constexpr (EPI == KEPI_SPLIT) {
-    if (a.tile_cnt) splitk_fixup<TO>(a, par * gridDim.x + tile, m0, n0, BM, BN, par, tid, 256);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -762,13 +697,6 @@ ConvArgs make_args(const ConvDesc& d, const Plan& p, float* partial) {
   a.nsplit = p.nsplit; a.kt_per_split = p.kt_per_split;
   a.slope = d.slope; a.tanh_out = d.tanh_out;
   a.nmajor = p.stages > 0 ? GHOST_KNOB("GHOST_CONV_NMAJOR", 1) : 0;
-  // in-kernel split-K fixup (splitk_fixup) when the caller provides zeroed tile counters and the GEMM writes
-  // the output type it reads (not the bf16 -> fp32 embedding GEMM, whose kernels are instantiated on the input
-  // type)
-  static const int fixup = GHOST_KNOB("GHOST_SPLITK_FIXUP", 1);
-  const int tiles = p.nMt * p.nNt * p.npar;
-  a.tile_cnt = (fixup && p.nsplit > 1 && d.tile_cnt && tiles <= d.tile_cnt_cap && d.ti == d.to) ? d.tile_cnt : nullptr;
-  a.fix_aad = d.epi == EPI_AAD;
   return a;
 }
 
@@ -874,7 +802,7 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
       const bool ok = p.nsplit > 1 ? launch_glds<TI, KEPI_SPLIT>(a, p, s)
                                    : (d.epi == EPI_AAD ? launch_glds<TI, KEPI_AAD>(a, p, s) : launch_glds<TI, KEPI_STD>(a, p, s));
       if (ok) {
-        if (p.nsplit > 1 && !a.tile_cnt) {
+        if (p.nsplit > 1) {
           const int ncols = d.epi == EPI_AAD ? d.C_aad : d.N;
           const long total = (long)p.M * ncols;
           dim3 grid((unsigned)((total + 255) / 256), 1, p.npar);
@@ -890,7 +818,6 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
   if (p.partial) {
     rc = p.fast ? dispatch_tile<TI, TO, KEPI_SPLIT, true>(a, p, s) : dispatch_tile<TI, TO, KEPI_SPLIT, false>(a, p, s);
     if (rc) return rc;
-    if (a.tile_cnt) return 0;   // the last split of every tile reduced it (splitk_fixup)
     const int ncols = d.epi == EPI_AAD ? d.C_aad : d.N;
     const long total = (long)p.M * ncols;
     dim3 grid((unsigned)((total + 255) / 256), 1, p.npar);

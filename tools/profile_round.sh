@@ -14,7 +14,7 @@
 #                                    roofline.rocprof / traffic / rocprof_agreement cite this same run's files
 set -e
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-ROUND=${ROUND:-r03}
+ROUND=${ROUND:-r04}
 R=/tmp/ghost_prof
 Q='--legs "" --cpu-batches ""'
 rm -rf $R && mkdir -p $R gpurun_out
