@@ -63,9 +63,15 @@ constexpr int ZLD = 64;
 GHOST_DEV int sw64(int row, int k) { return row * 64 + ((((k >> 3) ^ (row & 7)) << 3) | (k & 7)); }
 // the same for 32-element (64-byte) rows: chunks XOR-swizzled by (row >> 1) & 3
 GHOST_DEV int sw32(int row, int k) { return row * 32 + ((((k >> 3) ^ ((row >> 1) & 3)) << 3) | (k & 7)); }
+// 128-element (256-byte, one bank row) rows: chunks XOR-swizzled by row & 15
+GHOST_DEV int sw128(int row, int k) { return row * 128 + ((((k >> 3) ^ (row & 15)) << 3) | (k & 7)); }
+// the weight-row image of the AAD GEMMs (Ca-element rows, unpadded): the A-fragment ds_read_b128 of rows
+// 16 rt + lr, chunk 4 ks + lq meets no bank conflict in any 16-lane group (the Ca + 8 padding these replace
+// was 2-way on half the groups' slots at Ca = 64)
 template <int CA>
 GHOST_DEV int swca(int row, int k) {
-  if constexpr (CA == 64) return sw64(row, k);
+  if constexpr (CA == 128) return sw128(row, k);
+  else if constexpr (CA == 64) return sw64(row, k);
   else return sw32(row, k);
 }
 // LDS slot of layer l's projection rows: only the layers in ZPM are staged
@@ -109,6 +115,26 @@ GHOST_DEV void zp_store_acc(const f32x4 (&acc)[2], _Float16* __restrict__ zrow, 
   }
 }
 
+// The two 32-channel halves of a 64-channel tile of a wave's 16 pixels, as the register epilogue holds them (lane
+// (lr, lq): ow0 = channels 8 lq .. +7, ow1 = 32 + 8 lq .. +7 of pixel lr), stored as whole 128-byte rows: one
+// exchange between lanes lr and lr ^ 8 (DPP row_ror:8, by bank mask) and the first store writes pixels 0-7 (lane:
+// pixel lr & 7, chunk lq + 4 (lr >> 3)), the second pixels 8-15.  Stored as produced, each store instruction wrote
+// 16 half rows, and the stores took 1.4-1.7x the time of their bytes (B = 64 AADBlk7 pair: 240.5 -> 174.5 us).
+// pa / pb: element offsets of the lane's pixel lr & 7 / 8 + (lr & 7) plus the tile's channel base.
+template <typename T>
+GHOST_DEV void store_rows16(T* __restrict__ o, long pa, long pb, int lr, int lq, const u32x4& ow0, const u32x4& ow1) {
+  u32x4 rA, rB;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    // row_ror:8 = 0x128; bank mask 0xC: lanes 8-15 of each 16-lane row take their partner's value, 0x3: lanes 0-7
+    rA[k] = (unsigned)__builtin_amdgcn_update_dpp((int)ow0[k], (int)ow1[k], 0x128, 0xF, 0xC, false);
+    rB[k] = (unsigned)__builtin_amdgcn_update_dpp((int)ow1[k], (int)ow0[k], 0x128, 0xF, 0x3, false);
+  }
+  const int c = (lq + 4 * (lr >> 3)) * 8;
+  *reinterpret_cast<u32x4*>(o + pa + c) = rA;
+  *reinterpret_cast<u32x4*>(o + pb + c) = rB;
+}
+
 template <typename T, int L, int ZPM, int NT>
 GHOST_DEV void zp_stage_weights(const AadV3ArgsT<T>& a, T* s_wz, int tid) {
   if constexpr (ZPM != 0) {
@@ -129,7 +155,7 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
   static_assert(ZPM == 0 || C == 64, "tap partials: C = 64");
   constexpr int CT = C / 64;          // 64-channel tiles
   constexpr int KS = CA / 32;         // MFMA k-steps
-  constexpr int WLD = CA + 8;         // padded LDS weight row (T elements)
+  constexpr int WLD = CA;             // LDS weight row (T elements; chunks swizzled, swca)
   constexpr int NH = CT * 2;          // 16-byte h_in chunks per lane (8 channels each)
   __shared__ __attribute__((aligned(16))) T s_w[L * CT * 128 * WLD];
   __shared__ __attribute__((aligned(16))) float s_b[L * CT * 128];
@@ -154,7 +180,7 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
   for (int l = 0; l < L; ++l) {
     for (int idx = tid; idx < CT * 128 * (CA / 8); idx += NWV * 64) {
       const int row = idx / (CA / 8), kc = idx - row * (CA / 8);
-      *reinterpret_cast<u32x4*>(&s_w[(l * CT * 128 + row) * WLD + kc * 8]) =
+      *reinterpret_cast<u32x4*>(&s_w[swca<CA>(l * CT * 128 + row, kc * 8)]) =
           *reinterpret_cast<const u32x4*>(a.w3[l] + (long)row * CA + kc * 8);
     }
     // GEMM bias with the identity path folded in: row rho of tile ct (pack_aad_v3) starts from b3 - gi (gamma
@@ -214,13 +240,22 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
       const int oy = r / (2 * a.up.W), ox = r - oy * (2 * a.up.W);
       const Up2xTap tp = up2x_tap(a.up, oy, ox);
       const T* src = a.hin + (long)b * a.up.H * a.up.W * a.ldh;
+      // up2x_mix's arithmetic, two channels per packed-fp32 instruction (as aad_v5_kernel's hload)
+      const f32x2 ly0 = {tp.ly0, tp.ly0}, ly1 = {tp.ly1, tp.ly1}, lx0 = {tp.lx0, tp.lx0}, lx1 = {tp.lx1, tp.lx1};
 #pragma unroll
       for (int j = 0; j < NH; ++j) {
-        float v[8];
-        up2x_load16_f(src + (j >> 1) * 64 + (j & 1) * 32 + lq * 8, a.ldh, tp, v);
-        T* hv = reinterpret_cast<T*>(&hc[j]);
+        const T* xc = src + (j >> 1) * 64 + (j & 1) * 32 + lq * 8;
+        const u32x4 r00 = *reinterpret_cast<const u32x4*>(xc + (long)tp.o00 * a.ldh);
+        const u32x4 r01 = *reinterpret_cast<const u32x4*>(xc + (long)tp.o01 * a.ldh);
+        const u32x4 r10 = *reinterpret_cast<const u32x4*>(xc + (long)tp.o10 * a.ldh);
+        const u32x4 r11 = *reinterpret_cast<const u32x4*>(xc + (long)tp.o11 * a.ldh);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) hv[e] = (T)v[e];
+        for (int k = 0; k < 4; ++k) {
+          const f32x2 top = fma2(lx0, unpack2<T>(r00[k]), lx1 * unpack2<T>(r01[k]));
+          const f32x2 bot = fma2(lx0, unpack2<T>(r10[k]), lx1 * unpack2<T>(r11[k]));
+          const f32x2 v = fma2(ly0, top, ly1 * bot);
+          hc[j][k] = pack2<T>(v.x, v.y);
+        }
       }
     } else {
 #pragma unroll
@@ -255,6 +290,7 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
         const T* W = s_w + (l * CT + ct) * 128 * WLD;
         // half sh: row tiles {2sh, 2sh+1} (gamma) and {4+2sh, 5+2sh} (beta) = channels
         // ct*64 + 32sh + 8lq + e of this lane's pixel; one half's accumulators live at a time
+        u32x4 owp[2];
 #pragma unroll
         for (int sh = 0; sh < 2; ++sh) {
           asm volatile("" ::: "memory");
@@ -271,7 +307,7 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int rt = (i & 1) + 2 * sh + 4 * (i >> 1);
-              const v8_t<T> afrag = *reinterpret_cast<const v8_t<T>*>(&W[(rt * 16 + lr) * WLD + ks * 32 + lq * 8]);
+              const v8_t<T> afrag = *reinterpret_cast<const v8_t<T>*>(&W[swca<CA>(rt * 16 + lr, ks * 32 + lq * 8)]);
               acc[i] = mfma16x16x32<T>(afrag, bfrag, acc[i]);
             }
           }
@@ -291,11 +327,12 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
             const f32x2 v = fma2(om2, D, I);
             ow[kk] = relu ? relu_pack2<T>(v) : pack2<T>(v.x > 0.f ? v.x : v.x * a.slope, v.y > 0.f ? v.y : v.y * a.slope);
           }
-          if (ZPM && ((ZPM >> l) & 1)) {
-            __builtin_memcpy(&xf[sh], &ow, 16);
-          } else {
-            *reinterpret_cast<u32x4*>(a.out[l] + p * a.ldo[l] + c0) = ow;
-          }
+          if (ZPM && ((ZPM >> l) & 1)) __builtin_memcpy(&xf[sh], &ow, 16);
+          owp[sh] = ow;
+        }
+        if (!(ZPM && ((ZPM >> l) & 1))) {
+          const long p0 = p - lr + (lr & 7);   // the tile's pixel lr & 7 (pixels are consecutive)
+          store_rows16<T>(a.out[l] + ct * 64, p0 * a.ldo[l], (p0 + 8) * a.ldo[l], lr, lq, owp[0], owp[1]);
         }
       }
       if (ZPM && ((ZPM >> l) & 1))
@@ -641,13 +678,24 @@ GHOST_DEV u32x4 asm_lds16(uint32_t addr) {
 // has zero low bits)
 GHOST_DEV uint32_t lds_off(const void* p) { return (uint32_t)(uintptr_t)p; }
 
-template <typename T, int CA, int L, bool RELU, int ZPM = 0, bool ASMW = false>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v5_kernel(const AadV3ArgsT<T> a) {
-  constexpr int C = 64, KS = CA / 32, SPX = 6, SLOT_B = 2 * SPX * 128;
-  constexpr int WLD = ZPM ? CA : CA + 8;
-  auto widx = [](int row, int k) { return ZPM ? swca<CA>(row, k) : row * (CA + 8) + k; };
-  __shared__ __attribute__((aligned(16))) T s_w[L * 128 * WLD];
-  __shared__ __attribute__((aligned(16))) float s_b[L * 128];
+// C = 64 (AADBlk8, the roofline kernel): 8 waves, two workgroups per CU, double-buffered source slots.
+// C = 128 (AADBlk7's block-input pair, aad_v5_wide_kernel): 16 waves in ONE workgroup per CU (the 74 KB of
+// weight rows staged once per CU instead of twice; 4 waves per SIMD at <= 128 VGPRs), single-buffered slots
+// (a wave reads tile i's slot into registers before it DMAs tile i+1 into it), and hh recomputed per layer
+// (holding both 64-channel tiles' hh would cost 32 VGPRs)
+template <typename T, int CA, int L, bool RELU, int ZPM, bool ASMW, int C>
+GHOST_DEV void aad_v5_body(const AadV3ArgsT<T>& a) {
+  static_assert(C == 64 || (C == 128 && ZPM == 0 && !ASMW), "");
+  constexpr int CT = C / 64, NH = 2 * CT;         // 64-channel tiles; 16-byte h chunks per lane
+  constexpr int NW = C == 64 ? kWaves : 16;       // waves per workgroup
+  constexpr int NBUF = C == 64 ? 2 : 1;           // source slot buffers per wave
+  constexpr int IPWMAX = C == 64 ? 2 : 4;         // work items per workgroup (host: v5_takes)
+  constexpr int CPXH = C / 8;                     // 16-byte chunks per source pixel
+  constexpr int KS = CA / 32, SPX = 6, SLOT_B = 2 * SPX * C * 2;
+  constexpr int WLD = CA;
+  auto widx = [](int row, int k) { return swca<CA>(row, k); };
+  __shared__ __attribute__((aligned(16))) T s_w[L * CT * 128 * WLD];
+  __shared__ __attribute__((aligned(16))) float s_b[L * CT * 128];
   __shared__ __attribute__((aligned(16))) float s_rs[C];
   __shared__ __attribute__((aligned(16))) float s_nm[C];
   // mask rows (round 4): the logits sum_c (wh_c rs_c) h_c of a layer as MFMAs over the tile's h fragments.  Layer
@@ -659,20 +707,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   // every product of two 16-bit values is exact in the fp32 accumulation.
   __shared__ __attribute__((aligned(16))) T s_mA[L * 3 * C];
   __shared__ float s_k[L];
-  __shared__ __attribute__((aligned(16))) int s_rt[kWaves * 2 * 8];   // per wave its <= 2 row tiles (RowT)
+  __shared__ __attribute__((aligned(16))) int s_rt[NW * IPWMAX * 8];  // per wave its <= IPWMAX row tiles (RowT)
   __shared__ __attribute__((aligned(16))) float s_gi[L * C];
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
-  __shared__ __attribute__((aligned(1024))) unsigned char s_hA[kWaves * SLOT_B];
-  __shared__ __attribute__((aligned(1024))) unsigned char s_hB[kWaves * SLOT_B];
+  __shared__ __attribute__((aligned(1024))) unsigned char s_hA[NW * SLOT_B];
+  __shared__ __attribute__((aligned(1024))) unsigned char s_hB[NBUF == 2 ? NW * SLOT_B : 16];
   __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
   // ASMW: each wave's z_attr tile (16 pixels x CA channels), single-buffered: read at the top of tile i, then
   // refilled with tile i+1's by DMA
   constexpr int ZSLOT_B = 16 * CA * 2;
-  __shared__ __attribute__((aligned(1024))) unsigned char s_z[ASMW ? kWaves * ZSLOT_B : 16];
+  __shared__ __attribute__((aligned(1024))) unsigned char s_z[ASMW ? NW * ZSLOT_B : 16];
 
   const int tid = threadIdx.x, wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, lr = lane & 15,
             lq = lane >> 4;
-  if (a.tclk && tid == 0) a.tclk[blockIdx.x] = (unsigned long long)wall_clock64();
+  if (C == 64 && a.tclk && tid == 0) a.tclk[blockIdx.x] = (unsigned long long)wall_clock64();
 #ifdef GHOST_TUNING
   // A/B of the round-4 epilogue (tuning build only): bit 0 mask logits by MFMA (else the per-lane FMA chain),
   // bit 1 the identity path folded into the GEMM bias (else A + M (I - A))
@@ -683,28 +731,30 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #endif
   const int H = a.up.H, W = a.up.W, OW = 2 * W;
   const int NCT = OW / 8;                      // 8-column tiles per row tile
-  const int RT = 64 / NCT;                     // row tiles per workgroup (host: 1, 2, 4 or 8)
+  const int RT = 64 / NCT;                     // row tiles per work item (host: 1, 2, 4 or 8; NW % RT == 0)
   const int wpi = H / RT;                      // 1024-pixel work items per image
   const int IPW = a.v5_ipw;                    // work items per workgroup (consecutive, one image: wpi % IPW == 0)
   const int wi = a.v5_xcd ? xcd_remap((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   const int b = wi * IPW / wpi, g0 = wi * IPW - b * wpi;
-  zp_stage_weights<T, L, ZPM, kWaves * 64>(a, s_wz, tid);
+  zp_stage_weights<T, L, ZPM, NW * 64>(a, s_wz, tid);
 
   for (int l = 0; l < L; ++l) {
-    for (int idx = tid; idx < 128 * (CA / 8); idx += kWaves * 64) {
+    for (int idx = tid; idx < CT * 128 * (CA / 8); idx += NW * 64) {
       const int row = idx / (CA / 8), kc = idx - row * (CA / 8);
-      *reinterpret_cast<u32x4*>(&s_w[widx(l * 128 + row, kc * 8)]) =
+      *reinterpret_cast<u32x4*>(&s_w[widx(l * CT * 128 + row, kc * 8)]) =
           *reinterpret_cast<const u32x4*>(a.w3[l] + (long)row * CA + kc * 8);
     }
     // the GEMM bias with the identity path folded in (round 4): row rho (pack_aad_v3: i = rho >> 4 row tile,
     // gamma for i < 4, channel 32 ((i >> 1) & 1) + 8 ((rho >> 2) & 3) + 4 (i & 1) + (rho & 3)) starts from
     // b3 - gi (gamma) or b3 - bi (beta), so the accumulators are D = (gamma - gi, beta - bi) and
     // out = A + M (I - A) = I + (1 - M) (D_gamma hh + D_beta)
-    for (int idx = tid; idx < 128; idx += kWaves * 64) {
-      const int i = idx >> 4, c = 32 * ((i >> 1) & 1) + 8 * ((idx >> 2) & 3) + 4 * (i & 1) + (idx & 3);
-      s_b[l * 128 + idx] = a.b3[l][idx] - (di ? a.idgb[l][(long)b * a.id_ld + (i < 4 ? c : C + c)] : 0.f);
+    // (C = 128: tile ct's rows ct * 128 + rho, channels ct * 64 + the same)
+    for (int idx = tid; idx < CT * 128; idx += NW * 64) {
+      const int ct = idx >> 7, rho = idx & 127, i = rho >> 4;
+      const int c = ct * 64 + 32 * ((i >> 1) & 1) + 8 * ((rho >> 2) & 3) + 4 * (i & 1) + (rho & 3);
+      s_b[l * CT * 128 + idx] = a.b3[l][idx] - (di ? a.idgb[l][(long)b * a.id_ld + (i < 4 ? c : C + c)] : 0.f);
     }
-    for (int c = tid; c < C; c += kWaves * 64) {
+    for (int c = tid; c < C; c += NW * 64) {
       s_gi[l * C + c] = a.idgb[l][(long)b * a.id_ld + c];
       s_bi[l * C + c] = a.idgb[l][(long)b * a.id_ld + C + c];
 #ifdef GHOST_TUNING
@@ -712,7 +762,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #endif
     }
   }
-  for (int idx = tid; idx < L * C; idx += kWaves * 64) {
+  for (int idx = tid; idx < L * C; idx += NW * 64) {
     const int l = idx / C, c = idx - l * C;
     const float cf = a.wh[l][c] * a.stat[((long)b * C + c) * 2 + 1];
     const T hi = (T)cf;
@@ -722,7 +772,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     s_mA[(l * 3 + 1) * C + c] = mid;
     s_mA[(l * 3 + 2) * C + c] = (T)(r1 - (float)mid);
   }
-  for (int c = tid; c < C; c += kWaves * 64) {
+  for (int c = tid; c < C; c += NW * 64) {
     const float mu = a.stat[((long)b * C + c) * 2], rs = a.stat[((long)b * C + c) * 2 + 1];
     s_rs[c] = rs;
     s_nm[c] = -mu * rs;
@@ -748,9 +798,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 
   const int ri = lr >> 3, col = lr & 7;        // this lane's pixel: row ri of the row tile, column col
   const int mrow = (lr & 3) == 3 ? 0 : (lr & 3);   // mask A row: part lr & 3 of the split (row 3 repeats hi)
+  constexpr int TPI = 64 / NW;                 // tiles per wave and work item (8 or 4)
   const int rtl = wid % RT;                    // this wave's row tile inside a work item
-  const int nw = 8 * IPW;                      // tiles per wave: 8 per work item
-  const int ox_w = 8 * (wid / RT), ox_step = 64 / RT;   // wave's first column, column step between its tiles
+  const int nw = TPI * IPW;                    // tiles per wave
+  const int ox_w = 8 * (wid / RT), ox_step = 8 * (NW / RT);   // wave's first column, column step between its tiles
   // row tile of the wave's tile i (item i / 8): q = 0 -> output rows {0, 2H-1}, q >= 1 -> {2q-1, 2q}; its
   // source rows (scalar): sA = y0(oyA); sB = y1(oyA) for a pair, y0(oyB) for the edge tile; and this lane's
   // row: output row offset, y taps as slot rows (top / bottom) and weight
@@ -784,21 +835,19 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     r.prowB = oyB * OW;
     return r;
   };
-  // a wave walks at most two row tiles (IPW <= 2, v5_takes): both computed once, selected per tile by the
-  // uniform i >> 3
-  // the wave's (at most two, IPW <= 2) row tiles, computed once into LDS (8 words each) and read back per tile:
+  // the wave's (at most IPWMAX, v5_takes) row tiles, computed once into LDS (8 words each) and read back per tile:
   // holding them in registers across the loop spills, recomputing them costs ~20 VALU per use
   // (row_tile's readfirstlane needs a wave-uniform argument: one call per row tile, lane 0 stores it)
   for (int g = 0; g < IPW; ++g) {
     const RowT r = row_tile(g);
     if (lane == 0) {
-      int* d = s_rt + (wid * 2 + g) * 8;
+      int* d = s_rt + (wid * IPWMAX + g) * 8;
       d[0] = r.sA; d[1] = r.sB; d[2] = r.prowA; d[3] = r.prowB;
       d[4] = __float_as_int(r.flyA); d[5] = __float_as_int(r.flyB); d[6] = r.tbA; d[7] = r.tbB;
     }
   }
   auto rt_of = [&](int i) -> RowT {
-    const int* d = s_rt + (wid * 2 + (i >> 3)) * 8;
+    const int* d = s_rt + (wid * IPWMAX + i / TPI) * 8;
     const int4 u0 = *reinterpret_cast<const int4*>(d), u1 = *reinterpret_cast<const int4*>(d + 4);
     RowT r;
     r.sA = __builtin_amdgcn_readfirstlane(u0.x); r.sB = __builtin_amdgcn_readfirstlane(u0.y);
@@ -812,7 +861,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   // z fragments of tile i (registers) + its 2 x 6 source pixels (DMA into slot `slot` of this wave)
   auto issue = [&](int i, u32x4 (&zc)[KS], unsigned char* slot) {
     const RowT rt = rt_of(i);
-    const int ox0 = ox_w + ox_step * (i & 7);
+    const int ox0 = ox_w + ox_step * (i % TPI);
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (ASMW) {
       // z_attr of the tile's 16 pixels into this wave's z slot: piece = lane of instruction k holds pixel
@@ -836,13 +885,15 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     asm volatile("" : "+v"(rx));
     const int x_lo = __builtin_amdgcn_readfirstlane((int)rx);
     const int rowA = rt.sA * W, rowB = rt.sB * W;          // source row starts (pixels in the sample)
+    constexpr int NPC = 2 * SPX * CPXH;                      // slot pieces: 12 pixels x CPXH chunks (96 / 192)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (k == 1 && lane >= 32) continue;                    // 12 slot pixels x 8 chunks = 96 pieces
-      const int qs = k * 8 + (lane >> 3), cl = lane & 7;     // slot pixel / chunk position this lane fills
+    for (int k = 0; k < (NPC + 63) / 64; ++k) {
+      if (k * 64 + 64 > NPC && k * 64 + lane >= NPC) continue;
+      const int piece = k * 64 + lane;
+      const int qs = piece / CPXH, cl = piece % CPXH;       // slot pixel / chunk position this lane fills
       const int sr = qs >= SPX, px = qs - (sr ? SPX : 0);
       const int sx = min(x_lo + px, W - 1);
-      const int off = ((sr ? rowB : rowA) + sx) * a.ldh + ((cl ^ (qs & 7)) * 8);
+      const int off = ((sr ? rowB : rowA) + sx) * a.ldh + ((cl ^ (qs & (CPXH - 1))) * 8);
       if constexpr (ASMW)
         asm_dma16_s(src, (uint32_t)off * 2u, (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_off(dst + k * 1024)));
       else
@@ -851,11 +902,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
 #endif
   };
   // tile i's h_in chunks out of its LDS slot through the bilinear x2
-  auto hload = [&](int i, const unsigned char* slot, u32x4 (&hc)[2], f32x2 (&hh)[8], int& p) {
+  auto hload = [&](int i, const unsigned char* slot, u32x4 (&hc)[NH], f32x2 (&hh)[8], int& p, int& pa, int& pb) {
     const unsigned char* hs = slot + wid * SLOT_B;
     const RowT rt = rt_of(i);
-    const int ox0 = ox_w + ox_step * (i & 7);
-    p = (ri ? rt.prowB : rt.prowA) + ox0 + col;
+    const int ox0 = ox_w + ox_step * (i % TPI);
+    pa = rt.prowA + ox0 + col;   // the lane's column in the tile's rows A and B
+    pb = rt.prowB + ox0 + col;
+    p = ri ? pb : pa;
     const int tb = ri ? rt.tbB : rt.tbA, top = tb & 1, bot = tb >> 1;
     const float fly1 = ri ? rt.flyB : rt.flyA;
     const f32x2 ly0 = {1.f - fly1, 1.f - fly1}, ly1 = {fly1, fly1};
@@ -871,11 +924,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int q10 = bot * SPX + x0 - x_lo, q11 = bot * SPX + x1 - x_lo;
     const f32x2 lx0 = {1.f - flx1, 1.f - flx1}, lx1 = {flx1, flx1};
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NH; ++j) {
       const int ch = j * 4 + lq;
       auto ld = [&](int qq) {
         if constexpr (ASMW) return asm_lds16(lds_off(hs) + qq * 128 + ((ch ^ (qq & 7)) * 16));
-        else return *reinterpret_cast<const u32x4*>(hs + qq * 128 + ((ch ^ (qq & 7)) * 16));
+        else return *reinterpret_cast<const u32x4*>(hs + qq * (C * 2) + ((ch ^ (qq & (CPXH - 1))) * 16));
       };
       u32x4 r00 = ld(q00), r01 = ld(q01), r10 = ld(q10), r11 = ld(q11);
       if constexpr (ASMW) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r00), "+v"(r01), "+v"(r10), "+v"(r11));
@@ -886,7 +939,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
         const f32x2 v = fma2(ly0, tp, ly1 * bt);
         hc[j][k] = pack2<T>(v.x, v.y);
       }
-      // hh = (h - mu) rs of the stored (T-rounded) h, once per tile for both layers
+      // hh = (h - mu) rs of the stored (T-rounded) h, once per tile for both layers (C = 64)
+      if constexpr (CT == 1)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int c = j * 32 + lq * 8 + 2 * k;
@@ -895,7 +949,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       }
     }
   };
-  auto compute = [&](const int p, const u32x4 (&zc)[KS], const u32x4 (&hc)[2], const f32x2 (&hh)[8]) {
+  auto compute = [&](const int p, const int pa, const int pb, const u32x4 (&zc)[KS], const u32x4 (&hc)[NH],
+                     const f32x2 (&hh)[8]) {
     // mask logits: per layer one MFMA per 32-channel half over the h fragments (B operand: lane (lr, lq) holds
     // channels 32 j + 8 lq .. +7 of pixel lr, the z_attr layout); lane (lr, lq) gets rows 4 lq .. +3 =
     // (hi, mid, lo, hi) . h of pixel lr (row 3 repeats hi and is not used)
@@ -905,7 +960,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       for (int l = 0; l < L; ++l) {
         f32x4 mac = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < NH; ++j) {
           v8_t<T> bfr;
           __builtin_memcpy(&bfr, &hc[j], 16);
           const v8_t<T> afr = *reinterpret_cast<const v8_t<T>*>(&s_mA[(l * 3 + mrow) * C + j * 32 + lq * 8]);
@@ -936,67 +991,108 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       }
 #endif
     }
+    // layer l's 32 channels (ct, sh) = hs2 of the lane's pixel: the GEMM rows, the blend, the store (or the tap
+    // partials); h2[k] = hh of channels c0 + 2k, c0 + 2k + 1
+    auto layer_half = [&](const int l, const int hs2, const f32x2 (&h2)[4], f32x4 (&zacc)[2]) -> u32x4 {
+      const int ct = hs2 >> 1, sh = hs2 & 1;
+      const T* Wt = s_w + (l * CT + ct) * 128 * WLD;
+      if constexpr (CT == 1) asm volatile("" ::: "memory");
+      f32x4 acc[4];
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-      asm volatile("" ::: "memory");
-      const T* Wt = s_w + l * 128 * WLD;
-      f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      for (int i4 = 0; i4 < 4; ++i4) {
+        const int rt = (i4 & 1) + 2 * sh + 4 * (i4 >> 1);
+        acc[i4] = *reinterpret_cast<const f32x4*>(&s_b[(l * CT + ct) * 128 + rt * 16 + lq * 4]);
+      }
 #pragma unroll
-      for (int sh = 0; sh < 2; ++sh) {
-        asm volatile("" ::: "memory");
-        f32x4 acc[4];
+      for (int ks = 0; ks < KS; ++ks) {
+        v8_t<T> bfrag;
+        __builtin_memcpy(&bfrag, &zc[ks], 16);
 #pragma unroll
         for (int i4 = 0; i4 < 4; ++i4) {
           const int rt = (i4 & 1) + 2 * sh + 4 * (i4 >> 1);
-          acc[i4] = *reinterpret_cast<const f32x4*>(&s_b[l * 128 + rt * 16 + lq * 4]);
-        }
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          v8_t<T> bfrag;
-          __builtin_memcpy(&bfrag, &zc[ks], 16);
-#pragma unroll
-          for (int i4 = 0; i4 < 4; ++i4) {
-            const int rt = (i4 & 1) + 2 * sh + 4 * (i4 >> 1);
-            const v8_t<T> afrag = *reinterpret_cast<const v8_t<T>*>(&Wt[widx(rt * 16 + lr, ks * 32 + lq * 8)]);
-            acc[i4] = mfma16x16x32<T>(afrag, bfrag, acc[i4]);
-          }
-        }
-        const int c0 = sh * 32 + lq * 8;
-        const float om = 1.f - Mk[l];
-        const f32x2 om2 = {om, om};
-        u32x4 ow;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int c = c0 + 2 * k;
-          const f32x2 h2 = hh[sh * 4 + k];
-          const f32x2 gg = {acc[k >> 1][(2 * k) & 3], acc[k >> 1][(2 * k + 1) & 3]};
-          const f32x2 be = {acc[2 + (k >> 1)][(2 * k) & 3], acc[2 + (k >> 1)][(2 * k + 1) & 3]};
-          const f32x2 D = fma2(gg, h2, be);
-          const f32x2 I = fma2(*reinterpret_cast<const f32x2*>(&s_gi[l * C + c]), h2,
-                               *reinterpret_cast<const f32x2*>(&s_bi[l * C + c]));
-          f32x2 v;
-          if (di) {
-            v = fma2(om2, D, I);
-          } else {   // (tuning build) the A + M (I - A) form on an unfolded bias: D is A here
-            const f32x2 M2 = {Mk[l], Mk[l]};
-            v = fma2(M2, I - D, D);
-          }
-          if constexpr (RELU) {
-            ow[k] = relu_pack2<T>(v);
-          } else {
-            ow[k] = pack2<T>(v.x > 0.f ? v.x : v.x * a.slope, v.y > 0.f ? v.y : v.y * a.slope);
-          }
-        }
-        if (ZPM && ((ZPM >> l) & 1)) {
-          v8_t<T> xf;
-          __builtin_memcpy(&xf, &ow, 16);
-          zp_mfma_half(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, sh, zacc, lr, lq);
-        } else {
-          *reinterpret_cast<u32x4*>(a.out[l] + pimg * a.ldo[l] + (p * a.ldo[l] + c0)) = ow;
+          const v8_t<T> afrag = *reinterpret_cast<const v8_t<T>*>(&Wt[widx(rt * 16 + lr, ks * 32 + lq * 8)]);
+          acc[i4] = mfma16x16x32<T>(afrag, bfrag, acc[i4]);
         }
       }
-      if (ZPM && ((ZPM >> l) & 1))
-        zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + pimg * 32 + p * 32, lq);
+      const int c0 = ct * 64 + sh * 32 + lq * 8;
+      const float om = 1.f - Mk[l];
+      const f32x2 om2 = {om, om};
+      u32x4 ow;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = c0 + 2 * k;
+        const f32x2 gg = {acc[k >> 1][(2 * k) & 3], acc[k >> 1][(2 * k + 1) & 3]};
+        const f32x2 be = {acc[2 + (k >> 1)][(2 * k) & 3], acc[2 + (k >> 1)][(2 * k + 1) & 3]};
+        const f32x2 D = fma2(gg, h2[k], be);
+        const f32x2 I = fma2(*reinterpret_cast<const f32x2*>(&s_gi[l * C + c]), h2[k],
+                             *reinterpret_cast<const f32x2*>(&s_bi[l * C + c]));
+        f32x2 v;
+        if (di) {
+          v = fma2(om2, D, I);
+        } else {   // (tuning build) the A + M (I - A) form on an unfolded bias: D is A here
+          const f32x2 M2 = {Mk[l], Mk[l]};
+          v = fma2(M2, I - D, D);
+        }
+        if constexpr (RELU) {
+          ow[k] = relu_pack2<T>(v);
+        } else {
+          ow[k] = pack2<T>(v.x > 0.f ? v.x : v.x * a.slope, v.y > 0.f ? v.y : v.y * a.slope);
+        }
+      }
+      if (ZPM && ((ZPM >> l) & 1)) {
+        v8_t<T> xf;
+        __builtin_memcpy(&xf, &ow, 16);
+        zp_mfma_half(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, sh, zacc, lr, lq);
+      }
+      return ow;
+    };
+    // channel tile ct of layer l as whole 128-byte rows (store_rows16): row A's 8 pixels, then row B's
+    auto store_rows = [&](const int l, const int ct, const u32x4& ow0, const u32x4& ow1) {
+#ifdef GHOST_TUNING
+      if (a.v5_flags & 4) return;   // (tuning build, bit 2) no output stores: what the stores cost
+#endif
+      store_rows16<T>(a.out[l] + pimg * a.ldo[l] + ct * 64, (long)pa * a.ldo[l], (long)pb * a.ldo[l], lr, lq, ow0, ow1);
+    };
+    if constexpr (CT == 1) {
+      // layer-major: the tap partials of a layer accumulate over its two halves
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        asm volatile("" ::: "memory");
+        f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+        u32x4 ow[2];
+#pragma unroll
+        for (int sh = 0; sh < 2; ++sh) {
+          const f32x2 h2[4] = {hh[sh * 4], hh[sh * 4 + 1], hh[sh * 4 + 2], hh[sh * 4 + 3]};
+          ow[sh] = layer_half(l, sh, h2, zacc);
+        }
+        if (ZPM && ((ZPM >> l) & 1))
+          zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + pimg * 32 + p * 32, lq);
+        else
+          store_rows(l, 0, ow[0], ow[1]);
+      }
+    } else {
+      // C = 128: channel-tile-major, both layers per 64-channel tile, so a tile's hh (16 registers) is computed
+      // once for both layers
+      f32x4 zacc[2];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        asm volatile("" ::: "memory");
+        f32x2 h2[2][4];
+#pragma unroll
+        for (int sh = 0; sh < 2; ++sh)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int c = ct * 64 + sh * 32 + lq * 8 + 2 * k;
+            h2[sh][k] = fma2(unpack2<T>(hc[2 * ct + sh][k]), *reinterpret_cast<const f32x2*>(&s_rs[c]),
+                             *reinterpret_cast<const f32x2*>(&s_nm[c]));
+          }
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+          const u32x4 ow0 = layer_half(l, 2 * ct, h2[0], zacc);
+          const u32x4 ow1 = layer_half(l, 2 * ct + 1, h2[1], zacc);
+          store_rows(l, ct, ow0, ow1);
+        }
+      }
     }
   };
 
@@ -1021,33 +1117,44 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
       }
       if constexpr (KS == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(zc[0]), "+v"(zc[1]));
       else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(zc[0]));
-      u32x4 hc[2];
+      u32x4 hc[NH];
       f32x2 hh[8];
-      int p;
-      hload(i, cur, hc, hh, p);
+      int p, pa, pb;
+      hload(i, cur, hc, hh, p, pa, pb);
       asm volatile("" ::: "memory");
       if (i + 1 < nw) issue(i + 1, zn, nxt);
       asm volatile("" ::: "memory");
-      compute(p, zc, hc, hh);
+      compute(p, pa, pb, zc, hc, hh);
     }
   } else {
     for (int i = 0; i < nw; ++i) {
-      unsigned char* cur = (i & 1) ? s_hB : s_hA;
-      unsigned char* nxt = (i & 1) ? s_hA : s_hB;
+      unsigned char* cur = (NBUF == 2 && (i & 1)) ? s_hB : s_hA;
+      unsigned char* nxt = (NBUF == 2 && !(i & 1)) ? s_hB : s_hA;
       asm volatile("" ::: "memory");
-      u32x4 hc[2];
+      u32x4 hc[NH];
       f32x2 hh[8];
-      int p;
-      hload(i, cur, hc, hh, p);
+      int p, pa, pb;
+      hload(i, cur, hc, hh, p, pa, pb);
+      // one slot buffer: this wave's reads of tile i's slot have returned before tile i+1's DMA refills it
+      if constexpr (NBUF == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       asm volatile("" ::: "memory");
       if (i + 1 < nw) issue(i + 1, zn, nxt);
       asm volatile("" ::: "memory");
-      compute(p, zc, hc, hh);
+      compute(p, pa, pb, zc, hc, hh);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) zc[ks] = zn[ks];
     }
   }
-  if (a.tclk && lane == 0) a.tclk[gridDim.x + blockIdx.x * kWaves + wid] = (unsigned long long)wall_clock64();
+  if (C == 64 && a.tclk && lane == 0) a.tclk[gridDim.x + blockIdx.x * kWaves + wid] = (unsigned long long)wall_clock64();
+}
+
+template <typename T, int CA, int L, bool RELU, int ZPM = 0, bool ASMW = false>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v5_kernel(const AadV3ArgsT<T> a) {
+  aad_v5_body<T, CA, L, RELU, ZPM, ASMW, 64>(a);
+}
+template <typename T, int CA, int L, bool RELU>
+__global__ void __launch_bounds__(1024) aad_v5_wide_kernel(const AadV3ArgsT<T> a) {
+  aad_v5_body<T, CA, L, RELU, 0, false, 128>(a);
 }
 
 // v5's row pairing holds for this source height in fp32 (PyTorch's index arithmetic, as up2x_tap): output
@@ -1087,9 +1194,18 @@ static int v5_takes(const AadV3Desc& d, int zpm) {
   // OW / 8 column tiles must divide the 64 tiles of a 1024-pixel work item (OW in {64 .. 512}) and the
   // work items of an image must cover its H row tiles, IPW at a time
   const int nct = 2 * d.up_W / 8, rt = nct > 0 && 64 % nct == 0 ? 64 / nct : 0;
-  if (!use_v5 || !up || d.C != 64 || v3_ppw(d.HW, d.C) != 1024 || d.ldh % 8 || d.up_W % 4 || rt < 1 || rt > 8 ||
-      d.up_H % rt || d.up_H < 2 || ipw < 1 || (d.up_H / rt) % ipw || !v5_pairing_ok(up2x_src(d.up_H, d.up_W)))
+  if (!use_v5 || !up || d.ldh % 8 || d.up_W % 4 || rt < 1 || rt > 8 || d.up_H < 2 ||
+      !v5_pairing_ok(up2x_src(d.up_H, d.up_W)))
     return 0;
+  if (d.C == 128) {
+    // aad_v5_wide_kernel (AADBlk7's block-input pair): one 16-wave workgroup per CU; four work items per
+    // workgroup by default = one workgroup per CU for B = 64 at 128 x 128 (GHOST_V5W_IPW, A/B knob)
+    static const int use_w = GHOST_KNOB("GHOST_AAD_V5W", 1);
+    static const int ipw_w = GHOST_KNOB("GHOST_V5W_IPW", 4);
+    if (!use_w || zpm || d.Ca != 64 || d.HW % 1024 || d.up_H % rt || ipw_w < 1 || ipw_w > 4 || (d.up_H / rt) % ipw_w) return 0;
+    return ipw_w;
+  }
+  if (d.C != 64 || v3_ppw(d.HW, d.C) != 1024 || ipw < 1 || d.up_H % rt || (d.up_H / rt) % ipw) return 0;
   if (!(d.Ca == 64 || d.Ca == 32) || (zpm && d.L != 2) || ipw > 2) return 0;   // the kernel holds <= 2 row tiles
   return ipw;
 }
@@ -1098,7 +1214,7 @@ int aad_v3_clock_words(const AadV3Desc& d) {
   long grid = (long)d.B * d.HW / v3_ppw(d.HW, d.C);
   int zpm = 0;
   for (int l = 0; l < d.L; ++l) zpm |= d.zw[l] ? 1 << l : 0;
-  if (const int ipw = v5_takes(d, zpm)) grid /= ipw;
+  if (const int ipw = v5_takes(d, zpm)) grid = (long)d.B * d.HW / 1024 / ipw;
   return (int)(grid * (1 + kWaves));
 }
 
@@ -1151,6 +1267,22 @@ static int aad_v3_t(const AadV3Desc& d, hipStream_t s) {
   a.v5_ipw = v5_takes(d, zpm);
   a.v5_flags = GHOST_KNOB("GHOST_V5_FLAGS", 3);
   static const int v5_asm = GHOST_KNOB("GHOST_V5_ASM", 1);
+  if (a.v5_ipw && d.C == 128) {
+    a.PPW = 1024;
+    grid = dim3((unsigned)((long)d.B * d.HW / 1024 / a.v5_ipw));
+#define GHOST_V5W(l)                                                                             \
+    if (d.L == l) {                                                                              \
+      if (d.slope == 0.f)                                                                        \
+        hipLaunchKernelGGL((aad_v5_wide_kernel<T, 64, l, true>), grid, dim3(1024), 0, s, a);      \
+      else                                                                                       \
+        hipLaunchKernelGGL((aad_v5_wide_kernel<T, 64, l, false>), grid, dim3(1024), 0, s, a);     \
+      if (d.version_out) *d.version_out = 5;                                                     \
+      return (int)hipGetLastError();                                                             \
+    }
+    GHOST_V5W(1) GHOST_V5W(2)
+#undef GHOST_V5W
+    return -1;
+  }
   if (a.v5_ipw) {
     grid = dim3(grid.x / a.v5_ipw);
 #define GHOST_V5(ca, l)                                                                          \

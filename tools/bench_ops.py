@@ -165,7 +165,7 @@ def aad_v3_cases(lib, iters):
     ws = torch.empty(512 << 20, dtype=torch.uint8, device=DEV)
     # up: 1 = h_in through the x2 upsample
     for c, ca, n, L, up in [(64, 64, 256, 2, 1), (64, 64, 256, 2, 0), (64, 64, 256, 1, 0),
-                            (128, 64, 128, 1, 0), (128, 64, 128, 2, 0),
+                            (128, 64, 128, 1, 0), (128, 64, 128, 2, 0), (128, 64, 128, 2, 1),
                             (256, 128, 64, 1, 0), (512, 256, 32, 1, 0), (1024, 512 // 2, 16, 1, 0)]:
         hn = n // 2 if up & 1 else n
         zn = n
