@@ -115,26 +115,6 @@ GHOST_DEV void zp_store_acc(const f32x4 (&acc)[2], _Float16* __restrict__ zrow, 
   }
 }
 
-// The two 32-channel halves of a 64-channel tile of a wave's 16 pixels, as the register epilogue holds them (lane
-// (lr, lq): ow0 = channels 8 lq .. +7, ow1 = 32 + 8 lq .. +7 of pixel lr), stored as whole 128-byte rows: one
-// exchange between lanes lr and lr ^ 8 (DPP row_ror:8, by bank mask) and the first store writes pixels 0-7 (lane:
-// pixel lr & 7, chunk lq + 4 (lr >> 3)), the second pixels 8-15.  Stored as produced, each store instruction wrote
-// 16 half rows, and the stores took 1.4-1.7x the time of their bytes (B = 64 AADBlk7 pair: 240.5 -> 174.5 us).
-// pa / pb: element offsets of the lane's pixel lr & 7 / 8 + (lr & 7) plus the tile's channel base.
-template <typename T>
-GHOST_DEV void store_rows16(T* __restrict__ o, long pa, long pb, int lr, int lq, const u32x4& ow0, const u32x4& ow1) {
-  u32x4 rA, rB;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    // row_ror:8 = 0x128; bank mask 0xC: lanes 8-15 of each 16-lane row take their partner's value, 0x3: lanes 0-7
-    rA[k] = (unsigned)__builtin_amdgcn_update_dpp((int)ow0[k], (int)ow1[k], 0x128, 0xF, 0xC, false);
-    rB[k] = (unsigned)__builtin_amdgcn_update_dpp((int)ow1[k], (int)ow0[k], 0x128, 0xF, 0x3, false);
-  }
-  const int c = (lq + 4 * (lr >> 3)) * 8;
-  *reinterpret_cast<u32x4*>(o + pa + c) = rA;
-  *reinterpret_cast<u32x4*>(o + pb + c) = rB;
-}
-
 template <typename T, int L, int ZPM, int NT>
 GHOST_DEV void zp_stage_weights(const AadV3ArgsT<T>& a, T* s_wz, int tid) {
   if constexpr (ZPM != 0) {

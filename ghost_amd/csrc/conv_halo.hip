@@ -665,9 +665,12 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
         gb.y = (unsigned)__shfl_xor((int)sb.y, 16, 64);
         const uint2 a0 = odd ? ga : ov[0], a1 = odd ? ov[1] : ga;
         const uint2 b0 = odd ? gb : ov[2], b1 = odd ? ov[3] : gb;
-        T* yp = ay_ + pix * a.ldy + cur.n0 + (lq & 2) * 4;
-        *reinterpret_cast<u32x4*>(yp + (odd ? 16 : 0)) = u32x4{a0.x, a0.y, a1.x, a1.y};
-        *reinterpret_cast<u32x4*>(yp + (odd ? 48 : 32)) = u32x4{b0.x, b0.y, b1.x, b1.y};
+        // lane lq now holds chunk m = (lq >> 1) + 2 (lq & 1) of pixel q (a) and chunk 4 + m (b): the tile row's
+        // 16 pixels q - lr .. +15 are consecutive, so store_rows16 writes them as 8 whole rows per store
+        static_assert(G::TW % 16 == 0, "a pixel fragment lies in one tile row");
+        const long p0 = pix - lr + (lr & 7);
+        store_rows16<T>(ay_ + cur.n0, p0 * a.ldy, (p0 + 8) * a.ldy, lr, (lq >> 1) + 2 * (lq & 1),
+                        u32x4{a0.x, a0.y, a1.x, a1.y}, u32x4{b0.x, b0.y, b1.x, b1.y});
       }
     }
     if constexpr (STATS) {

@@ -134,6 +134,27 @@ template <> GHOST_DEV unsigned relu_pack2<_Float16>(f32x2 v) {
   return __builtin_bit_cast(unsigned, __builtin_elementwise_max(x, s16x2{0, 0}));
 }
 
+// Whole-row stores of a 16-pixel x 64-channel 16-bit tile held as MFMA epilogues hold it: lane (lr, lq) has ow0 =
+// 16-byte chunk m (channels 8 m .. 8 m + 7, m in 0..3 set by lq) and ow1 = chunk 4 + m of pixel lr.  One exchange
+// between lanes lr and lr ^ 8 (DPP row_ror:8, by bank mask) and the first store writes pixels 0-7 (lane: pixel lr & 7,
+// chunk m + 4 (lr >> 3)), the second pixels 8-15: each store instruction writes 8 whole 128-byte rows instead of 16
+// half rows.  The half-row form took 1.4-1.7x the time of its bytes (B = 64 AADBlk7 pair: 240.5 -> 174.5 us, the
+// same kernel with the stores skipped 115 us; profiles/r04_ab_aad_stores.txt).
+// o + pa / o + pb: the channel-0 element of the lane's pixel lr & 7 / 8 + (lr & 7).
+template <typename T>
+GHOST_DEV void store_rows16(T* __restrict__ o, long pa, long pb, int lr, int m, const u32x4& ow0, const u32x4& ow1) {
+  u32x4 rA, rB;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    // row_ror:8 = 0x128; bank mask 0xC: lanes 8-15 of each 16-lane row take their partner's value, 0x3: lanes 0-7
+    rA[k] = (unsigned)__builtin_amdgcn_update_dpp((int)ow0[k], (int)ow1[k], 0x128, 0xF, 0xC, false);
+    rB[k] = (unsigned)__builtin_amdgcn_update_dpp((int)ow1[k], (int)ow0[k], 0x128, 0xF, 0x3, false);
+  }
+  const int c = (m + 4 * (lr >> 3)) * 8;
+  *reinterpret_cast<u32x4*>(o + pa + c) = rA;
+  *reinterpret_cast<u32x4*>(o + pb + c) = rB;
+}
+
 // ghost dtype enum of a storage type
 template <typename T> constexpr int gdt();
 template <> constexpr int gdt<float>() { return GHOST_F32; }
