@@ -573,24 +573,39 @@ def latency_leg(dev, n=20):
         out[name] = {"latency_ms": round(float(np.median(lat)) * 1e3, 3),
                      "host_ms": round(float(np.median(host)) * 1e3, 3)}
         # the same swap replayed as one HIP graph (ghost_amd.inference.GraphedSwap: inputs copied into the
-        # captured buffers, one hipGraphLaunch; identical bytes)
+        # captured buffers, one hipGraphLaunch; identical bytes) with the plan's two streams (its default) and,
+        # beside it, captured as one chain (two_streams = 0)
         from ghost_amd.inference import GraphedSwap
-        gs = GraphedSwap(G, 1, dev)
-        for _ in range(5):
-            gs(crop, z, out=y)
+        for key, ts in (("graphed", None), ("graphed_one_chain", 0)):
+            gs = GraphedSwap(G, 1, dev, two_streams=ts)
+            for _ in range(5):
+                gs(crop, z, out=y)
+            torch.cuda.synchronize()
+            lat, host = [], []
+            for _ in range(n):
+                t0 = time.perf_counter()
+                gs(crop, z, out=y)
+                t1 = time.perf_counter()
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                host.append(t1 - t0)
+                lat.append(t2 - t0)
+            out[name][key] = {"latency_ms": round(float(np.median(lat)) * 1e3, 3),
+                              "host_ms": round(float(np.median(host)) * 1e3, 3)}
+            del gs
+        # eager with one stream (the plan option two_streams = 0)
+        G.set_option("two_streams", 0)
+        for _ in range(3):
+            G.swap_u8(crop, z, out=y)
         torch.cuda.synchronize()
-        lat, host = [], []
+        lat = []
         for _ in range(n):
             t0 = time.perf_counter()
-            gs(crop, z, out=y)
-            t1 = time.perf_counter()
+            G.swap_u8(crop, z, out=y)
             torch.cuda.synchronize()
-            t2 = time.perf_counter()
-            host.append(t1 - t0)
-            lat.append(t2 - t0)
-        out[name]["graphed"] = {"latency_ms": round(float(np.median(lat)) * 1e3, 3),
-                                "host_ms": round(float(np.median(host)) * 1e3, 3)}
-        del gs, G
+            lat.append(time.perf_counter() - t0)
+        out[name]["one_stream_latency_ms"] = round(float(np.median(lat)) * 1e3, 3)
+        del G
         torch.cuda.empty_cache()
     return out
 

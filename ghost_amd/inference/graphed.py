@@ -9,6 +9,13 @@ replays it with one ``hipGraphLaunch``.  The inputs are copied into the graph's 
 the result is read from its output buffer, so the replay runs the same kernels on the same weights: the
 output bytes are identical to ``swap_u8``'s (tests/test_gpu_pipeline.py).
 
+``two_streams``: the plan option the capture runs with (None: the module's own, 1 by default; the option is set for
+the warm-up and capture and restored afterwards).  With 1 the encoder's up path is a second branch the replay runs
+beside the down path, with 0 the graph is one chain.  The replay issues the nodes back to back, so the two branches'
+small B = 1 kernels overlap more than in an eager call (a rocprofv3 trace of fp32 calls, tools/graph_trace.py: the
+graphed kernels' sum 15.9 ms against 11.1 eager for the same 705 launches), yet the branch form still ended sooner
+on the boxes measured (bench ``config1_latency``: graphed / graphed_one_chain).
+
 The graph holds the module's packed weights and workspace as they were at capture, and the ``GraphedSwap``
 keeps that runtime (its packed weight tensors, native handle and workspace) alive for as long as it lives.  A
 replay after the module was re-packed (``load_state_dict``, ``.to`` / ``.half``, an in-place parameter change,
@@ -23,7 +30,8 @@ import torch
 
 
 class GraphedSwap:
-    def __init__(self, G, B: int, device, z_rows: int = 1, z_dtype: Optional[torch.dtype] = None):
+    def __init__(self, G, B: int, device, z_rows: int = 1, z_dtype: Optional[torch.dtype] = None,
+                 two_streams: Optional[int] = None):
         dev = torch.device(device)
         if z_rows not in (1, B):
             raise ValueError("ghost_amd: z_rows must be 1 or B")
@@ -35,18 +43,27 @@ class GraphedSwap:
         side = torch.cuda.Stream(dev)
         cur = torch.cuda.current_stream(dev)
         side.wait_stream(cur)
-        with torch.cuda.stream(side):       # warm-up outside the capture: packs the weights, creates the
-            for _ in range(2):              # native handle's streams/events, sizes the workspace
+        with torch.cuda.stream(side):           # warm-up outside the capture: packs the weights, creates the
+            G.swap_u8(self.crops, self.z, out=self.out)   # native handle (its options), streams/events, workspace
+        saved = G.get_option("two_streams")
+        if two_streams is not None:
+            G.set_option("two_streams", int(two_streams))
+        try:
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    G.swap_u8(self.crops, self.z, out=self.out)
+            cur.wait_stream(side)
+            torch.cuda.synchronize(dev)
+            self.graph = torch.cuda.CUDAGraph()
+            # a capture stream of its own: the module's workspace cache is keyed by stream, so the captured
+            # workspace (allocated in the graph's private pool) is never handed to an eager call or to another
+            # GraphedSwap
+            self._capture_stream = torch.cuda.Stream(dev)
+            with torch.cuda.graph(self.graph, stream=self._capture_stream):
                 G.swap_u8(self.crops, self.z, out=self.out)
-        cur.wait_stream(side)
-        torch.cuda.synchronize(dev)
-        self.graph = torch.cuda.CUDAGraph()
-        # a capture stream of its own: the module's workspace cache is keyed by stream, so the captured workspace
-        # (allocated in the graph's private pool) is never handed to an eager call or to another GraphedSwap
-        self._capture_stream = torch.cuda.Stream(dev)
-        with torch.cuda.graph(self.graph, stream=self._capture_stream):
-            G.swap_u8(self.crops, self.z, out=self.out)
-        torch.cuda.synchronize(dev)
+            torch.cuda.synchronize(dev)
+        finally:
+            G.set_option("two_streams", saved)
         # the captured kernels read the packed weights of this runtime (and its handle / workspace): hold it
         self._rt = G._rt
 
