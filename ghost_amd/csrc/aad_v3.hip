@@ -1180,10 +1180,15 @@ static int v5_takes(const AadV3Desc& d, int zpm) {
   if (d.C == 128) {
     // aad_v5_wide_kernel (AADBlk7's block-input pair): one 16-wave workgroup per CU; four work items per
     // workgroup by default = one workgroup per CU for B = 64 at 128 x 128 (GHOST_V5W_IPW, A/B knob)
+    // Only where the grid fills the GPU: it is one workgroup per CU, so a small batch (B = 1: 16 work items at
+    // 128 x 128) would run on a few CUs — there the v3 kernel's 512-pixel workgroups spread wider.
     static const int use_w = GHOST_KNOB("GHOST_AAD_V5W", 1);
-    static const int ipw_w = GHOST_KNOB("GHOST_V5W_IPW", 4);
-    if (!use_w || zpm || d.Ca != 64 || d.HW % 1024 || d.up_H % rt || ipw_w < 1 || ipw_w > 4 || (d.up_H / rt) % ipw_w) return 0;
-    return ipw_w;
+    static const int ipw_max = GHOST_KNOB("GHOST_V5W_IPW", 4);
+    if (!use_w || zpm || d.Ca != 64 || d.HW % 1024 || d.up_H % rt) return 0;
+    const long items = (long)d.B * d.HW / 1024;
+    for (int ipw_w = 4; ipw_w >= 1; ipw_w >>= 1)
+      if (ipw_w <= ipw_max && (d.up_H / rt) % ipw_w == 0 && items / ipw_w >= 256) return ipw_w;
+    return 0;
   }
   if (d.C != 64 || v3_ppw(d.HW, d.C) != 1024 || ipw < 1 || d.up_H % rt || (d.up_H / rt) % ipw) return 0;
   if (!(d.Ca == 64 || d.Ca == 32) || (zpm && d.L != 2) || ipw > 2) return 0;   // the kernel holds <= 2 row tiles

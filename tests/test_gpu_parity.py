@@ -674,8 +674,10 @@ def test_conv3x3_narrow_op(lib, dt, cin, cout, H, W, use_res):
                                               (64, 32, 128, 4, 2, 0), (128, 64, 64, 8, 1, 0), (128, 32, 64, 8, 1, 0),
                                               (64, 64, 256, 2, 2, 1), (64, 32, 128, 4, 2, 1), (64, 64, 64, 8, 1, 1),
                                               (128, 64, 128, 2, 1, 1), (128, 32, 64, 8, 1, 1), (128, 64, 128, 2, 2, 0),
-                                              # aad_v5_wide_kernel: AADBlk7's block-input pair (and L = 1), 16 waves
-                                              (128, 64, 128, 2, 2, 1), (128, 64, 64, 4, 2, 1),
+                                              # aad_v5_wide_kernel (taken when B * HW / 1024 >= 256): AADBlk7's
+                                              # block-input pair, L = 1, a 64 x 64 output; B = 2 runs the v3 kernel
+                                              (128, 64, 128, 16, 2, 1), (128, 64, 128, 16, 1, 1), (128, 64, 64, 64, 2, 1),
+                                              (128, 64, 128, 2, 2, 1),
                                               # C = 256: every channel tile in one workgroup
                                               (256, 64, 64, 8, 1, 0),
                                               # aad_wide: one 64-channel tile per workgroup
