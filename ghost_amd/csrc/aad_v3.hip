@@ -1045,10 +1045,14 @@ GHOST_DEV void aad_v5_body(const AadV3ArgsT<T>& a) {
           const f32x2 h2[4] = {hh[sh * 4], hh[sh * 4 + 1], hh[sh * 4 + 2], hh[sh * 4 + 3]};
           ow[sh] = layer_half(l, sh, h2, zacc);
         }
-        if (ZPM && ((ZPM >> l) & 1))
+        if (ZPM && ((ZPM >> l) & 1)) {
+#ifdef GHOST_TUNING
+          if (a.v5_flags & 8) continue;   // (tuning build, bit 3) no tap-partial stores: what they cost
+#endif
           zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + pimg * 32 + p * 32, lq);
-        else
+        } else {
           store_rows(l, 0, ow[0], ow[1]);
+        }
       }
     } else {
       // C = 128: channel-tile-major, both layers per 64-channel tile, so a tile's hh (16 registers) is computed
