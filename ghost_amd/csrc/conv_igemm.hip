@@ -652,16 +652,20 @@ Plan make_plan(const ConvDesc& d) {
     s = d.force_split;
   } else if (p.stages > 0) {
     // deep ring: one resident workgroup per CU; split K until the grid covers the CUs
+    // (GHOST_SPLIT_DEEP: the grid target in workgroups, tuning build)
+    static const int deep_target = GHOST_KNOB("GHOST_SPLIT_DEEP", 256);
+    static const int deep_minks = GHOST_KNOB("GHOST_SPLIT_DEEP_MINK", 8);
     if (tiles < 256 && nk >= 16) {
-      s = (256 + tiles - 1) / tiles;
-      s = s < nk / 8 ? s : nk / 8;
+      s = (deep_target + tiles - 1) / tiles;
+      s = s < nk / deep_minks ? s : nk / deep_minks;
       if (s < 1) s = 1;
     }
   } else if ((tiles < (d.min_wgs > 0 ? d.min_wgs : 256) && nk >= 16) ||
              (d.min_wgs <= 0 && tiles == 256 && nk >= 64)) {
     // one round of 256 tiles with a deep reduction splits in two as well (measured: the 4x4 deconv
     // 2048->512 -26 %, the 16x16 4x4/s2 conv 256->512 -19 %)
-    const int target = 2 * (d.min_wgs > 0 ? d.min_wgs : 256);
+    static const int split_mul = GHOST_KNOB("GHOST_SPLIT_MUL", 2);   // (tuning build) workgroups per CU aimed at
+    const int target = split_mul * (d.min_wgs > 0 ? d.min_wgs : 256);
     s = (target + tiles - 1) / tiles;       // aim for >= 2 workgroups per CU
     s = s < nk / 8 ? s : nk / 8;            // keep >= 8 K steps per split
     if (s < 1) s = 1;
