@@ -573,10 +573,10 @@ def latency_leg(dev, n=20):
         out[name] = {"latency_ms": round(float(np.median(lat)) * 1e3, 3),
                      "host_ms": round(float(np.median(host)) * 1e3, 3)}
         # the same swap replayed as one HIP graph (ghost_amd.inference.GraphedSwap: inputs copied into the
-        # captured buffers, one hipGraphLaunch; identical bytes) with the plan's two streams (its default) and,
-        # beside it, captured as one chain (two_streams = 0)
+        # captured buffers, one hipGraphLaunch; identical bytes) captured as one chain (its default) and, beside
+        # it, with the eager plan's two streams
         from ghost_amd.inference import GraphedSwap
-        for key, ts in (("graphed", None), ("graphed_one_chain", 0)):
+        for key, ts in (("graphed", 0), ("graphed_two_streams", 1)):
             gs = GraphedSwap(G, 1, dev, two_streams=ts)
             for _ in range(5):
                 gs(crop, z, out=y)

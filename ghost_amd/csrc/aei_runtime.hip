@@ -902,8 +902,11 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
     else
       c.check(input_to_nhwc(io.xt_dtype, io.xt, io.st, B, 3, 256, 256, h->dt, xin, c.s, 4), "input_to_nhwc");
   }
-  // the resnet encoder and get_attr run on one stream; the dry run sizes a second scratch region
-  c.dual = h->opt[GHOST_AEI_OPT_TWO_STREAMS] && mode != M_ATTR && !h->resnet && !c.force_single;
+  // the resnet encoder and get_attr run on one stream; the dry run sizes a second scratch region.  Below 8 frames
+  // the plan stays on one stream: at B = 1 the up path's kernels are a few microseconds each and the cross-stream
+  // event hand-offs cost more than the overlap returns — eager B = 1 bf16 took 2.40-2.48 ms with the second stream
+  // on two of three boxes against 1.72-1.80 on one stream on all three (bench config1_latency, round 4)
+  c.dual = h->opt[GHOST_AEI_OPT_TWO_STREAMS] && mode != M_ATTR && !h->resnet && !c.force_single && B >= 8;
   GenIn gin{};
   float* zid32 = nullptr;
   auto prologue = [&]() {

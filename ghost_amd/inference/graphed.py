@@ -9,12 +9,14 @@ replays it with one ``hipGraphLaunch``.  The inputs are copied into the graph's 
 the result is read from its output buffer, so the replay runs the same kernels on the same weights: the
 output bytes are identical to ``swap_u8``'s (tests/test_gpu_pipeline.py).
 
-``two_streams``: the plan option the capture runs with (None: the module's own, 1 by default; the option is set for
-the warm-up and capture and restored afterwards).  With 1 the encoder's up path is a second branch the replay runs
-beside the down path, with 0 the graph is one chain.  The replay issues the nodes back to back, so the two branches'
-small B = 1 kernels overlap more than in an eager call (a rocprofv3 trace of fp32 calls, tools/graph_trace.py: the
-graphed kernels' sum 15.9 ms against 11.1 eager for the same 705 launches), yet the branch form still ended sooner
-on the boxes measured (bench ``config1_latency``: graphed / graphed_one_chain).
+``two_streams`` (default 0): the plan option the capture runs with (set for the warm-up and capture, restored
+afterwards).  With 0 the graph is one chain of kernels; with 1 (the eager default) the encoder's up path is a second
+branch the replay runs beside the down path.  The replay issues the nodes back to back, so the two branches' small
+B = 1 kernels overlap and contend far more than in an eager call (a rocprofv3 trace of the same calls,
+tools/graph_trace.py: the graphed kernels' sum 15.9 ms against 11.1 eager for 705 fp32 launches), and on some boxes
+the branch form replayed far slower than eager (bench ``config1_latency``, round 4: bf16 2.86 ms graphed with two
+branches, 1.72 as one chain, 1.62 eager; fp32 3.82 / 2.15 / 2.08 — round 3 saw the same 2× on fp32).  One chain
+tracked eager on every box measured, so it is the default.
 
 The graph holds the module's packed weights and workspace as they were at capture, and the ``GraphedSwap``
 keeps that runtime (its packed weight tensors, native handle and workspace) alive for as long as it lives.  A
@@ -31,7 +33,7 @@ import torch
 
 class GraphedSwap:
     def __init__(self, G, B: int, device, z_rows: int = 1, z_dtype: Optional[torch.dtype] = None,
-                 two_streams: Optional[int] = None):
+                 two_streams: Optional[int] = 0):
         dev = torch.device(device)
         if z_rows not in (1, B):
             raise ValueError("ghost_amd: z_rows must be 1 or B")

@@ -86,7 +86,8 @@ int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_str
  *                                    z_attr8 upsample) on a second, handle-owned HIP stream, overlapped with
  *                                    the generator's AADBlk k, which waits only for z_attr_k; the caller's
  *                                    stream waits for that stream before the call's last launch, so the
- *                                    ordering seen by the caller is unchanged (0: one stream).  Same results.
+ *                                    ordering seen by the caller is unchanged (0: one stream; batches of
+ *                                    fewer than 8 frames always run on one stream).  Same results.
  *   GHOST_AEI_OPT_TAP_PARTIALS (2):  bf16, C = 64 output block (AADBlk8): the 3x3 conv to 3 channels is
  *                                    contracted in its producers: each AADLayer that feeds it writes the 27
  *                                    per-tap partial sums of its channels (fp16, 32 per pixel) instead of its

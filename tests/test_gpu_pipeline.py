@@ -205,13 +205,13 @@ def test_gather_pipeline_two_batches_in_flight(lib):
 
 @pytest.mark.parametrize("dt,B", [(None, 1), (torch.bfloat16, 1), (torch.bfloat16, 4), (torch.float16, 2)])
 def test_graphed_swap_is_bit_identical(lib, dt, B):
-    """GraphedSwap (one HIP graph replay of the whole native plan, captured with the two-stream plan — the
-    default — or as one chain) gives the bytes of an eager swap_u8, for new inputs copied into the captured buffers
-    on every call; the capture leaves the module's own two_streams option as it was."""
+    """GraphedSwap (one HIP graph replay of the whole native plan, captured as one chain — the default — or with
+    the two-stream plan) gives the bytes of an eager swap_u8, for new inputs copied into the captured buffers on
+    every call; the capture leaves the module's own two_streams option as it was."""
     from ghost_amd.inference import GraphedSwap
     G, _p = model("unet", 2, dt)
     g = GraphedSwap(G, B, DEV)
-    g2 = GraphedSwap(G, B, DEV, two_streams=0)
+    g2 = GraphedSwap(G, B, DEV, two_streams=1)
     assert G.get_option("two_streams") == 1
     for seed in (3, 4):
         crops = torch.from_numpy(aei_ref.make_u8_crops(B, seed)).to(DEV)
