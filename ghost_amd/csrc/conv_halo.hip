@@ -868,6 +868,13 @@ bool convT_halo_supported(const ConvDesc& d) {
   if (d.Hi % HaloTCfg<64>::TIH || d.Wi % HaloTCfg<64>::TIW || d.Kpad < 4 * d.Cin) return false;
   if (!(d.N % 64 == 0 || d.N == 32) || d.Npad < d.N) return false;
   if ((uintptr_t)d.x % 16 || (uintptr_t)d.w % 16 || (uintptr_t)d.y % 8 || (d.res && (uintptr_t)d.res % 8)) return false;
+  // one workgroup per (input tile, 64-channel block) with the whole reduction: a small batch (B = 1: 16-32
+  // workgroups, 53 us per deconv) leaves the GPU idle; there the implicit GEMM splits K over >= 256 workgroups
+  {
+    const int bn = d.N == 32 ? 32 : 64;
+    const long nt = (long)d.B * (d.Hi / HaloTCfg<64>::TIH) * (d.Wi / HaloTCfg<64>::TIW) * ((d.N + bn - 1) / bn);
+    if (nt < 128) return false;
+  }
   return (long)d.Hi * d.Wi * d.ldx < (1L << 31);
 }
 

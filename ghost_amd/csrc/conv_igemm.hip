@@ -347,13 +347,17 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a) {
   const float* base = a.partial + ((long)par * a.nsplit * a.M + m) * a.NT;
   const long sstride = (long)a.M * a.NT;
   if constexpr (EPI == KEPI_STD) {
+    // the slab loads unrolled ahead of the (sequential, order-preserving) sum: a deep split no longer waits
+    // one memory latency per slab
     float v = 0.f;
+#pragma unroll 8
     for (int s = 0; s < a.nsplit; ++s) v += base[s * sstride + c];
     const long op = out_pixel(a, m, py, px);
     store_std<TO>(a, epi_std<TO>(a, v, c, op), c, op);
   } else {
     const int ng = (c >> 4) * 32 + (c & 15);
     float ga = 0.f, ba = 0.f;
+#pragma unroll 8
     for (int s = 0; s < a.nsplit; ++s) {
       ga += base[s * sstride + ng];
       ba += base[s * sstride + ng + 16];
