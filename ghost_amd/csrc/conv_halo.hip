@@ -927,6 +927,15 @@ bool conv3x3_halo_supported(const ConvDesc& d) {
   if ((!halo_exact_wide(d) && !halo_small_ok(d) && !halo_img8(d)) || d.Kpad < 9 * d.Cin || d.Npad < d.N) return false;
   if ((uintptr_t)d.x % 16 || (uintptr_t)d.w % 16 || (uintptr_t)d.y % 8 || (d.res && (uintptr_t)d.res % 8)) return false;
   if ((long)d.Hi * d.Wi * d.ldx >= (1L << 31) || (long)d.Npad * d.Kpad >= (1L << 31)) return false;   // 32-bit offsets
+  // a work item is one (tile, 64-channel block) with the whole 9 x Cin reduction: under 64 of them (B = 1 at 32 x 32,
+  // 512 -> 512: 16 workgroups, 105 us) most CUs idle, and the implicit GEMM's split K spreads the same conv wider
+  if (!halo_img8(d)) {
+    const bool wide = halo_exact_wide(d);
+    const int th = wide ? HaloWide::TH : HaloSmall::TH, tw = wide ? HaloWide::TW : HaloSmall::TW;
+    const long items = (long)d.B * ((d.Hi + th - 1) / th) * ((d.Wi + tw - 1) / tw) * (d.N / 64);
+    static const int min_items = GHOST_KNOB("GHOST_HALO_MIN_ITEMS", 64);
+    if (items < min_items) return false;
+  }
   // measured (tools/bench_ops.py, B = 64): faster than the implicit GEMM at every generator stage
   // from 32x32 up (N = 64 .. 512); GHOST_CONV_HALO_MAXN caps N for A/B runs
   static const int max_n = GHOST_KNOB("GHOST_CONV_HALO_MAXN", 1 << 30);
