@@ -47,6 +47,8 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+from ghost_amd.inference.streams import stream_set  # noqa: E402
+
 try:
     BASELINE_METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 except (OSError, ValueError, KeyError):
@@ -218,6 +220,13 @@ def identity_rows(n, dev):
     return torch.from_numpy(np.random.Generator(np.random.PCG64(1)).normal(size=(n, 512)).astype(np.float32)).to(dev)
 
 
+def compute_streams(dev, n):
+    """The compute streams of n batches in flight: the caller's stream, then the device StreamSet's (streams.py: one
+    fixed set of streams per process, so no leg adds hardware-queue sharing for the legs after it)."""
+    ss = stream_set(dev)
+    return [torch.cuda.current_stream(dev)] + [ss.compute(i) for i in range(1, max(1, n))]
+
+
 def timed(fn, steps, warmup):
     for _ in range(warmup):
         fn()
@@ -245,7 +254,7 @@ def arcface_leg(dev, n, steps, nstreams=1):
     crops = torch.from_numpy(np.random.Generator(np.random.PCG64(5)).integers(0, 256, (n, 224, 224, 3),
                                                                            dtype=np.uint8)).to(dev)
     main = torch.cuda.current_stream(dev)
-    comp = [main] + [torch.cuda.Stream(dev) for _ in range(max(1, nstreams) - 1)]
+    comp = compute_streams(dev, nstreams)
     for c in comp[1:]:
         c.wait_stream(main)
     k = [0]
@@ -277,11 +286,13 @@ def fp16_leg(dev, crops, z, steps, warmup, backbone, nb, nstreams=1):
     G.load_state_dict(make_weights(param_specs(backbone, nb)))
     G = G.to(dev).half()
     zh = z.half()
+    table = G.identity_table(zh)               # the identity's projections once (as the headline)
+    idx = torch.zeros(crops.shape[0], dtype=torch.int32, device=dev)
     B = crops.shape[0]
     ns = max(1, nstreams)
     outs = [torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev) for _ in range(ns)]
     main = torch.cuda.current_stream(dev)
-    comp = [main] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+    comp = compute_streams(dev, ns)
     for c in comp[1:]:
         c.wait_stream(main)
     k = [0]
@@ -289,7 +300,7 @@ def fp16_leg(dev, crops, z, steps, warmup, backbone, nb, nstreams=1):
     def step():
         i = k[0] % ns
         with torch.cuda.stream(comp[i]):
-            G.swap_u8(crops, zh, out=outs[i])
+            G.swap_u8_indexed(crops, table, idx, out=outs[i])
         k[0] += 1
 
     el = timed(step, steps, warmup)
@@ -300,7 +311,7 @@ def fp16_leg(dev, crops, z, steps, warmup, backbone, nb, nstreams=1):
             "dtype": "f16", "frames_per_s": round(B * steps / el, 1), "ms_per_batch": round(el * 1e3 / steps, 3)}
 
 
-def d2h_leg(G, crops, z, steps, nstreams=1):
+def d2h_leg(swap, crops, steps, nstreams=1):
     """Config 2 including faceshifter_run.py:22's .cpu(): each batch's uint8 swaps are copied into a
     pinned host buffer on a copy stream while the next batch is swapped (two device/host slots); with
     nstreams = 2 consecutive batches are swapped on two compute streams (two batches in flight, as the
@@ -309,9 +320,9 @@ def d2h_leg(G, crops, z, steps, nstreams=1):
     B = crops.shape[0]
     outs = [torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev) for _ in range(2)]
     hosts = [torch.empty(B, 256, 256, 3, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
-    copy = torch.cuda.Stream(dev)
+    copy = stream_set(dev).d2h
     main = torch.cuda.current_stream(dev)
-    comp = [main] + [torch.cuda.Stream(dev) for _ in range(max(1, nstreams) - 1)]
+    comp = compute_streams(dev, nstreams)
     for c in comp[1:]:
         c.wait_stream(main)
     done = [torch.cuda.Event() for _ in range(2)]
@@ -324,7 +335,7 @@ def d2h_leg(G, crops, z, steps, nstreams=1):
         if copied[s] is not None:
             cur.wait_event(copied[s])          # the copy still reading this slot
         with torch.cuda.stream(cur):
-            G.swap_u8(crops, z, out=outs[s])
+            swap(crops, outs[s])
         done[s].record(cur)
         with torch.cuda.stream(copy):
             copy.wait_event(done[s])
@@ -353,11 +364,12 @@ def config5_leg(dev, B, steps, warmup, n_ident=4, nstreams=1):
     crops = torch.from_numpy(np.random.Generator(np.random.PCG64(77)).integers(0, 256, size=(B, 256, 256, 3),
                                                                             dtype=np.uint8)).to(dev)
     zs = identity_rows(n_ident, dev)
-    idx = torch.arange(B, device=dev) % n_ident
+    idx = (torch.arange(B, device=dev) % n_ident).to(torch.int32)
+    table = G.identity_table(zs)               # the 4 identities' projections once per video
     ns = max(1, nstreams)
     outs = [torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev) for _ in range(ns)]
     main = torch.cuda.current_stream(dev)
-    comp = [main] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+    comp = compute_streams(dev, ns)
     for c in comp[1:]:
         c.wait_stream(main)
     k = [0]
@@ -365,7 +377,7 @@ def config5_leg(dev, B, steps, warmup, n_ident=4, nstreams=1):
     def step():   # batch k on compute stream k % ns (ns batches in flight, as the headline loop)
         i = k[0] % ns
         with torch.cuda.stream(comp[i]):
-            swap_mixed_identities(crops, idx, zs, G, out=outs[i])
+            swap_mixed_identities(crops, idx, zs, G, out=outs[i], table=table)
         k[0] += 1
 
     el = timed(step, steps, warmup)
@@ -480,7 +492,7 @@ def video_leg(G, dev, n_frames, BS=64, H=1080, W=1920):
     z = identity_rows(1, dev)
     CH = 32
     bufs = [torch.empty(CH, H, W, 3, dtype=torch.uint8, device=dev) for _ in range(2)]
-    s_in, s_out = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    s_in, s_out = stream_set(dev).h2d, stream_set(dev).d2h
     cur = torch.cuda.current_stream(dev)
 
     ev_times = {"masks": [], "blend": []}
@@ -573,10 +585,10 @@ def latency_leg(dev, n=20):
         out[name] = {"latency_ms": round(float(np.median(lat)) * 1e3, 3),
                      "host_ms": round(float(np.median(host)) * 1e3, 3)}
         # the same swap replayed as one HIP graph (ghost_amd.inference.GraphedSwap: inputs copied into the
-        # captured buffers, one hipGraphLaunch; identical bytes) captured as one chain (its default) and, beside
-        # it, with the eager plan's two streams
+        # captured buffers, one hipGraphLaunch; identical bytes); at B = 1 the plan is one chain of kernels
+        # whatever two_streams says (batches under 8 frames run on one stream), so one capture is timed
         from ghost_amd.inference import GraphedSwap
-        for key, ts in (("graphed", 0), ("graphed_two_streams", 1)):
+        for key, ts in (("graphed", 0),):
             gs = GraphedSwap(G, 1, dev, two_streams=ts)
             for _ in range(5):
                 gs(crop, z, out=y)
@@ -700,7 +712,9 @@ def headline_record(world, B, steps, warmup, el, backbone, num_blocks, identitie
                                + (", RCCL all-gather of swapped crops" if world > 1 else ""),
                    "global_batch": world * B, "per_gpu_batch": B, "backbone": backbone,
                    "num_blocks": num_blocks, "identities": max(1, identities),
-                   "parallelism": f"dp{world}", "batches_in_flight": nstreams},
+                   "parallelism": f"dp{world}", "batches_in_flight": nstreams,
+                   "identity_projection": "fc1/fc2/up1 once per source identity (AEI_Net.identity_table, before the "
+                                          "timed region), gathered per sample by identity index in every step"},
     }
 
 
@@ -714,6 +728,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    stream_set(dev)       # the process's streams first, so they hold distinct hardware queues (streams.py)
 
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     G = make_model(a.backbone, a.num_blocks, dt, dev)
@@ -725,16 +740,21 @@ def main():
     rng = np.random.Generator(np.random.PCG64(1000 + rank))
     crops = torch.from_numpy(rng.integers(0, 256, size=(B, 256, 256, 3), dtype=np.uint8)).to(dev)
     zs = identity_rows(max(1, a.identities), dev)
-    if a.identities > 1:      # config 5: per-sample identity rows (dp.swap_mixed_identities)
-        z = zs.index_select(0, torch.arange(B, device=dev) % a.identities).contiguous()
-    else:
-        z = zs[:1]
+    z = zs[:1]
+    # the source identities' projections (every AADLayer's fc1/fc2 and up1) once, before the timed region — once per
+    # identity per video, as a weight pack is once per model; each step gathers its samples' rows by identity index
+    # (config 5: mixed identities in every batch; config 2: one identity, an all-zero index)
+    table = G.identity_table(zs)
+    idx = (torch.arange(B, device=dev) % max(1, a.identities)).to(torch.int32)
+
+    def swap(c, o):
+        return G.swap_u8_indexed(c, table, idx, out=o)
     # swap -> all-gather of the uint8 swaps to every rank; the gather of step k overlaps step k + 1
     # (dp.GatherPipeline; GHOST_DP_OVERLAP=0 gathers synchronously after each step).  --streams 2 (default)
     # keeps two independent batches in flight on two HIP streams: one batch's latency-bound low-resolution
     # stages overlap the other's HBM/MFMA-bound stages (every batch still runs its whole forward)
     from ghost_amd.inference.dp import GatherPipeline
-    pipe = GatherPipeline(lambda c, o: G.swap_u8(c, z, out=o), (B, 256, 256, 3), dev,
+    pipe = GatherPipeline(swap, (B, 256, 256, 3), dev,
                           depth=2 if os.environ.get("GHOST_DP_OVERLAP", "1") != "0" else 1,
                           streams=max(1, a.streams))
 
@@ -763,7 +783,7 @@ def main():
         # per-class breakdown from a separate, untimed pass with one batch at a time (every kernel class
         # bracketed; with batches in flight a class's time would include the other batch's kernels)
         pipe.drain()
-        pipe1 = GatherPipeline(lambda c, o: G.swap_u8(c, z, out=o), (B, 256, 256, 3), dev, depth=pipe.depth,
+        pipe1 = GatherPipeline(swap, (B, 256, 256, 3), dev, depth=pipe.depth,
                                streams=1)
         G.profile(0xFF)
         for _ in range(a.steps):
@@ -905,7 +925,7 @@ def main():
         if legs or multi_legs:
             res["legs"] = dict(multi_legs)
         if "d2h" in legs:
-            res["legs"]["d2h"] = d2h_leg(G, crops, z, a.steps, pipe.nstreams)
+            res["legs"]["d2h"] = d2h_leg(swap, crops, a.steps, pipe.nstreams)
         if "fp16" in legs:
             res["legs"]["fp16"] = fp16_leg(dev, crops, z, a.steps, 3, a.backbone, a.num_blocks, pipe.nstreams)
         if "video" in legs and a.video > 0:

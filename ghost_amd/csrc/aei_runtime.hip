@@ -640,11 +640,12 @@ struct GenIn {
   void* m;
 };
 
-GenIn generator_prologue(Ctx& c, int B, const float* zid32) {
+// idgb_out / m_out: where to write them (the identity table of ghost_aei_identity_table), else the workspace
+GenIn generator_prologue(Ctx& c, int B, const float* zid32, float* idgb_out = nullptr, void* m_out = nullptr) {
   ghost_aei* h = c.h;
   const int es = h->esz;
   // identity projections of every AADLayer at once: idgb[b] = [gamma_id | beta_id] per layer (fc1/fc2)
-  float* idgb = (float*)c.alloc((size_t)B * h->id_total * sizeof(float));
+  float* idgb = idgb_out ? idgb_out : (float*)c.alloc((size_t)B * h->id_total * sizeof(float));
   {
     ConvDesc d;
     d.ti = d.to = GHOST_F32;
@@ -656,7 +657,7 @@ GenIn generator_prologue(Ctx& c, int B, const float* zid32) {
     run_conv(c, d, 7, -1, 2.0 * B * h->id_total * h->c_id);
   }
   // m1 = up1(z_id): ConvT k2 on a 1x1 input == GEMM to [B, 2, 2, 1024] (AEI_Net.py:101,123)
-  void* m = c.alloc((size_t)B * 4 * 1024 * es);
+  void* m = m_out ? m_out : c.alloc((size_t)B * 4 * 1024 * es);
   {
     ConvDesc d;
     d.ti = GHOST_F32; d.to = h->dt;
@@ -874,8 +875,8 @@ void declare_slots(ghost_aei* h) {
   }
 }
 
-// shared driver for forward / get_attr / swap
-enum Mode { M_FORWARD, M_ATTR, M_SWAP };
+// shared driver for forward / get_attr / swap / the identity table
+enum Mode { M_FORWARD, M_ATTR, M_SWAP, M_IDTABLE };
 
 struct Io {
   const void* xt = nullptr; int xt_dtype = 0; int64_t st[4] = {0, 0, 0, 0};
@@ -883,11 +884,26 @@ struct Io {
   const void* zid = nullptr; int zid_dtype = 0; int64_t zid_rs = 0;
   void* y = nullptr; uint8_t* u8 = nullptr;
   void* attr[8] = {nullptr};
+  // identity table (M_IDTABLE writes it; a swap with table != nullptr gathers its rows by idx instead of projecting
+  // z_id): n_ident rows of idgb (id_total fp32) then n_ident rows of m1 (4096 in the handle dtype)
+  void* table = nullptr; int n_ident = 0; const int32_t* idx = nullptr;
 };
+
+// the identity table's layout: [n][id_total] fp32 gamma_id/beta_id rows (256-aligned block), then [n][4096] m1 rows
+size_t table_idgb_bytes(const ghost_aei* h, int n) { return ((size_t)n * h->id_total * 4 + 255) & ~size_t(255); }
+size_t table_bytes(const ghost_aei* h, int n) { return table_idgb_bytes(h, n) + (size_t)n * 4096 * h->esz; }
 
 void plan(Ctx& c, Mode mode, int B, Io io) {
   ghost_aei* h = c.h;
   const int es = h->esz;
+  if (mode == M_IDTABLE) {
+    // the per-identity table: B = identities; the same fp32 z rows and GEMMs as a swap's prologue, written into the
+    // table instead of the workspace (AADLayer.py:28-29 fc1/fc2 and AEI_Net.py:101 up1 on each source embedding once)
+    float* z32 = (float*)c.alloc((size_t)B * h->c_id * sizeof(float));
+    if (!c.dry && c.ok()) c.check(rows_to_f32(io.zid_dtype, io.zid, io.zid_rs, B, h->c_id, z32, c.s), "rows_to_f32");
+    generator_prologue(c, B, z32, (float*)io.table, (char*)io.table + table_idgb_bytes(h, B));
+    return;
+  }
   void* attr[8];
   for (int k = 1; k <= 8; ++k) {
     int C, H;
@@ -911,9 +927,26 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
   float* zid32 = nullptr;
   auto prologue = [&]() {
     zid32 = (float*)c.alloc((size_t)B * h->c_id * sizeof(float));
+    if (io.table) {
+      // per-sample rows of the identity table (one gather launch instead of z -> fp32 and the two projection
+      // GEMMs); the same allocations as the projecting prologue, so the swap workspace size covers both
+      gin.idgb = (float*)c.alloc((size_t)B * h->id_total * sizeof(float));
+      gin.m = c.alloc((size_t)B * 4 * 1024 * es);
+      if (c.dry || !c.ok()) return;
+      const void* tab[2] = {io.table, (const char*)io.table + table_idgb_bytes(h, io.n_ident)};
+      const int64_t rb[2] = {(int64_t)h->id_total * 4, (int64_t)4096 * es};
+      void* outs[2] = {gin.idgb, gin.m};
+      int e = c.prof_begin(7);
+      c.check(gather_identity_rows(2, tab, rb, outs, io.n_ident, io.idx, B, c.s), "gather_identity_rows");
+      c.prof_end(7, e, (double)B * (rb[0] + rb[1]) * 2, 0);
+      return;
+    }
     if (!c.dry && c.ok()) c.check(rows_to_f32(io.zid_dtype, io.zid, io.zid_rs, B, h->c_id, zid32, c.s), "rows_to_f32");
     gin = generator_prologue(c, B, zid32);
   };
+  // the identity table's gather runs on the caller's stream, first: identity_index may be a temporary the caller
+  // frees stream-ordered on that stream right after this call
+  if (mode != M_ATTR && io.table) prologue();
   if (mode != M_ATTR && c.dual) {
     // up-path stream: z_id -> idgb, m1 first (overlapping the down path), then the encoder's up path
     hipStream_t s_main = c.s;
@@ -924,7 +957,7 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
       c.s = c.s_up;
       c.scratch = c.scratch_up;
     }
-    prologue();
+    if (!io.table) prologue();
     if (!c.dry) {
       if (c.ok()) c.check((int)hipEventRecord(h->zev[1], c.s), "event record");
       c.s = s_main;
@@ -933,7 +966,7 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
   }
   encoder(c, xin, B, attr);
   if (mode == M_ATTR) return;
-  if (!c.dual) prologue();
+  if (!c.dual && !io.table) prologue();
   void* y = (mode == M_SWAP) ? c.alloc((size_t)B * 256 * 256 * 3 * es) : io.y;
   generator(c, B, attr, gin, y, io.u8);
   // the caller's stream waits for everything this call queued on the up-path stream, also when a launch
@@ -1157,6 +1190,42 @@ extern "C" int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t cro
   Io io;
   io.crops = crops; io.crop_bs = crop_batch_stride;
   io.zid = z_id; io.zid_dtype = zid_dtype; io.zid_rs = zid_row_stride;
+  io.u8 = out_u8;
+  return run(h, M_SWAP, B, io, ws, ws_bytes, stream);
+}
+
+extern "C" int64_t ghost_aei_identity_table_bytes(ghost_aei* h, int n_ident) {
+  if (!h || n_ident <= 0) return fail(GHOST_EINVAL, "bad argument");
+  return (int64_t)table_bytes(h, n_ident);
+}
+
+extern "C" int64_t ghost_aei_identity_table_workspace_bytes(ghost_aei* h, int n_ident) {
+  if (!h || n_ident <= 0) return fail(GHOST_EINVAL, "bad argument");
+  return plan_bytes(h, M_IDTABLE, n_ident);
+}
+
+extern "C" int ghost_aei_identity_table(ghost_aei* h, const void* z_id, int zid_dtype, int64_t zid_row_stride,
+                                        int n_ident, void* table, int64_t table_bytes_, void* ws, int64_t ws_bytes,
+                                        void* stream) {
+  if (!z_id || !table) return fail(GHOST_EINVAL, "null argument");
+  if (!h || n_ident <= 0) return fail(GHOST_EINVAL, "bad argument");
+  if ((uintptr_t)table % 256) return fail(GHOST_EINVAL, "identity table must be 256-byte aligned");
+  if (table_bytes_ < (int64_t)table_bytes(h, n_ident)) return fail(GHOST_EINVAL, "identity table too small");
+  Io io;
+  io.zid = z_id; io.zid_dtype = zid_dtype; io.zid_rs = zid_row_stride;
+  io.table = table; io.n_ident = n_ident;
+  return run(h, M_IDTABLE, n_ident, io, ws, ws_bytes, stream);
+}
+
+extern "C" int ghost_aei_swap_u8_indexed(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_stride, int B,
+                                         const void* table, int n_ident, const int32_t* identity_index,
+                                         uint8_t* out_u8, void* ws, int64_t ws_bytes, void* stream) {
+  if (!crops || !table || !identity_index || !out_u8) return fail(GHOST_EINVAL, "null argument");
+  if (n_ident <= 0) return fail(GHOST_EINVAL, "n_ident must be positive");
+  if ((uintptr_t)table % 256) return fail(GHOST_EINVAL, "identity table must be 256-byte aligned");
+  Io io;
+  io.crops = crops; io.crop_bs = crop_batch_stride;
+  io.table = const_cast<void*>(table); io.n_ident = n_ident; io.idx = identity_index;
   io.u8 = out_u8;
   return run(h, M_SWAP, B, io, ws, ws_bytes, stream);
 }

@@ -56,6 +56,12 @@ int y_to_u8_bgr(int dt, const void* y, int ldy, int B, int H, int W, uint8_t* ou
 // rows of z_id ([B, c_id] with a row stride, any float dtype) -> fp32 [B, c_id]
 int rows_to_f32(int xdt, const void* x, int64_t row_stride, int B, int n, float* y, hipStream_t s);
 
+// per-sample rows from a per-identity table (the identity table of ghost_aei_swap_u8_indexed): for each of
+// nseg segments, out[g][b] = tab[g][idx[b]] (row_bytes[g] bytes, multiples of 16, 16-byte aligned).  An index
+// outside [0, n_rows) is clamped (memory-safe; the host wrapper validates indices)
+int gather_identity_rows(int nseg, const void* const* tab, const int64_t* row_bytes, void* const* out, int n_rows,
+                         const int32_t* idx, int B, hipStream_t s);
+
 // NHWC (ld) -> NCHW contiguous copy in the same dtype (attr export / tests)
 int nhwc_to_nchw(int dt, const void* x, int ldx, int B, int H, int W, int C, void* y, hipStream_t s);
 

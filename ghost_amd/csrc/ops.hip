@@ -873,6 +873,41 @@ int rows_to_f32(int xdt, const void* x, int64_t row_stride, int B, int n, float*
   return (int)hipGetLastError();
 }
 
+struct GatherSegs {
+  const uint4* tab[2];
+  uint4* out[2];
+  long row16[2];
+};
+
+// blockIdx.y = sample, blockIdx.z = segment; 16-byte copies of one table row
+__global__ void __launch_bounds__(256) gather_rows_kernel(GatherSegs g, int n_rows, const int32_t* __restrict__ idx) {
+  const int b = blockIdx.y, sg = blockIdx.z;
+  int r = idx[b];
+  r = r < 0 ? 0 : (r >= n_rows ? n_rows - 1 : r);
+  const long n = g.row16[sg];
+  const uint4* __restrict__ src = g.tab[sg] + (long)r * n;
+  uint4* __restrict__ dst = g.out[sg] + (long)b * n;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = src[i];
+}
+
+int gather_identity_rows(int nseg, const void* const* tab, const int64_t* row_bytes, void* const* out, int n_rows,
+                         const int32_t* idx, int B, hipStream_t s) {
+  if (nseg < 1 || nseg > 2 || n_rows < 1 || B < 1 || !idx) return -1;
+  GatherSegs g{};
+  long most = 0;
+  for (int i = 0; i < nseg; ++i) {
+    if (!tab[i] || !out[i] || row_bytes[i] <= 0 || row_bytes[i] % 16 || ((uintptr_t)tab[i] | (uintptr_t)out[i]) % 16)
+      return -1;
+    g.tab[i] = (const uint4*)tab[i];
+    g.out[i] = (uint4*)out[i];
+    g.row16[i] = row_bytes[i] / 16;
+    most = most > g.row16[i] ? most : g.row16[i];
+  }
+  dim3 grid((unsigned)std::min<long>((most + 255) / 256, 32), (unsigned)B, (unsigned)nseg);
+  hipLaunchKernelGGL(gather_rows_kernel, grid, dim3(256), 0, s, g, n_rows, idx);
+  return (int)hipGetLastError();
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 nhwc_nchw_kernel(const T* __restrict__ x, int ldx, int B, int H, int W, int C, T* __restrict__ y) {

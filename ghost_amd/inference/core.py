@@ -102,10 +102,19 @@ def swap_identity_frames(resized_frs, present: Sequence[int], source_embed: torc
     out = torch.empty(n, 256, 256, 3, dtype=torch.uint8, device=device)
     host = torch.empty(n, 256, 256, 3, dtype=torch.uint8, pin_memory=True)
     cur = torch.cuda.current_stream(device)
-    copy = torch.cuda.Stream(device)
+    from .streams import stream_set
+    copy = stream_set(device).d2h
+    # the identity's projections once for all its batches (AEI_Net.identity_table; core.py recomputes them in every
+    # faceshifter_batch call), gathered per sample with an all-zero index
+    z_rows = z.reshape(z.shape[0], -1)
+    table = G.identity_table(z_rows) if hasattr(G, "identity_table") and z_rows.shape[0] == 1 else None
+    zero = torch.zeros(min(BS, n), dtype=torch.int32, device=device) if table is not None else None
     for i in range(0, n, BS):
         j = min(n, i + BS)
-        G.swap_u8(crops[i:j], z, out=out[i:j])
+        if table is not None:
+            G.swap_u8_indexed(crops[i:j], table, zero[:j - i], out=out[i:j])
+        else:
+            G.swap_u8(crops[i:j], z, out=out[i:j])
         done = torch.cuda.Event()
         done.record(cur)
         with torch.cuda.stream(copy):

@@ -95,11 +95,13 @@ def model_inference_dp(resized_frs: np.ndarray, present: Sequence[int], source_e
 
 
 def _identity_crops(ident):
-    """One identity of model_inference_multi -> (host crops of its present frames in frame order (a list of
-    uint8 arrays or one [n,h,w,3] array), present, source embedding, whether the crops still need resize_frames'
-    224 -> 256 resize)."""
+    """One identity of model_inference_multi -> (crops of its present frames in frame order (a list of host uint8
+    arrays, one host [n,h,w,3] array, or a device tensor — resize_frames' output), present, source embedding, whether
+    the crops still need resize_frames' 224 -> 256 resize)."""
     if len(ident) == 3:                       # (resized_frs, present, source_embed): resize_frames already ran
         resized, present, emb = ident
+        if present is None:                   # (crop_frames, None, source_embed): the crop_frames form
+            return _identity_crops((resized, emb))
         return resized, np.asarray(present), emb, False
     if len(ident) == 2:                       # (crop_frames, source_embed): crop_frames_and_get_transforms' lists
         crop_frames, emb = ident
@@ -116,7 +118,7 @@ def _identity_crops(ident):
 
 
 def model_inference_multi(identities: Sequence, G, BS: int = 64, device=None, group=None, collect: str = "rank0",
-                          output: str = "host", streams: int = 2):
+                          output: str = "host", streams: int = 2, force_collective: bool = False):
     """The identity loop of model_inference (utils/inference/core.py:56-88) for every identity of a video at once,
     data-parallel over the group (BASELINE config 5: several source -> target identities in one video).
 
@@ -133,7 +135,8 @@ def model_inference_multi(identities: Sequence, G, BS: int = 64, device=None, gr
     memory batch by batch on a copy stream (``output="host"``), and returns ``final_frames_list`` as core.py:88
     builds it: per identity one entry per video frame, the swapped uint8 crop or ``[]``.  ``output="device"``
     returns the same lists holding device tensor views instead (no host copy).  Ranks that receive nothing return
-    ``None``."""
+    ``None``.  ``force_collective``: issue the per-batch gather even in a one-rank group (GatherPipeline), the N > 1
+    data path on one GPU."""
     if collect not in ("rank0", "all"):
         raise ValueError(f"ghost_amd: collect must be 'rank0' or 'all', got {collect!r}")
     if output not in ("host", "device"):
@@ -152,7 +155,7 @@ def model_inference_multi(identities: Sequence, G, BS: int = 64, device=None, gr
     fshape = (256, 256, 3)
     for crops, _, _, needs in idents:
         if len(crops) and not needs:
-            fshape = tuple(np.asarray(crops[0]).shape)
+            fshape = tuple(crops[0].shape) if torch.is_tensor(crops) else tuple(np.asarray(crops[0]).shape)
             break
     # this rank's crops (host -> device once, per identity part; crop_frames parts resized 224 -> 256 on the device,
     # video_processing.py:184) and their identity rows
@@ -162,25 +165,38 @@ def model_inference_multi(identities: Sequence, G, BS: int = 64, device=None, gr
         if a >= b:
             continue
         part = crops[a - offs[q]:b - offs[q]]
-        host = torch.from_numpy(np.ascontiguousarray(np.stack(part) if isinstance(part, list) else np.asarray(part)))
-        dpart = host.pin_memory().to(device, non_blocking=True) if gpu else host.to(device)
+        if torch.is_tensor(part):             # resize_frames' device crops (or a host tensor)
+            dpart = part.to(device)
+        else:
+            host = torch.from_numpy(np.ascontiguousarray(np.stack(part) if isinstance(part, list) else np.asarray(part)))
+            dpart = host.pin_memory().to(device, non_blocking=True) if gpu else host.to(device)
         if needs and tuple(dpart.shape[1:3]) != (256, 256):
             from .blend import resize_u8
             dpart = resize_u8(dpart, (256, 256))
         parts.append(dpart)
         ids.append(np.full(b - a, q, np.int64))
     embeds = torch.stack([torch.as_tensor(e).reshape(-1) for _, _, e, _ in idents]).to(device) if idents else None
+    # the identities' projections once (AEI_Net.identity_table: every AADLayer's fc1/fc2 and up1 per source
+    # embedding), each batch then gathers its samples' rows by identity index (swap_u8_indexed); a swap object
+    # without the table API gets per-sample embedding rows instead
+    indexed = hasattr(G, "identity_table") and hasattr(G, "swap_u8_indexed")
+    table = None
     if parts:
         local = parts[0] if len(parts) == 1 else torch.cat(parts)
         if tuple(local.shape[1:]) != fshape:
             raise ValueError(f"ghost_amd: identities' crops differ in shape ({tuple(local.shape[1:])} vs {fshape})")
-        z_all = embeds.index_select(0, torch.from_numpy(np.concatenate(ids)).to(device))
         try:
             pdt = next(G.parameters()).dtype
         except (AttributeError, StopIteration):
             pdt = None
         if pdt == torch.float16:
-            z_all = z_all.half()                            # core.py:65-66 (a .half() module)
+            embeds = embeds.half()                          # core.py:65-66 (a .half() module)
+        ids_d = torch.from_numpy(np.concatenate(ids)).to(device)
+        if indexed:
+            table = G.identity_table(embeds)
+            z_all = ids_d.to(torch.int32)                   # valid by construction: built from 0..len(idents)-1
+        else:
+            z_all = embeds.index_select(0, ids_d)
     else:
         local = torch.empty((0,) + fshape, dtype=torch.uint8, device=device)
         z_all = None
@@ -188,13 +204,24 @@ def model_inference_multi(identities: Sequence, G, BS: int = 64, device=None, gr
     B = max(1, min(BS, per))
     zb = [None]
     streams = max(1, streams) if gpu else 1
-    pipe = GatherPipeline(lambda c, o: G.swap_u8(c, zb[0], out=o), (B,) + fshape, device, group=group,
-                          depth=2 * streams, streams=streams, dst=0 if collect == "rank0" else None)
+    if indexed:
+        def swap(c, o):
+            return G.swap_u8_indexed(c, table, zb[0], out=o)
+    else:
+        def swap(c, o):
+            return G.swap_u8(c, zb[0], out=o)
+    pipe = GatherPipeline(swap, (B,) + fshape, device, group=group,
+                          depth=2 * streams, streams=streams, dst=0 if collect == "rank0" else None,
+                          force_collective=force_collective)
     receiver = pipe.receiver
     out_all = torch.empty((n,) + fshape, dtype=torch.uint8, device=device) if receiver else None
     host_all = (torch.empty((n,) + fshape, dtype=torch.uint8, pin_memory=True)
                 if receiver and output == "host" and gpu else None)
-    copy = torch.cuda.Stream(device) if host_all is not None else None
+    if host_all is not None:
+        from .streams import stream_set
+        copy = stream_set(device).d2h
+    else:
+        copy = None
     cur = torch.cuda.current_stream(device) if gpu else None
     bounds = [shard_bounds(n, world, r)[:2] for r in range(world)]
 
@@ -244,10 +271,13 @@ def model_inference_multi(identities: Sequence, G, BS: int = 64, device=None, gr
 
 
 def swap_mixed_identities(crops: torch.Tensor, identity_index: torch.Tensor, source_embeds: torch.Tensor, G,
-                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Config 5 (several identities in one batch): each crop carries the index of its source
-    identity; the per-sample z_id rows are gathered on the device and the AAD identity path
-    (fc1/fc2 per sample, AADLayer.py:28-29) handles the mix in one launch sequence."""
+                          out: Optional[torch.Tensor] = None, table=None) -> torch.Tensor:
+    """Config 5 (several identities in one batch): each crop carries the index of its source identity.  With
+    ``table`` (``G.identity_table(source_embeds)``, built once per video) the identity rows of every AADLayer are
+    gathered per sample (``swap_u8_indexed``); without it the per-sample z_id rows are gathered on the device and
+    projected inside the swap (fc1/fc2 per sample, AADLayer.py:28-29).  Same bytes either way (batches <= 64)."""
+    if table is not None:
+        return G.swap_u8_indexed(crops, table, identity_index, out=out)
     z = source_embeds.reshape(source_embeds.shape[0], -1).index_select(0, identity_index.to(source_embeds.device))
     return G.swap_u8(crops, z, out=out)
 
@@ -276,27 +306,40 @@ class GatherPipeline:
     rows, rank by rank.  Rows past a rank's count travel as padding and are dropped.
 
     ``streams`` > 1 keeps that many batches in flight on the GPU: submit k runs its swap (and issues its
-    all-gather) on pipeline-owned stream k % streams, after the caller's stream (where the crops were
-    produced); consecutive batches are independent, so the low-resolution, latency-bound stages of one
-    batch (encoder, 2x2..8x8 blocks) overlap the HBM- and MFMA-bound 64x64..256x256 stages of the other.
+    all-gather) on compute stream k % streams of the device's ``StreamSet`` (streams.py: 0 is the caller's current
+    stream, 1 the set's side stream; a stream other than the caller's first waits for the caller's stream, where
+    the crops were produced); consecutive batches are independent, so the low-resolution, latency-bound stages of
+    one batch (encoder, 2x2..8x8 blocks) overlap the HBM- and MFMA-bound 64x64..256x256 stages of the other.
     ``result`` and ``drain`` make the caller's stream wait for the batch's stream.  ``depth`` is rounded up
     to a multiple of ``streams`` so a slot is always rewritten on the stream that last wrote it.
     """
 
     def __init__(self, swap: Callable, batch_shape, device, dtype=torch.uint8, group=None, depth: int = 2,
-                 streams: int = 1, dst: Optional[int] = None):
+                 streams: int = 1, dst: Optional[int] = None, force_collective: bool = False):
         self.nstreams = max(1, int(streams))
         depth = max(1, depth)
         depth = (depth + self.nstreams - 1) // self.nstreams * self.nstreams
         self.swap, self.group, self.depth = swap, group, depth
         self.device = torch.device(device)
-        self.streams = ([torch.cuda.Stream(self.device) for _ in range(self.nstreams)]
-                        if self.nstreams > 1 else [None])
+        # batch k runs on compute stream k % streams of the device's StreamSet: 0 = the caller's current stream,
+        # 1 = the set's side stream (the process's stream count stays fixed however many pipelines it builds)
+        if self.nstreams > 1:
+            from .streams import stream_set
+            ss = stream_set(self.device)
+            self.streams = [ss.compute(i) for i in range(self.nstreams)]
+        else:
+            self.streams = [None]
         self.done = [None] * depth             # per slot: event after its swap + all-gather issue (streams > 1)
         dist_on = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if dist_on else 1
         self.rank = dist.get_rank(group) if dist_on else 0
-        self.nccl = self.world > 1 and dist.get_backend(group) == "nccl"
+        # force_collective: issue the gather / all-gather even in a one-rank group, so the N > 1 data path (async
+        # RCCL collective per slot, Work.wait() on a pipeline stream, slot reuse under a live work object) runs on a
+        # single GPU exactly as it does on eight
+        if force_collective and not dist_on:
+            raise RuntimeError("GatherPipeline: force_collective needs an initialised process group")
+        self.collective = self.world > 1 or bool(force_collective)
+        self.nccl = self.collective and dist.get_backend(group) == "nccl"
         shape = tuple(batch_shape)
         self.rows = shape[0]
         self.outs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(self.depth)]
@@ -305,7 +348,7 @@ class GatherPipeline:
         self.dst = dst
         self.receiver = dst is None or self.rank == dst
         self.gath = ([torch.empty((self.world * shape[0],) + shape[1:], dtype=dtype, device=device)
-                      if self.receiver else None for _ in range(self.depth)] if self.world > 1 else self.outs)
+                      if self.receiver else None for _ in range(self.depth)] if self.collective else self.outs)
         self.pending: List[Optional[object]] = [None] * self.depth
         self.gen = [0] * self.depth
         self.k = 0
@@ -330,6 +373,8 @@ class GatherPipeline:
                              f"with {n} rows of at most {self.rows}")
         slot = self.k % self.depth
         st = self.streams[self.k % self.nstreams]
+        if st is not None and st == torch.cuda.current_stream(self.device):
+            st = None                               # the caller runs on the side stream itself
         if st is not None:
             st.wait_stream(torch.cuda.current_stream(self.device))   # the crops are ready on the caller's stream
             crops.record_stream(st)
@@ -337,21 +382,21 @@ class GatherPipeline:
             self._wait(slot)                      # the collective still reading this slot's buffer
             if n:
                 self.swap(crops, self.outs[slot][:n])
-            if self.world > 1 and self.dst is not None:
+            if self.collective and self.dst is not None:
                 g = self.gath[slot]
                 self.pending[slot] = dist.gather(self.outs[slot], list(g.chunk(self.world)) if g is not None else None,
                                                  dst=_global_rank(self.group, self.dst), group=self.group,
                                                  async_op=True)
-            elif self.world > 1:
+            elif self.collective:
                 if self.nccl:
                     self.pending[slot] = dist.all_gather_into_tensor(self.gath[slot], self.outs[slot],
                                                                      group=self.group, async_op=True)
                 else:
                     self.pending[slot] = dist.all_gather(list(self.gath[slot].chunk(self.world)), self.outs[slot],
                                                          group=self.group, async_op=True)
-            if st is not None:
+            if self.nstreams > 1:
                 ev = torch.cuda.Event()
-                ev.record(st)
+                ev.record(st if st is not None else torch.cuda.current_stream(self.device))
                 self.done[slot] = ev
         self.gen[slot] += 1
         self.k += 1
@@ -372,6 +417,10 @@ class GatherPipeline:
         if all(c == self.rows for c in ticket.counts):
             return g
         return torch.cat([g[r * self.rows:r * self.rows + c] for r, c in enumerate(ticket.counts)])
+
+    def in_flight(self) -> int:
+        """Collectives issued and not yet waited on (0 after ``drain``)."""
+        return sum(w is not None for w in self.pending)
 
     def drain(self):
         for s in range(self.depth):

@@ -14,9 +14,10 @@ afterwards).  With 0 the graph is one chain of kernels; with 1 (the eager defaul
 branch the replay runs beside the down path.  The replay issues the nodes back to back, so the two branches' small
 B = 1 kernels overlap and contend far more than in an eager call (a rocprofv3 trace of the same calls,
 tools/graph_trace.py: the graphed kernels' sum 15.9 ms against 11.1 eager for 705 fp32 launches), and on some boxes
-the branch form replayed far slower than eager (bench ``config1_latency``, round 4: bf16 2.86 ms graphed with two
-branches, 1.72 as one chain, 1.62 eager; fp32 3.82 / 2.15 / 2.08 — round 3 saw the same 2× on fp32).  One chain
-tracked eager on every box measured, so it is the default.
+the branch form replayed far slower than eager (round 4, before the plan ran batches of fewer than 8 frames on one
+stream: bf16 2.86 ms graphed with two branches, 1.72 as one chain, 1.62 eager).  Since then the plan itself runs a batch
+of B < 8 on one stream, so at B = 1 both settings capture the same single chain; the branch form exists from B = 8 on
+(tests/test_gpu_pipeline.py covers it at B = 8).  One chain tracked eager on every box measured, so it is the default.
 
 The graph holds the module's packed weights and workspace as they were at capture, and the ``GraphedSwap``
 keeps that runtime (its packed weight tensors, native handle and workspace) alive for as long as it lives.  A
@@ -64,8 +65,12 @@ class GraphedSwap:
             with torch.cuda.graph(self.graph, stream=self._capture_stream):
                 G.swap_u8(self.crops, self.z, out=self.out)
             torch.cuda.synchronize(dev)
+            # the workspace the captured kernels write (allocated in the graph's private pool): held here, so neither
+            # the module's LRU cache nor an option change (which clears that cache) can release it under the graph
+            self._ws = list(G._rt.ws.ws.values())
         finally:
-            G.set_option("two_streams", saved)
+            if G.get_option("two_streams") != saved:
+                G.set_option("two_streams", saved)
         # the captured kernels read the packed weights of this runtime (and its handle / workspace): hold it
         self._rt = G._rt
 

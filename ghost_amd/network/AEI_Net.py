@@ -158,7 +158,8 @@ class _Runtime:
             self.geom.append((c_.value, h_.value, w_.value))
 
     def workspace(self, mode: str, B: int, dev: torch.device, stream: int) -> torch.Tensor:
-        fn = self.lib.ghost_aei_swap_workspace_bytes if mode == "swap" else self.lib.ghost_aei_workspace_bytes
+        fn = {"swap": self.lib.ghost_aei_swap_workspace_bytes,
+              "idtable": self.lib.ghost_aei_identity_table_workspace_bytes}.get(mode, self.lib.ghost_aei_workspace_bytes)
 
         def nbytes():
             n = fn(self.h, B)
@@ -173,6 +174,19 @@ class _Runtime:
                 self.lib.ghost_aei_destroy(self.h)
         except Exception:
             pass
+
+
+class IdentityTable:
+    """Device rows of ``AEI_Net.identity_table``: per source identity, every AADLayer's gamma_id / beta_id (fp32) and
+    up1's output (the plan dtype).  Holds the runtime (packed weights, handle) it was computed with, so a table from
+    before a re-pack is detected instead of used."""
+
+    def __init__(self, rt, buf: torch.Tensor, off: int, n: int, device: torch.device):
+        self.rt, self.buf, self.n, self.device = rt, buf, n, device
+        self.ptr = buf.data_ptr() + off
+
+    def __len__(self):
+        return self.n
 
 
 class AEI_Net(PackedModule):
@@ -346,6 +360,88 @@ class AEI_Net(PackedModule):
         _lib.check(lib.ghost_aei_swap_u8(rt.h, crops_u8.data_ptr(), cstride, B, z.data_ptr(),
                                          _lib.gdtype(z.dtype), zrs, out.data_ptr(), ws.data_ptr(), ws.numel(),
                                          stream), "AEI_Net.swap_u8")
+        return out
+
+    @torch.no_grad()
+    def identity_table(self, source_embeds: torch.Tensor) -> "IdentityTable":
+        """The per-identity projection table of ``source_embeds`` ([n, c_id] rows on the device, any float dtype):
+        every AADLayer's fc1/fc2 (gamma_id, beta_id; AADLayer.py:28-29) and up1 (AEI_Net.py:101) of each source
+        embedding, computed once (``ghost_aei_identity_table``) for the module's current weights.  A video's source
+        identity is the same for every frame (faceshifter_run.py:15-16 repeats one z_id over the batch), so
+        ``swap_u8_indexed`` then gathers each sample's rows instead of projecting the embedding per frame."""
+        _lib.require_gpu(source_embeds, "AEI_Net.identity_table")
+        dev = source_embeds.device
+        rt = self._runtime(dev)
+        z = source_embeds.reshape(source_embeds.shape[0], -1)
+        if z.shape[0] < 1 or z.shape[1] != self.c_id:
+            raise RuntimeError(f"ghost_amd: source_embeds must hold n >= 1 rows of {self.c_id}, got "
+                               f"{tuple(source_embeds.shape)}")
+        if z.stride(1) != 1:
+            z = z.contiguous()
+        n = z.shape[0]
+        lib = rt.lib
+        nb = lib.ghost_aei_identity_table_bytes(rt.h, n)
+        if nb < 0:
+            _lib.check(int(nb), "identity table sizing")
+        buf = torch.empty(int(nb) + 256, dtype=torch.uint8, device=dev)
+        off = (-buf.data_ptr()) % 256
+        stream = _lib.stream_ptr(dev)
+        ws = rt.workspace("idtable", n, dev, stream)
+        _lib.check(lib.ghost_aei_identity_table(rt.h, z.data_ptr(), _lib.gdtype(z.dtype), z.stride(0), n,
+                                                buf.data_ptr() + off, int(nb), ws.data_ptr(), ws.numel(), stream),
+                   "AEI_Net.identity_table")
+        return IdentityTable(rt, buf, off, n, dev)
+
+    @torch.no_grad()
+    def swap_u8_indexed(self, crops_u8: torch.Tensor, table: "IdentityTable", identity_index: torch.Tensor,
+                        out: Optional[torch.Tensor] = None):
+        """``swap_u8`` for a batch whose sample b swaps in identity ``identity_index[b]`` of ``table`` (config 5's
+        mixed-identity batches, or one identity with an all-zero index): the identity rows are gathered from the
+        table (one launch) instead of projected from per-sample z rows.  The bytes equal ``swap_u8(crops,
+        source_embeds[identity_index])`` for batches of up to 64 frames (the projections are the same GEMM rows).
+        ``identity_index``: int32/int64 [B]; a host tensor is range-checked here (IndexError as
+        ``source_embeds[identity_index]`` would raise), a device tensor is the caller's to keep in range (an
+        out-of-range value is clamped on the device, never read out of bounds)."""
+        _lib.require_gpu(crops_u8, "AEI_Net.swap_u8_indexed")
+        if crops_u8.dtype != torch.uint8 or crops_u8.ndim != 4 or tuple(crops_u8.shape[1:]) != (256, 256, 3):
+            raise RuntimeError("ghost_amd: crops must be uint8 [B,256,256,3]")
+        if crops_u8[0].stride() != (768, 3, 1):
+            crops_u8 = crops_u8.contiguous()
+        dev = crops_u8.device
+        if not isinstance(table, IdentityTable):
+            raise TypeError("ghost_amd: table must come from AEI_Net.identity_table")
+        rt = self._runtime(dev)
+        if table.rt is not rt or table.device != dev:
+            raise RuntimeError("ghost_amd: the identity table was built for other weights or another device (the "
+                               "module was re-packed since: load_state_dict / .to / .half / a parameter change); "
+                               "rebuild it with identity_table")
+        B = crops_u8.shape[0]
+        idx = identity_index.reshape(-1)
+        if idx.shape[0] != B:
+            raise RuntimeError(f"ghost_amd: identity_index must hold {B} entries, got {tuple(identity_index.shape)}")
+        if idx.dtype not in (torch.int32, torch.int64, torch.int16, torch.uint8):
+            raise TypeError(f"ghost_amd: identity_index must be an integer tensor, got {idx.dtype}")
+        if idx.device.type == "cpu":
+            if B and (int(idx.min()) < 0 or int(idx.max()) >= table.n):
+                raise IndexError(f"ghost_amd: identity_index out of range for {table.n} identities")
+            idx = idx.to(torch.int32).to(dev)
+        else:
+            _lib.require_same_device(idx, dev, "identity_index")
+            if idx.dtype != torch.int32 or not idx.is_contiguous():
+                idx = idx.to(torch.int32).contiguous()
+        if out is None:
+            out = torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=dev)
+        elif (tuple(out.shape) != (B, 256, 256, 3) or out.dtype != torch.uint8 or not out.is_contiguous()
+              or out.device != dev):
+            raise RuntimeError(f"ghost_amd: out must be a contiguous uint8 [{B},256,256,3] tensor on {dev}, got "
+                               f"{out.dtype} {tuple(out.shape)} on {out.device}")
+        lib = rt.lib
+        stream = _lib.stream_ptr(dev)
+        ws = rt.workspace("swap", B, dev, stream)
+        cstride = crops_u8.stride(0) if B > 1 else 256 * 256 * 3
+        _lib.check(lib.ghost_aei_swap_u8_indexed(rt.h, crops_u8.data_ptr(), cstride, B, table.ptr, table.n,
+                                                 idx.data_ptr(), out.data_ptr(), ws.data_ptr(), ws.numel(), stream),
+                   "AEI_Net.swap_u8_indexed")
         return out
 
     def profile(self, class_mask: int):

@@ -15,6 +15,9 @@
  *   network/AEI_Net.py:158-159   AEI_Net.get_attr(X)                       -> ghost_aei_get_attr
  *   utils/inference/faceshifter_run.py:5-22 + utils/inference/core.py:13-26
  *                                faceshifter_batch(transform_target_to_torch(crops)) -> ghost_aei_swap_u8
+ *   network/AADLayer.py:28-29 + utils/inference/faceshifter_run.py:15-16
+ *                                fc1/fc2(z_id) per AADLayer, once per source identity -> ghost_aei_identity_table,
+ *                                                                          ghost_aei_swap_u8_indexed
  *   network/AADLayer.py:20-38    AADLayer.forward(h_in, z_attr, z_id)       -> ghost_aad_layer_nhwc
  *   network/AEI_Net.py:19-24     conv4x4 (Conv 4x4/s2 + BN + LReLU)         -> ghost_conv2d_nhwc
  *   network/AEI_Net.py:27-41     deconv4x4 (ConvT 4x4/s2 + BN + LReLU + skip) -> ghost_conv_transpose4x4s2_nhwc
@@ -76,6 +79,24 @@ int64_t ghost_aei_swap_workspace_bytes(ghost_aei* h, int B);
 int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_stride, int B, const void* z_id,
                       int zid_dtype, int64_t zid_row_stride, uint8_t* out_u8, void* ws, int64_t ws_bytes,
                       void* stream);
+
+/* Per-identity projection table (AADLayer.py:28-29 fc1/fc2 of every AADLayer, AEI_Net.py:101 up1; a source
+ * embedding's gamma_id / beta_id / m1 rows do not depend on the target frame, faceshifter_run.py:15-16 repeats one
+ * z_id over the batch): computed once per (identity, weight version) and gathered per sample by identity_index.
+ * ghost_aei_identity_table writes the rows of n_ident z_id rows (any float dtype, row stride zid_row_stride) into
+ * table (device, 256-byte aligned, ghost_aei_identity_table_bytes(h, n_ident) bytes; workspace
+ * ghost_aei_identity_table_workspace_bytes).  The table holds results of the handle's bound weights: rebuild it after
+ * re-binding.  Rows are bit-identical to the projections a ghost_aei_swap_u8 of up to 64 frames computes.
+ * ghost_aei_swap_u8_indexed = ghost_aei_swap_u8 with sample b's identity rows taken from table row
+ * identity_index[b] (device int32 [B], values in [0, n_ident); an out-of-range value is clamped — memory-safe, not an
+ * error: validate on the host).  Workspace: ghost_aei_swap_workspace_bytes. */
+int64_t ghost_aei_identity_table_bytes(ghost_aei* h, int n_ident);
+int64_t ghost_aei_identity_table_workspace_bytes(ghost_aei* h, int n_ident);
+int ghost_aei_identity_table(ghost_aei* h, const void* z_id, int zid_dtype, int64_t zid_row_stride, int n_ident,
+                             void* table, int64_t table_bytes, void* ws, int64_t ws_bytes, void* stream);
+int ghost_aei_swap_u8_indexed(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_stride, int B, const void* table,
+                              int n_ident, const int32_t* identity_index, uint8_t* out_u8, void* ws, int64_t ws_bytes,
+                              void* stream);
 
 /* Per-handle plan options (defaults are the measured choices; every forward of the handle uses them):
  *   GHOST_AEI_OPT_FUSE_UPSAMPLE (1): AADBlk8's first AADLayer pair samples upsample2x(AADBlk7 output) on the fly

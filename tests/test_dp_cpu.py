@@ -337,6 +337,19 @@ class _FakeGz(_FakeG):
         return y
 
 
+class _FakeGzTable(_FakeGz):
+    """The same stand-in with AEI_Net's identity-table API (identity_table / swap_u8_indexed): the path
+    model_inference_multi takes with the real module."""
+
+    def identity_table(self, embeds):
+        self.tables = getattr(self, "tables", 0) + 1
+        return embeds.reshape(embeds.shape[0], -1).clone()
+
+    def swap_u8_indexed(self, crops, table, idx, out=None):
+        assert idx.dtype == torch.int32 and int(idx.max()) < table.shape[0]
+        return self.swap_u8(crops, table.index_select(0, idx.to(torch.int64)), out=out)
+
+
 MULTI_PRESENT = [[1, 1, 0, 1, 1, 1, 0], [0, 1, 1, 1, 0, 0, 1], [1, 0, 0, 0, 0, 1, 1]]
 
 
@@ -456,3 +469,80 @@ def test_bench_config5_multi_leg_reporting_gloo():
     per = (l0["crops"] + 1) // 2               # rank 0's contiguous shard
     # 2 output modes x (1 warm-up + 2 timed) = 6 pipeline calls, each swapping the rank's whole shard
     assert sum(c0) == 6 * per and sum(c1) == 6 * (l0["crops"] - per), (sum(c0), sum(c1), per)
+
+
+def test_model_inference_multi_identity_forms():
+    """model_inference_multi takes each identity as (crop_frames, source_embed), (crop_frames, None,
+    source_embed) or (resized_frs, present, source_embed) with resized_frs a numpy array or a tensor (resize_frames'
+    output): all forms give the single-process per-identity lists (one process, no process group)."""
+    from ghost_amd.inference import dp
+    idents, crops_of = _multi_case()
+    exp = _multi_expect()
+    forms = [
+        idents,
+        [(idents[0][0], None, idents[0][1])] + idents[1:],
+        [idents[0]] + [(torch.from_numpy(c), p, e) for c, p, e in idents[1:]],
+    ]
+    for f in forms:
+        _same_lists(dp.model_inference_multi(f, _FakeGz(), BS=3, device="cpu"), exp)
+        G = _FakeGzTable()
+        _same_lists(dp.model_inference_multi(f, G, BS=3, device="cpu"), exp)
+        assert G.tables == 1                # the identities' projections once per call, then gathered per batch
+
+
+def _forced_worker(rank, world, port, q):
+    from ghost_amd.inference import dp
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        G = _FakeGz()
+        crops = torch.from_numpy(np.random.Generator(np.random.PCG64(3)).integers(0, 256, (11, 8, 8, 3),
+                                                                              dtype=np.uint8))
+        z = torch.full((1, 512), 5.0)
+        out = {}
+        for dst in (None, 0):
+            pipe = dp.GatherPipeline(lambda c, o: G.swap_u8(c, z, out=o), (4, 8, 8, 3), "cpu", depth=2, dst=dst,
+                                     force_collective=True)
+            assert pipe.collective and pipe.gath[0] is not pipe.outs[0]
+            t = [pipe.submit(crops[0:4]), pipe.submit(crops[4:8])]
+            assert pipe.in_flight() == 2
+            got = [pipe.result(t[0]).clone()]
+            t.append(pipe.submit(crops[8:11], counts=[3]))       # reuses slot 0
+            try:
+                pipe.result(t[0])
+                stale = False
+            except RuntimeError:
+                stale = True
+            got += [pipe.result(t[1]).clone(), pipe.result(t[2]).clone()]
+            pipe.drain()
+            out[dst] = (torch.cat(got).numpy().copy(), stale, pipe.in_flight())
+        idents, _ = _multi_case()
+        multi = dp.model_inference_multi(idents, G, BS=3, device="cpu", force_collective=True)
+        q.put((out, G.swap_u8(crops, z).numpy().copy(),
+               [[f if isinstance(f, list) else f.copy() for f in fl] for fl in multi]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_pipeline_force_collective_one_rank_gloo():
+    """VERDICT r04 item 1 (CPU half; the RCCL half is tests/test_gpu_pipeline.py): force_collective issues the
+    gather / all-gather in a one-rank group — same bytes as the direct swap, a reused slot's ticket still raises,
+    drain() leaves nothing in flight; model_inference_multi with it returns the expected lists."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_worker, args=(0, 1, _free_port(), q))
+    p.start()
+    out, ref, multi = q.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    for dst in (None, 0):
+        got, stale, left = out[dst]
+        assert np.array_equal(got, ref) and stale and left == 0
+    _same_lists(multi, _multi_expect())
+
+
+def test_force_collective_needs_a_group():
+    from ghost_amd.inference import dp
+    with pytest.raises(RuntimeError, match="process group"):
+        dp.GatherPipeline(lambda c, o: None, (2, 8, 8, 3), "cpu", force_collective=True)

@@ -203,11 +203,13 @@ def test_gather_pipeline_two_batches_in_flight(lib):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("dt,B", [(None, 1), (torch.bfloat16, 1), (torch.bfloat16, 4), (torch.float16, 2)])
+@pytest.mark.parametrize("dt,B", [(None, 1), (torch.bfloat16, 1), (torch.bfloat16, 4), (torch.float16, 2),
+                                  (torch.bfloat16, 8), (torch.float16, 8)])
 def test_graphed_swap_is_bit_identical(lib, dt, B):
     """GraphedSwap (one HIP graph replay of the whole native plan, captured as one chain — the default — or with
     the two-stream plan) gives the bytes of an eager swap_u8, for new inputs copied into the captured buffers on
-    every call; the capture leaves the module's own two_streams option as it was."""
+    every call; the capture leaves the module's own two_streams option as it was.  The plan runs batches of fewer
+    than 8 frames on one stream, so only B = 8 captures the cross-stream events and the up-path branch."""
     from ghost_amd.inference import GraphedSwap
     G, _p = model("unet", 2, dt)
     g = GraphedSwap(G, B, DEV)
@@ -297,3 +299,113 @@ def test_model_inference_multi_rccl_one_rank(lib):
                         u8_close(x if mode == "host" else x.cpu().numpy(), y, max_lsb=1, frac=1e-3)
     finally:
         dist.destroy_process_group()
+
+
+def test_pipeline_rccl_collectives_two_streams_one_rank(lib):
+    """the N > 1 data path on one GPU.  GatherPipeline(streams=2, force_collective=True) over a
+    one-rank RCCL group issues bench.py's per-slot async all_gather_into_tensor (dst=None) and the video mux's gather
+    to rank 0 (dst=0) from two pipeline streams, waits on each slot's Work on a pipeline stream before the slot is
+    rewritten, and must give the bytes of the no-collective two-stream run; a reused slot's ticket raises; drain()
+    leaves no collective in flight.  model_inference_multi(collect='rank0'|'all', force_collective=True) must give
+    the bytes of the same call without the collective (/root/reference/utils/inference/core.py:72-88)."""
+    import torch.distributed as dist
+    from ghost_amd.inference.dp import GatherPipeline, model_inference_multi
+    G, _ = model("unet", 2, torch.bfloat16)
+    B, nb = 8, 5
+    crops = torch.from_numpy(aei_ref.make_u8_crops(B * nb - 3, 37)).to(DEV)
+    _, z = aei_ref.make_inputs(1, 37)
+    zd = z.to(DEV)
+
+    def run(pipe):
+        got, pending, stale = [], [], None
+        for i in range(0, crops.shape[0], B):
+            c = crops[i:i + B]
+            pending.append(pipe.submit(c, counts=[c.shape[0]] if c.shape[0] < B else None))
+            if len(pending) == 2:
+                t = pending.pop(0)
+                got.append(pipe.result(t).clone())
+                stale = stale or t
+        got += [pipe.result(t).clone() for t in pending]
+        pipe.drain()
+        torch.cuda.synchronize()
+        return got, stale
+
+    ref, _ = run(GatherPipeline(lambda c, o: G.swap_u8(c, zd, out=o), (B, 256, 256, 3), DEV, depth=2, streams=2))
+    pres = [[1, 1, 0, 1, 1, 1, 1, 0, 1], [0, 1, 1, 1, 0, 1, 1, 1, 1]]
+    g = np.random.default_rng(19)
+    idents = []
+    for q, pr in enumerate(pres):
+        _, zq = aei_ref.make_inputs(1, 200 + q)
+        idents.append((g.integers(0, 256, (sum(pr), 256, 256, 3), dtype=np.uint8), np.array(pr, np.float64), zq))
+    multi_ref = model_inference_multi(idents, G, BS=4, device=DEV, output="device")
+    multi_ref = [[x.clone() if torch.is_tensor(x) else x for x in fl] for fl in multi_ref]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        for dst in (None, 0):
+            pipe = GatherPipeline(lambda c, o: G.swap_u8(c, zd, out=o), (B, 256, 256, 3), DEV, depth=2, streams=2,
+                                  dst=dst, force_collective=True)
+            assert pipe.collective and pipe.nccl and pipe.nstreams == 2
+            assert pipe.gath[0].data_ptr() != pipe.outs[0].data_ptr()
+            got, stale = run(pipe)
+            assert pipe.in_flight() == 0
+            with pytest.raises(RuntimeError, match="overwritten"):
+                pipe.result(stale)
+            assert len(got) == len(ref)
+            for a, b in zip(got, ref):
+                assert torch.equal(a, b)
+        for collect in ("rank0", "all"):
+            for mode in ("device", "host"):
+                got = model_inference_multi(idents, G, BS=4, device=DEV, collect=collect, output=mode,
+                                            force_collective=True)
+                for fl, rl in zip(got, multi_ref):
+                    assert len(fl) == len(rl)
+                    for x, y in zip(fl, rl):
+                        if isinstance(y, list):
+                            assert isinstance(x, list) and x == []
+                        else:
+                            xx = x if mode == "device" else torch.from_numpy(np.asarray(x)).to(DEV)
+                            assert torch.equal(xx, y)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("backbone,nb,dt,B,nid", [("unet", 2, torch.bfloat16, 8, 1), ("unet", 2, torch.bfloat16, 64, 1),
+                                                  ("linknet", 3, torch.bfloat16, 8, 4), ("unet", 2, None, 2, 2),
+                                                  ("linknet", 3, torch.float16, 8, 3)])
+def test_identity_table_indexed_swap_is_bit_identical(lib, backbone, nb, dt, B, nid):
+    """VERDICT r04 item 6 (/root/reference/network/AADLayer.py:28-33, faceshifter_run.py:15-16): the
+    per-identity projection table (fc1/fc2 of every AADLayer and up1, computed once per identity) gathered by
+    identity_index gives the bytes of swap_u8 with per-sample z rows (source_embeds[identity_index]) — one identity
+    (B = 8 and the bench's B = 64) and mixed batches of 2-4 identities, bf16 / fp32 / fp16."""
+    G, _ = model(backbone, nb, dt)
+    if dt == torch.float16:
+        G = G.half()
+    crops = torch.from_numpy(aei_ref.make_u8_crops(B, 43)).to(DEV)
+    _, zs = aei_ref.make_inputs(nid, 43)
+    zs = zs.to(DEV)
+    if dt == torch.float16:
+        zs = zs.half()
+    idx = (torch.arange(B) * 7 + 1) % nid
+    table = G.identity_table(zs)
+    assert len(table) == nid
+    got = G.swap_u8_indexed(crops, table, idx)                       # host index: range-checked, then copied
+    got_dev = G.swap_u8_indexed(crops, table, idx.to(DEV).to(torch.int32))
+    ref = G.swap_u8(crops, zs.index_select(0, idx.to(DEV)).contiguous() if nid > 1 else zs)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert torch.equal(got_dev, ref)
+    with pytest.raises(IndexError):
+        G.swap_u8_indexed(crops, table, torch.full((B,), nid))
+
+
+def test_identity_table_refuses_stale_weights(lib):
+    """A table holds the projections of the weights it was built with: after a re-pack it is refused."""
+    G, p = model("unet", 2, torch.bfloat16)
+    _, z = aei_ref.make_inputs(1, 44)
+    table = G.identity_table(z.to(DEV))
+    crops = torch.from_numpy(aei_ref.make_u8_crops(1, 44)).to(DEV)
+    G.swap_u8_indexed(crops, table, torch.zeros(1, dtype=torch.int32))
+    G.load_state_dict(p)
+    G.swap_u8(crops, z.to(DEV))                 # re-packs
+    with pytest.raises(RuntimeError, match="rebuild"):
+        G.swap_u8_indexed(crops, table, torch.zeros(1, dtype=torch.int32))

@@ -22,6 +22,9 @@
 #   arctrace:N     kernel trace of tools/run_arc.py N (ArcFace)            -> gpurun_out/arc_kt_N.txt
 #   gtrace:DT      kernel trace of eager vs GraphedSwap at B = 1 (DT fp32/bf16) -> gpurun_out/gtrace_DT.txt
 #   mfma           MFMA / VALU PMC passes (tools/pmc_mfma.sh, ROUND=rNN)   -> gpurun_out/rNN_mfma.json
+#   qprobeset      the same with ghost_amd's StreamSet created first       -> gpurun_out/queue_probe_set.txt
+#   qprobe         which streams share a hardware queue (tools/queue_probe.py) -> gpurun_out/queue_probe.txt
+#   legs:LIST      bench.py with --legs LIST (':'-separated), no CPU baseline -> gpurun_out/legs_LIST.log
 # Extra bench.py arguments for quick/quick1/ab/knobs/streams: BENCH_ARGS="--opt tap_partials=1".
 # knobs needs the tuning library on the box (GHOST_TUNING=1 python -m ghost_amd.build; list the shipping
 # library in .gpurunignore for that call if the push should carry only one of them).
@@ -77,6 +80,11 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/gtr -o run -- python3 tools/graph_trace.py $dt > "gpurun_out/gtrace_$dt.txt" 2>&1; must $?
       python3 tools/graph_trace.py --analyze /tmp/gtr/run_results.db >> "gpurun_out/gtrace_$dt.txt" 2>&1 ;;
     mfma) bash tools/pmc_mfma.sh; must $? ;;
+    qprobe) timeout -k 10 120 python -u tools/queue_probe.py > gpurun_out/queue_probe.txt 2>&1; must $? ;;
+    qprobeset) timeout -k 10 120 python -u tools/queue_probe.py --set --extra 3 > gpurun_out/queue_probe_set.txt 2>&1; must $? ;;
+    legs:*)
+      l="${step#legs:}"
+      eval timeout -k 10 400 python -u bench.py --cpu-batches '""' --legs "${l//:/,}" $BENCH_ARGS > "gpurun_out/legs_${l//:/_}.log" 2>&1; must $? ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
