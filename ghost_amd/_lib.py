@@ -44,6 +44,7 @@ _SIGS = {
     "ghost_aei_forward": (i32, [vp, vp, i32, i64p, i32, vp, i32, i64, vp, vp, C.POINTER(vp), vp, i64, vp]),
     "ghost_aei_get_attr": (i32, [vp, vp, i32, i64p, i32, C.POINTER(vp), vp, i64, vp]),
     "ghost_aei_swap_u8": (i32, [vp, vp, i64, i32, vp, i32, i64, vp, vp, i64, vp]),
+    "ghost_aei_up_stream": (i32, [vp, i32, C.POINTER(vp)]),
     "ghost_aei_identity_table_bytes": (i64, [vp, i32]),
     "ghost_aei_identity_table_workspace_bytes": (i64, [vp, i32]),
     "ghost_aei_identity_table": (i32, [vp, vp, i32, i64, i32, vp, i64, vp, i64, vp]),

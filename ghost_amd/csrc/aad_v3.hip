@@ -826,6 +826,11 @@ GHOST_DEV void aad_v5_body(const AadV3ArgsT<T>& a) {
       d[4] = __float_as_int(r.flyA); d[5] = __float_as_int(r.flyB); d[6] = r.tbA; d[7] = r.tbB;
     }
   }
+  // lane 0 wrote the records, every lane of the wave reads them in rt_of: order the LDS stores before those loads
+  // explicitly (the wave-synchronous ordering is not a guarantee of the memory model)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   auto rt_of = [&](int i) -> RowT {
     const int* d = s_rt + (wid * IPWMAX + i / TPI) * 8;
     const int4 u0 = *reinterpret_cast<const int4*>(d), u1 = *reinterpret_cast<const int4*>(d + 4);

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -994,26 +995,44 @@ int64_t plan_bytes(ghost_aei* h, Mode mode, int B) {
   return (int64_t)(((c.off + 255) & ~size_t(255)) + kMainSlack + (c.dual ? 2 : 1) * scr + 256);
 }
 
-// the handle's up-path stream and events on device `dev` (the current device; created once per device);
-// false: this call runs on one stream
-bool ensure_up_stream(ghost_aei* h, int dev) {
-  auto it = h->up_path.find(dev);
-  if (it != h->up_path.end()) return it->second.s != nullptr;
-  ghost_aei::UpPath& u = h->up_path[dev];   // a failed creation leaves a null stream: one stream from then on
+// The up-path stream of device `dev`: ONE per device for the whole process, shared by every handle and never
+// destroyed.  A process gets 4 hardware queues per priority; streams created and destroyed with each handle (a
+// bench leg's second model, a GraphedSwap's runtime) churned that pool, and the D2H / video legs that ran after
+// such a leg lost the two-batch overlap (-14 %, tools/leg_probe.py).  The handles' up-path
+// work serialises on the shared stream, which it already did for the two batches in flight of one handle; every
+// call orders itself against it with its own events.  nullptr: creation failed (the calls run on one stream).
+hipStream_t shared_up_stream(int dev) {
+  static std::mutex mu;
+  static std::map<int, hipStream_t> streams;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = streams.find(dev);
+  if (it != streams.end()) return it->second;
   // the up path fills the CUs the generator's small low-resolution launches leave idle: its stream gets
   // the lowest priority, so the generator's workgroups dispatch first when both streams have work
   static const int low_prio = GHOST_KNOB("GHOST_UP_STREAM_LOWPRIO", 1);
   int least = 0, greatest = 0;
   if (!low_prio || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least) != hipSuccess) s = nullptr;
+  streams[dev] = s;
+  return s;
+}
+
+// the handle's up-path stream and events on device `dev` (the current device; events created once per device);
+// false: this call runs on one stream
+bool ensure_up_stream(ghost_aei* h, int dev) {
+  auto it = h->up_path.find(dev);
+  if (it != h->up_path.end()) return it->second.s != nullptr;
+  ghost_aei::UpPath& u = h->up_path[dev];   // a failed creation leaves a null stream: one stream from then on
   ghost_aei::UpPath tmp;
-  bool ok = hipStreamCreateWithPriority(&tmp.s, hipStreamNonBlocking, least) == hipSuccess;
+  tmp.s = shared_up_stream(dev);
+  bool ok = tmp.s != nullptr;
   for (auto& e : tmp.zev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&tmp.zend, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     for (auto e : tmp.zev)
       if (e) (void)hipEventDestroy(e);
     if (tmp.zend) (void)hipEventDestroy(tmp.zend);
-    if (tmp.s) (void)hipStreamDestroy(tmp.s);
     return false;
   }
   u = tmp;
@@ -1107,7 +1126,7 @@ extern "C" void ghost_aei_destroy(ghost_aei* h) {
     for (auto e : kv.second.zev)
       if (e) (void)hipEventDestroy(e);
     if (kv.second.zend) (void)hipEventDestroy(kv.second.zend);
-    if (kv.second.s) (void)hipStreamDestroy(kv.second.s);
+    // kv.second.s is the process's shared up-path stream (shared_up_stream): not the handle's to destroy
   }
   delete h;
 }
@@ -1228,6 +1247,13 @@ extern "C" int ghost_aei_swap_u8_indexed(ghost_aei* h, const uint8_t* crops, int
   io.table = const_cast<void*>(table); io.n_ident = n_ident; io.idx = identity_index;
   io.u8 = out_u8;
   return run(h, M_SWAP, B, io, ws, ws_bytes, stream);
+}
+
+extern "C" int ghost_aei_up_stream(ghost_aei* h, int device, void** stream) {
+  if (!h || !stream) return fail(GHOST_EINVAL, "null argument");
+  auto it = h->up_path.find(device);
+  *stream = it == h->up_path.end() ? nullptr : (void*)it->second.s;
+  return 0;
 }
 
 extern "C" int ghost_aei_profile(ghost_aei* h, int class_mask) {

@@ -104,11 +104,18 @@ def blend_image(full_frame: torch.Tensor, swaps: torch.Tensor, masks: torch.Tens
     if tuple(swaps.shape[1:3]) != (224, 224):
         swaps = resize_u8(swaps, (224, 224))          # image_processing.py:63
     masks = torch.as_tensor(masks).to(dev)
-    if masks.dtype != torch.float64:      # q/255 in float32 -> the float64 q/255.0 numpy computes
-        # a 256-entry table of numpy's correctly rounded q / 255 (torch's device division by a scalar multiplies by
-        # the reciprocal, which is not), indexed by the recovered q
-        lut = torch.from_numpy(np.arange(256, dtype=np.float64) / 255).to(dev)
-        masks = lut[torch.round(masks.to(torch.float32) * 255.0).clamp_(0, 255).to(torch.int64)]
+    if masks.dtype != torch.float64:
+        # a float32 / float16 q/255 mask (masks.face_masks) -> the float64 q/255.0 numpy computes: a 256-entry table
+        # of numpy's correctly rounded q / 255 (torch's device division by a scalar multiplies by the reciprocal,
+        # which is not), indexed by the recovered q.  Only when every value is such a q/255: any other
+        # soft mask is promoted to float64 unchanged
+        m32 = masks.to(torch.float32)
+        q = torch.round(m32 * 255.0)
+        if bool(((m32 * 255.0 - q).abs() <= 1e-3).all()) and bool(((q >= 0) & (q <= 255)).all()):
+            lut = torch.from_numpy(np.arange(256, dtype=np.float64) / 255).to(dev)
+            masks = lut[q.to(torch.int64)]
+        else:
+            masks = masks.to(torch.float64)
     masks = masks.contiguous()
     if tuple(masks.shape) != (J, 224, 224) or len(tfms) != J:
         raise RuntimeError("ghost_amd: blend_image needs J masks [224,224] and J transforms")

@@ -134,6 +134,10 @@ int ghost_aei_get_option(ghost_aei* h, int option, int* value);
  * NULL taps clears them. */
 int ghost_aei_set_taps(ghost_aei* h, void* const taps[8]);
 
+/* the handle's up-path stream on `device` (created by the first two-stream forward / swap there; NULL before, or
+ * when the handle runs on one stream): diagnostics of hardware-queue sharing (tools/leg_probe.py) */
+int ghost_aei_up_stream(ghost_aei* h, int device, void** stream);
+
 /* per-kernel-class device timing with HIP events (bench instrumentation).
  * class_mask bit i enables class i; classes: 0 AAD kernels (all stages), 1 the block-input AAD
  * kernel at 256x256 (through-upsample, aad_v4), 2 conv3x3 (all), 3 conv3x3 at 256x256, 4 IN stats + mask,

@@ -135,6 +135,13 @@ def test_blend_image_matches_get_final_image(seed):
         got = blend_image(fr, torch.from_numpy(swaps256), torch.from_numpy(m), tfms).cpu().numpy()
         d = np.abs(got.astype(np.int16) - ref.astype(np.int16))
         assert d.max() == 0, (m.dtype, d.max(), (d > 0).mean())
+    # a soft float32 mask that is not q/255 is taken as its own float64 values, not snapped
+    soft = (masks * 0.7 + 0.0013).astype(np.float32)
+    ref = R.get_final_image(list(swaps256), frame, tfms, list(soft.astype(np.float64)))
+    fr = torch.from_numpy(frame.copy()).to("cuda:0")
+    got = blend_image(fr, torch.from_numpy(swaps256), torch.from_numpy(soft), tfms).cpu().numpy()
+    d = np.abs(got.astype(np.int16) - ref.astype(np.int16))
+    assert d.max() == 0, ("soft", d.max(), (d > 0).mean())
 
 
 @pytest.mark.gpu
