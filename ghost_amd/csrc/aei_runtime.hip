@@ -79,6 +79,7 @@ struct ghost_aei {
     hipEvent_t zev[9] = {nullptr};
     hipEvent_t zend = nullptr;
   };
+
   std::map<int, UpPath> up_path;
   hipEvent_t* zev = nullptr;                   // the events of the device of the running call
   void* taps[8] = {nullptr};                   // ghost_aei_set_taps: AADBlk1..7 outputs copied here

@@ -500,8 +500,16 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   // W16: the epilogue writes 16-byte pieces (8 stores per wave; see there) — the two-block (Cin = 64) tiles of
   // the 256 x 256 stage only: with more blocks per tile the exchange's registers push the kernel into spills
   constexpr bool W16 = !EPX && NCB == 2 && IMG == 1 && !(DBG & 16);
+  // LDSW (round 5): the other exact-tile convs (NCB >= 4: the 128 x 128 .. 32 x 32 stages) stage the epilogue through
+  // the LDS of the tile's finished last stage — each wave writes its 64 pixels x 64 channels (8-byte pieces as the
+  // accumulators hold them; pixel rows of 128 bytes at a 136-byte pitch) and reads them back as whole 128-byte pixel
+  // rows, so its 8 global stores each write 8 whole rows (1 KB) instead of 16 stores of 8-byte quarter pieces.  The
+  // register exchange of W16 does the same at NCB = 2 but spills the NCB >= 4 kernels; the LDS path needs no
+  // extra live registers, only one barrier per tile (every wave past its last read of the stage).
+  constexpr int LPITCH = 136, LWAVE = 64 * LPITCH;
+  constexpr bool LDSW = !EPX && !W16 && IMG == 1 && !RESW && !(DBG & 16) && STAGE_B >= NW * LWAVE;
   const bool plain = !a.scale && !a.shift && a.slope == 1.f && !a.tanh_out;
-  constexpr int NST = ((DBG & 16) || EPX) ? 0 : (W16 ? 8 : 16) + (STATS ? 1 : 0);
+  constexpr int NST = ((DBG & 16) || EPX) ? 0 : ((W16 || LDSW) ? 8 : 16) + (STATS ? 1 : 0);
   if (nmine == 0) return;
   Tile cur = tile_of(0);
   set_dma_tile(cur);
@@ -556,9 +564,14 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       }
     }
     if constexpr (cb + 1 < NCB) return;
-    // epilogue: exactly 16 vector stores per wave (N % 64 == 0, full tiles) + 1 with STATS, the
-    // youngest VM ops when the next tile's first stage waits.  The residual tile is loaded as one
+    // epilogue: exactly 16 vector stores per wave (N % 64 == 0, full tiles; 8 with W16 / LDSW) + 1 with STATS,
+    // the youngest VM ops when the next tile's first stage waits.  The residual tile is loaded as one
     // batch first: a load between two stores would wait for the older store (in-order vmcnt)
+    unsigned char* stg = const_cast<unsigned char*>(buf) + wid * LWAVE;   // LDSW: this wave's part of the stage
+    if constexpr (LDSW) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();         // every wave has read its last fragments of this stage
+    }
     uint2 rraw[4][4];
     if (ares_) {
 #pragma unroll
@@ -648,6 +661,10 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
           acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
         if constexpr (W16) ov[j] = o;
+        else if constexpr (LDSW) {
+          // pixel q's row of 64 channels: this lane's 8 bytes are channels 16 j + 4 lq .. +3
+          *reinterpret_cast<uint2*>(stg + q * LPITCH + 32 * j + 8 * lq) = o;
+        }
         else if constexpr (!(DBG & 16)) *reinterpret_cast<uint2*>(ay_ + pix * a.ldy + n) = o;
         else if ((o.x ^ o.y) == 0x7fc00001u) *reinterpret_cast<uint2*>(ay_ + pix * a.ldy + n) = o;
         }
@@ -671,6 +688,22 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
         const long p0 = pix - lr + (lr & 7);
         store_rows16<T>(ay_ + cur.n0, p0 * a.ldy, (p0 + 8) * a.ldy, lr, (lq >> 1) + 2 * (lq & 1),
                         u32x4{a0.x, a0.y, a1.x, a1.y}, u32x4{b0.x, b0.y, b1.x, b1.y});
+      }
+    }
+    if constexpr (LDSW) {
+      // the wave's tile back as whole rows: store s writes pixels 8 s .. 8 s + 7 (consecutive columns of one tile
+      // row), lane L chunk L & 7 of pixel 8 s + L / 8 (LDS ops of a wave complete in order: no wait between the
+      // writes above and these reads)
+      asm volatile("" ::: "memory");
+      const int c = lane & 7, q0 = lane >> 3;
+      // the wave's first pixel and this lane's pixel / chunk within a store (element offsets)
+      T* __restrict__ yw = ay_ + (cur.base + (long)(cur.y0 + G::hrow0(wid)) * a.W + cur.x0) * a.ldy + cur.n0;
+      const int lo = q0 * a.ldy + c * 8;
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const int q = 8 * st + q0;   // tile row st / 4, columns 8 (st % 4) .. +7
+        const u32x4 v = *reinterpret_cast<const u32x4*>(stg + q * LPITCH + c * 16);
+        *reinterpret_cast<u32x4*>(yw + ((st >> 2) * a.W + 8 * (st & 3)) * a.ldy + lo) = v;
       }
     }
     if constexpr (STATS) {
