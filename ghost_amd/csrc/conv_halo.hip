@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   constexpr bool EPX = G::TW == 16;   // small tiles: overhang masking + the extended epilogue
   static_assert(!(EPX && STATS), "IN partials only from exact tiles");
   // DBG (experiments only, GHOST_HALO_DBG): 2 no halo DMA, 4 no weight DMA, 8 no LDS reads/MFMA,
-  // 16 no output stores
+  // 16 no output stores, 32 no epilogue, 64 no fragment reads after tap 1 (MFMAs on stale fragments)
   // RESW: Cin <= 64 and N == 64 — the whole weight tensor (<= 2 blocks x 36 KB) stays resident in
   // LDS for the kernel and only the halo (39 KB) streams per stage; otherwise every stage carries
   // its channel block's 9 x 64 weight rows too (75 KB).
@@ -509,7 +509,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   constexpr int LPITCH = 136, LWAVE = 64 * LPITCH;
   constexpr bool LDSW = !EPX && !W16 && IMG == 1 && !RESW && !(DBG & 16) && STAGE_B >= NW * LWAVE;
   const bool plain = !a.scale && !a.shift && a.slope == 1.f && !a.tanh_out;
-  constexpr int NST = ((DBG & 16) || EPX) ? 0 : ((W16 || LDSW) ? 8 : 16) + (STATS ? 1 : 0);
+  constexpr int NST = ((DBG & 48) || EPX) ? 0 : ((W16 || LDSW) ? 8 : 16) + (STATS ? 1 : 0);
   if (nmine == 0) return;
   Tile cur = tile_of(0);
   set_dma_tile(cur);
@@ -552,18 +552,49 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
     // (measured: the same time as one register set read then used, and with s_setprio around the MFMAs)
     if constexpr ((DBG & 8) == 0) {
       load_frags(0, wf[0], pf[0]);
+      if constexpr ((DBG & 64) != 0) load_frags(1, wf[1], pf[1]);
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        asm volatile("" ::: "memory");
-        if (tap + 1 < 9) load_frags(tap + 1, wf[(tap + 1) & 1], pf[(tap + 1) & 1]);
+        // this tap's fragments (issued during the previous tap's MFMAs) have landed: wait for them BEFORE issuing
+        // the next tap's 8 reads — after those the wave has 16 LDS reads outstanding, more than the 4-bit lgkmcnt
+        // can distinguish, and the compiler's own wait (placed at the first MFMA) would be lgkmcnt(0)
+        if constexpr ((DBG & 128) == 0) __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (tap + 1 < 9 && (DBG & 64) == 0) load_frags(tap + 1, wf[(tap + 1) & 1], pf[(tap + 1) & 1]);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             acc[j][i] = mfma16x16x32<T>(wf[tap & 1][j], pf[tap & 1][i], acc[j][i]);
+        // the software pipeline pinned (round 5): tap + 1's 8 fragment reads go out one per MFMA over the first half
+        // of this tap's 16 MFMAs, which then run while they land.  Left to itself the scheduler sank the reads to
+        // their first use, and every tap waited two or three times on LDS reads it had just issued.
+        if constexpr ((DBG & 128) == 0) {
+          if (tap + 1 < 9 && (DBG & 64) == 0) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);   // the 8 DS reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);  // then the 16 MFMAs
+          } else {
+            __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          asm volatile("" ::: "memory");
+        }
       }
     }
     if constexpr (cb + 1 < NCB) return;
+    if constexpr ((DBG & 32) != 0) {   // (experiments) no epilogue: the accumulators only kept alive
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          t += acc[j][i][0] + acc[j][i][1] + acc[j][i][2] + acc[j][i][3];
+          acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      if (__float_as_uint(t) == 0x7fc00123u) ay_[lane] = (T)t;
+      return;
+    }
     // epilogue: exactly 16 vector stores per wave (N % 64 == 0, full tiles; 8 with W16 / LDSW) + 1 with STATS,
     // the youngest VM ops when the next tile's first stage waits.  The residual tile is loaded as one
     // batch first: a load between two stores would wait for the older store (in-order vmcnt)
@@ -1040,6 +1071,8 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
       GHOST_PP_DBG(true, 2, 2) GHOST_PP_DBG(true, 2, 8) GHOST_PP_DBG(true, 2, 16) GHOST_PP_DBG(true, 2, 18)
       GHOST_PP_DBG(true, 2, 26) GHOST_PP_DBG(true, 2, 24)
       GHOST_PP_DBG(false, 4, 6) GHOST_PP_DBG(false, 4, 8) GHOST_PP_DBG(false, 4, 16) GHOST_PP_DBG(false, 4, 22)
+      GHOST_PP_DBG(false, 4, 54) GHOST_PP_DBG(false, 4, 118) GHOST_PP_DBG(false, 4, 38) GHOST_PP_DBG(false, 4, 64)
+      GHOST_PP_DBG(false, 4, 86)
       GHOST_PP_DBG(false, 8, 6) GHOST_PP_DBG(false, 8, 8) GHOST_PP_DBG(false, 8, 16) GHOST_PP_DBG(false, 8, 22)
       GHOST_PP_DBG(false, 8, 24) GHOST_PP_DBG(false, 8, 30) GHOST_PP_DBG(false, 8, 2) GHOST_PP_DBG(false, 8, 4)
 #undef GHOST_PP_DBG
