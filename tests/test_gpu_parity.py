@@ -574,15 +574,18 @@ def _lib_mod():
 
 
 def test_full_batch64_bf16_properties_and_fp32_rows(lib):
-    """B=64 (the bench configuration): batch independence and oracle parity on sampled rows."""
+    """B=64 (the bench configuration): every one of the 64 fp32 rows (and their 8 attribute maps) against the oracle's
+    batched forward within 1e-3 (was 3 sampled rows), then the bf16 gate on four rows."""
     G32 = model("unet", 2)
     xt, z = aei_ref.make_inputs(64, 11)
-    Y, _ = G32(xt.to(DEV), z.to(DEV))
+    Y, attr = G32(xt.to(DEV), z.to(DEV))
     Ycpu = Y.cpu()
     p = weights("unet", 2)
-    for r in (0, 37, 63):
-        yr, _ = aei_ref.aei_forward(p, xt[r:r + 1], z[r:r + 1])
-        assert float((Ycpu[r:r + 1] - yr).abs().max()) <= 1e-3, r
+    yr, ar = aei_ref.aei_forward(p, xt, z)          # the whole batch on the CPU (~20 s on the box's 16 threads)
+    err = (Ycpu - yr).abs().amax(dim=(1, 2, 3))
+    assert float(err.max()) <= 1e-3, (int(err.argmax()), float(err.max()))
+    for k, (a, b) in enumerate(zip(attr, ar)):
+        assert float((a.cpu() - b).abs().max()) <= 1e-3, k
     Gb = model("unet", 2, compute_dtype=torch.bfloat16)
     Yb, _ = Gb(xt.to(DEV), z.to(DEV))
     # single frames are too few pixels for a steady end-to-end statistic: the B = 1 kernel set is
