@@ -595,6 +595,20 @@ def latency_leg(dev, n=20):
             lat.append(t2 - t0)
         out[name] = {"latency_ms": round(float(np.median(lat)) * 1e3, 3),
                      "host_ms": round(float(np.median(host)) * 1e3, 3)}
+        # the same swap with the source identity's projections prepared once (AEI_Net.identity_table: inference.py
+        # embeds the source once and swaps it into every target image), one gather instead of the two GEMMs
+        table = G.identity_table(z)
+        idx = torch.zeros(1, dtype=torch.int32, device=dev)
+        for _ in range(3):
+            G.swap_u8_indexed(crop, table, idx, out=y)
+        torch.cuda.synchronize()
+        lat = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            G.swap_u8_indexed(crop, table, idx, out=y)
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t0)
+        out[name]["identity_table_latency_ms"] = round(float(np.median(lat)) * 1e3, 3)
         # the same swap replayed as one HIP graph (ghost_amd.inference.GraphedSwap: inputs copied into the
         # captured buffers, one hipGraphLaunch; identical bytes); at B = 1 the plan is one chain of kernels
         # whatever two_streams says (batches under 8 frames run on one stream), so one capture is timed

@@ -1164,12 +1164,17 @@ static bool v5_pairing_ok(const Up2xSrc& u) {
 
 // pixels per workgroup: one sample's block; C = 256 stages its weights once per 1024 pixels, and so may the
 // C = 128 layers (128 x 128 stage: GHOST_V3_PPW128, A/B knob)
-static int v3_ppw(int HW, int C) {
+// B > 0: a small batch halves the C = 128 / 256 workgroups (down to 256 pixels, a multiple of the 8 waves' 16-pixel
+// tiles in pairs) while the grid has fewer than 128 of them (B = 1, 128 x 128 block-input pair: 32 -> 64 workgroups)
+static int v3_ppw(int HW, int C, long B = 0) {
+  int ppw = (HW >= 65536 || C == 256) ? 1024 : 512;
   if (C == 128) {
     static const int p128 = GHOST_KNOB("GHOST_V3_PPW128", 512);
-    if ((p128 == 1024 || p128 == 2048) && HW % p128 == 0) return p128;
+    if ((p128 == 1024 || p128 == 2048) && HW % p128 == 0) ppw = p128;
   }
-  return (HW >= 65536 || C == 256) ? 1024 : 512;
+  if (B > 0 && C != 64)
+    while (ppw > 256 && B * HW / ppw < 128) ppw /= 2;
+  return ppw;
 }
 
 // the v5 kernel's work items per workgroup if it takes this launch, else 0
@@ -1201,11 +1206,12 @@ static int v5_takes(const AadV3Desc& d, int zpm) {
   }
   if (d.C != 64 || v3_ppw(d.HW, d.C) != 1024 || ipw < 1 || d.up_H % rt || (d.up_H / rt) % ipw) return 0;
   if (!(d.Ca == 64 || d.Ca == 32) || (zpm && d.L != 2) || ipw > 2) return 0;   // the kernel holds <= 2 row tiles
-  return ipw;
+  // one work item per workgroup where two would leave the grid under a round of workgroups (B = 1: 32 -> 64)
+  return (long)d.B * d.HW / 1024 / ipw >= 256 ? ipw : 1;
 }
 
 int aad_v3_clock_words(const AadV3Desc& d) {
-  long grid = (long)d.B * d.HW / v3_ppw(d.HW, d.C);
+  long grid = (long)d.B * d.HW / v3_ppw(d.HW, d.C, d.B);
   int zpm = 0;
   for (int l = 0; l < d.L; ++l) zpm |= d.zw[l] ? 1 << l : 0;
   if (const int ipw = v5_takes(d, zpm)) grid = (long)d.B * d.HW / 1024 / ipw;
@@ -1221,7 +1227,7 @@ bool aad_v3_supported(int dt, int B, int HW, int C, int Ca, int lda, int ldh, in
   const bool shape = (C == 64 && (Ca == 64 || Ca == 32)) || (C == 128 && (Ca == 128 || Ca == 64 || Ca == 32)) ||
                      (c256 && C == 256 && (Ca == 128 || Ca == 64));
   if (!shape || lda % 8 || ldh % 8 || ldo % 8) return false;
-  const int ppw = v3_ppw(HW, C);
+  const int ppw = v3_ppw(HW, C, B);
   return HW % ppw == 0 && (long)B * HW / ppw >= 32;
 }
 
@@ -1234,7 +1240,7 @@ static int aad_v3_t(const AadV3Desc& d, hipStream_t s) {
     a.idgb[l] = d.idgb[l]; a.out[l] = (T*)d.out[l]; a.ldo[l] = d.ldo[l];
   }
   a.lda = d.lda; a.ldh = d.ldh; a.id_ld = d.id_ld; a.HW = d.HW; a.slope = d.slope;
-  a.PPW = v3_ppw(d.HW, d.C);
+  a.PPW = v3_ppw(d.HW, d.C, d.B);
   int zpm = 0;
   for (int l = 0; l < d.L; ++l)
     if (d.zw[l]) {

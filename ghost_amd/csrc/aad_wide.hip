@@ -345,8 +345,11 @@ static bool aad_gemm_ok(const AadWideDesc& d) {
   // Ca = 512 only: at Ca = 256 (the 32x32 stage) four K stages do not amortise the tile's prologue and
   // epilogue at one workgroup per CU (measured 80-86 us against aad_wide's 52-57 us; Ca = 512: 62-66
   // against 78-83 us)
+  // and only where the 256 x 256 tiles make half a round of workgroups: at B = 1 the 16 x 16 stage is 8 of them
+  // (28-32 us each, profiles/r05_step_trace_b1.txt); aad_wide's 16-pixel workgroups spread the layer over the CUs
+  const long wgs = (long)d.B * d.HW / 256 * (d.C / 128);
   return on && d.HW % 256 == 0 && d.C % 128 == 0 && d.Ca == 512 && d.lda % 8 == 0 &&
-         d.ldh % 8 == 0 && d.ldo % 8 == 0 && (uintptr_t)d.za % 16 == 0 && (uintptr_t)d.w3 % 16 == 0;
+         d.ldh % 8 == 0 && d.ldo % 8 == 0 && (uintptr_t)d.za % 16 == 0 && (uintptr_t)d.w3 % 16 == 0 && wgs >= 128;
 }
 
 template <typename T>

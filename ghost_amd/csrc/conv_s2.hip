@@ -227,6 +227,9 @@ bool conv4x4s2_patch_supported(const ConvDesc& d) {
   const int Ho = d.Hi / 2, Wo = d.Wi / 2;
   if (Ho % TH || Wo % TW || d.ldy % 4 || (uintptr_t)d.y % 8) return false;
   if ((uintptr_t)d.scale % 16 || (uintptr_t)d.shift % 16) return false;
+  // one workgroup per output tile and 64 channels, the whole reduction each: under 32 of them (B = 1: the 16 x 16 and
+  // 32 x 32 outputs, 8 and 16 workgroups, 27 and 15 us) the implicit GEMM's split K spreads the conv wider
+  if ((long)d.B * (Ho / TH) * (Wo / TW) * (d.N / BN) < 32) return false;
   return (long)d.Hi * d.Wi * d.ldx < (1L << 31);
 }
 

@@ -276,14 +276,20 @@ int in_stats_from_tiles(const float* part, int B, int nrec, int C, float* stat, 
   return (int)hipGetLastError();
 }
 
-static void stats_geometry(int HW, int& chunk, int& nchunk) {
+// chunk: pixels per workgroup (<= 1024); smaller while the grid (chunks x 64-channel groups x samples) has fewer than
+// 256 workgroups, down to 64 pixels and to at most 16 chunks (the final kernel sums a (sample, channel)'s chunks in
+// one thread) — B = 1: one 256-pixel chunk per channel group was 16 workgroups, 14 us
+static void stats_geometry(int B, int HW, int C, int& chunk, int& nchunk) {
   chunk = HW < 1024 ? HW : 1024;
+  const long groups = (long)B * ((C + 63) / 64);
+  while (chunk > 64 && groups * ((HW + chunk - 1) / chunk) < 256 && (HW + chunk / 2 - 1) / (chunk / 2) <= 16)
+    chunk /= 2;
   nchunk = (HW + chunk - 1) / chunk;
 }
 
 size_t in_stats_workspace_bytes(int B, int HW, int C) {
   int chunk, nchunk;
-  stats_geometry(HW, chunk, nchunk);
+  stats_geometry(B, HW, C, chunk, nchunk);
   const int nrec = nchunk > HW / 512 ? nchunk : HW / 512;   // >= in_stats_up_quad_kernel's records
   // + the upsample weight tables of in_stats_up_quad_kernel (6 x max(H, W) <= 6 x 4096 floats)
   return (size_t)B * nrec * C * 2 * sizeof(float) + 6 * 4096 * sizeof(float) + 256;
@@ -299,7 +305,7 @@ template <typename T>
 static void in_stats_launch(const T* x, int ldx, int B, int HW, int C, float* stat, float* part, const Up2xSrc* up,
                             hipStream_t s) {
   int chunk, nchunk;
-  stats_geometry(HW, chunk, nchunk);
+  stats_geometry(B, HW, C, chunk, nchunk);
   dim3 g1(nchunk, (C + 63) / 64, B);
   dim3 g2((B * C + 255) / 256);
   const Up2xSrc u = up ? *up : Up2xSrc{0, 0, 0.f, 0.f};

@@ -11,6 +11,7 @@
 #   quick          bench.py without legs / CPU baseline                    -> gpurun_out/quick.log
 #   quick1         the same with one batch in flight (--streams 1)         -> gpurun_out/quick1.log
 #   trace          one-stream kernel trace, per-step kernel sequence       -> gpurun_out/step_trace.txt
+#   trace1         the same at B = 1                                       -> gpurun_out/step_trace_b1.txt
 #   ops:NAME       tools/bench_ops.py --only NAME                          -> gpurun_out/ops_NAME.log
 #   profile        the round's committed profile set (tools/profile_round.sh, ROUND=rNN)
 #   ab:LIB         bench.py quick with GHOST_LIB_FILE=LIB (same-box A/B)   -> gpurun_out/ab_LIB.log
@@ -43,6 +44,10 @@ for step in "$@"; do
     bench) timeout -k 10 600 python -u bench.py > gpurun_out/bench.log 2>&1; must $? ;;
     quick) eval timeout -k 10 300 python -u bench.py $Q $BENCH_ARGS > gpurun_out/quick.log 2>&1; must $? ;;
     quick1) eval timeout -k 10 300 python -u bench.py $Q --streams 1 $BENCH_ARGS > gpurun_out/quick1.log 2>&1; must $? ;;
+    trace1)
+      rm -rf /tmp/gt1
+      eval timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/gt1 -o run -- python3 bench.py --batch 1 --steps 5 --warmup 3 $Q --no-profile --streams 1 $BENCH_ARGS > gpurun_out/trace1.log 2>&1; must $?
+      python3 tools/step_trace.py /tmp/gt1/run_results.db > gpurun_out/step_trace_b1.txt ;;
     trace)
       rm -rf /tmp/gt
       eval timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/gt -o run -- python3 bench.py --steps 3 --warmup 2 $Q --no-profile --streams 1 $BENCH_ARGS > gpurun_out/trace.log 2>&1; must $?
