@@ -18,6 +18,7 @@
 #   knobs:SPECS    bench.py quick through the tuning build, one run per spec and --streams 1 / 2; SPECS is
 #                  ';'-separated env settings, e.g. "GHOST_V5_IPW=1;GHOST_V5_IPW=2;GHOST_AAD_V5=0"
 #                                                                          -> gpurun_out/ab_knobs.txt
+#   envab:SPECS    bench.py quick (40 steps) once per ';'-separated env setting (shipping build) -> gpurun_out/ab_env.txt
 #   streams:LIST   bench.py quick at --streams N for N in the ','-list     -> gpurun_out/ab_streams.txt
 #   arc:LIST       tools/run_arc.py N for N in the ','-list (ArcFace)      -> gpurun_out/arc_batch.txt
 #   arctrace:N     kernel trace of tools/run_arc.py N (ArcFace)            -> gpurun_out/arc_kt_N.txt
@@ -63,6 +64,13 @@ for step in "$@"; do
           rc=$?; [ $rc -eq 0 ] || cp /tmp/o.log gpurun_out/knobs_fail.log; must $rc
           last /tmp/o.log "$v streams=$st" >> gpurun_out/ab_knobs.txt
         done
+      done ;;
+    envab:*)
+      IFS=';' read -ra specs <<< "${step#envab:}"
+      for v in "${specs[@]}"; do
+        eval env $v timeout -k 10 200 python -u bench.py $Q --steps 40 $BENCH_ARGS > /tmp/o.log 2>&1
+        rc=$?; [ $rc -eq 0 ] || cp /tmp/o.log gpurun_out/envab_fail.log; must $rc
+        last /tmp/o.log "$v" >> gpurun_out/ab_env.txt
       done ;;
     streams:*)
       IFS=',' read -ra ns <<< "${step#streams:}"
