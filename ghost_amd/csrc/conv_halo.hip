@@ -385,7 +385,10 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   __shared__ __attribute__((aligned(1024))) unsigned char ldsw[RESW ? 2 * WBLK_B : 16];
   __shared__ __attribute__((aligned(16))) float s_sc[NMAX], s_sh[NMAX];   // N <= NMAX (conv3x3_pp_takes / conv3x3_halo)
   __shared__ __attribute__((aligned(16))) float s_ex[EPX ? 3 * NMAX : 4];   // PReLU slope, scale2, shift2 (EPX)
-  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4, wid = tid >> 6;
+  // wid through readfirstlane: the DMA pieces' conditions and LDS destinations are then wave-uniform (scalar branches,
+  // m0 from SGPRs) instead of exec-masked per-lane code at every stage top
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lq = lane >> 4,
+            wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int prow = lane >> 2, slot = lane & 3;
 
   for (int n = tid; n < a.N; n += NW * 64) {
