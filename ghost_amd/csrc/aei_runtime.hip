@@ -70,7 +70,7 @@ struct ghost_aei {
   std::map<std::string, const void*> slots;   // name -> device pointer (nullptr = unbound)
   int id_total = 0;                            // sum over AAD layers of 2*c_x
   // per-handle plan options (ghost_aei_set_option); defaults are the measured choices
-  int opt[GHOST_AEI_NOPT] = {1, 1, 1, GHOST_KNOB("GHOST_AAD_ZP", 2)};
+  int opt[GHOST_AEI_NOPT] = {1, 1, 1, GHOST_KNOB("GHOST_AAD_ZP", 2), 1};
   // GHOST_AEI_OPT_TWO_STREAMS: the encoder up path's stream and its events, one set per device (created
   // on first use on the device of the caller's stream): zev[k] = z_attr_k written (k = 2..8), zev[0] = the
   // down path done, zev[1] = idgb / m1 ready; zend = everything this call queued on the up stream
@@ -128,6 +128,9 @@ namespace {
 // ---------------------------------------------------------------------------
 // execution context: dry run (sizing) or real run (launches)
 // ---------------------------------------------------------------------------
+constexpr int kSemWords = 4096;                  // arrival counters per stream (16 KB)
+constexpr size_t kSemBytes = 2 * kSemWords * sizeof(unsigned);   // the main and the up-path stream's sets
+
 struct Ctx {
   ghost_aei* h;
   bool dry;
@@ -143,6 +146,11 @@ struct Ctx {
   int dev = 0;
   hipStream_t s_up = nullptr;
   char* scratch_up = nullptr;
+  // arrival counters of the fused reductions (split-K fix-up, InstanceNorm final pass): one set per stream,
+  // zeroed once per call before the first launch and left zero by every launch (GHOST_AEI_OPT_FUSE_REDUCE)
+  unsigned* sem_main = nullptr;
+  unsigned* sem_up = nullptr;
+  unsigned* sem() const { return scratch_up && scratch == scratch_up ? sem_up : sem_main; }
   int rc = 0;
   std::string where;
 
@@ -216,6 +224,8 @@ void run_conv(Ctx& c, ConvDesc& d, int cls_all, int cls_big, double flops) {
   const bool big = d.Hi == 256 || d.Hi * (d.kind == CONV_T4S2 ? 2 : 1) == 256;
   int e_all = c.prof_begin(cls_all);
   int e_big = (big && cls_big >= 0) ? c.prof_begin(cls_big) : -1;
+  d.sem = c.sem();
+  d.nsem = d.sem ? kSemWords : 0;
   c.check(conv_launch(d, c.scratch, c.scratch_cap, c.s), "conv_launch");
   double bytes = 0;
   if (d.epi == EPI_AAD) {
@@ -235,7 +245,9 @@ void run_stats(Ctx& c, const void* x, int ldx, int B, int HW, int C, float* stat
     return;
   }
   int e = c.prof_begin(4);
-  c.check(in_stats(c.h->dt, x, ldx, B, HW, C, stat, c.scratch, c.scratch_cap, c.s), "in_stats");
+  unsigned* sem = c.sem();
+  c.check(in_stats(c.h->dt, x, ldx, B, HW, C, stat, c.scratch, c.scratch_cap, c.s, sem, sem ? kSemWords : 0),
+          "in_stats");
   c.prof_end(4, e, (double)B * HW * C * c.h->esz, 0);
 }
 
@@ -248,7 +260,9 @@ void run_stats_up(Ctx& c, const void* x, int ldx, int B, int H, int W, int C, fl
     return;
   }
   int e = c.prof_begin(4);
-  c.check(in_stats_up2x(c.h->dt, x, ldx, B, H, W, C, stat, c.scratch, c.scratch_cap, c.s), "in_stats_up2x");
+  unsigned* sem = c.sem();
+  c.check(in_stats_up2x(c.h->dt, x, ldx, B, H, W, C, stat, c.scratch, c.scratch_cap, c.s, sem, sem ? kSemWords : 0),
+          "in_stats_up2x");
   c.prof_end(4, e, (double)B * H * W * C * c.h->esz, 0);
 }
 
@@ -993,7 +1007,7 @@ int64_t plan_bytes(ghost_aei* h, Mode mode, int B) {
   plan(c, mode, B, io);
   if (!c.ok()) return (int64_t)c.rc;
   const size_t scr = (c.scratch_need + 255) & ~size_t(255);
-  return (int64_t)(((c.off + 255) & ~size_t(255)) + kMainSlack + (c.dual ? 2 : 1) * scr + 256);
+  return (int64_t)(((c.off + 255) & ~size_t(255)) + kMainSlack + kSemBytes + (c.dual ? 2 : 1) * scr + 256);
 }
 
 // The up-path stream of device `dev`: ONE per device for the whole process, shared by every handle and never
@@ -1069,19 +1083,27 @@ int run(ghost_aei* h, Mode mode, int B, const Io& io, void* ws, int64_t ws_bytes
   if (!dry.ok()) return fail(dry.rc, dry.where);
   const size_t main_bytes = ((dry.off + 255) & ~size_t(255)) + kMainSlack;
   const size_t scr = (dry.scratch_need + 255) & ~size_t(255);
-  const size_t need = main_bytes + (dry.dual ? 2 : 1) * scr + 256;
+  const size_t need = main_bytes + kSemBytes + (dry.dual ? 2 : 1) * scr + 256;
   if (!ws || (size_t)ws_bytes < need)
     return fail(GHOST_ENOWS, "workspace too small: need " + std::to_string(need) + " bytes");
   Ctx c{};
   c.h = h; c.dry = false;
   c.base = (char*)(((uintptr_t)ws + 255) & ~uintptr_t(255));
   c.cap = main_bytes;
-  c.scratch = c.base + main_bytes;
+  c.scratch = c.base + main_bytes + kSemBytes;
   c.scratch_cap = dry.scratch_need;
   c.s = (hipStream_t)stream;
   DeviceGuard guard(c.s);
   if (!guard.ok) return fail(GHOST_EINVAL, "cannot make the device of the caller's stream current");
   c.dev = guard.dev;
+  if (h->opt[GHOST_AEI_OPT_FUSE_REDUCE]) {
+    // the counters start at zero (the workspace is the caller's memory); queued before every launch of the call,
+    // which the up-path stream's launches follow through its events
+    unsigned* sem = (unsigned*)(c.base + main_bytes);
+    if (hipMemsetAsync(sem, 0, kSemBytes, c.s) != hipSuccess) return fail(GHOST_EINVAL, "counter reset failed");
+    c.sem_main = sem;
+    c.sem_up = sem + kSemWords;
+  }
   if (dry.dual && ensure_up_stream(h, c.dev)) {
     c.s_up = h->up_path[c.dev].s;
     h->zev = h->up_path[c.dev].zev;

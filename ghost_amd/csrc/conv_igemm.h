@@ -59,6 +59,11 @@ struct ConvDesc {
   // it (conv3x3_pp_takes): per (sample, tile, wave, channel) the mean and centred sum of squares of
   // 64 pixels; in_stats_from_tiles() merges them in fp64 into [B][C][2] mean / rstd
   float* in_part = nullptr;
+  // optional arrival counters (zero on entry, left zero): a split-K GEMM whose partial tiles are small enough
+  // reduces them in the last of each tile's workgroups to finish instead of a second kernel (same sums, same
+  // order, same bytes).  Needs one word per (tile, phase); launches on one stream may share the words.
+  unsigned* sem = nullptr;
+  int nsem = 0;
 };
 
 // bytes of fp32 split-K workspace the launch may use

@@ -48,6 +48,8 @@ struct ConvArgs {
   float slope;
   int tanh_out;
   int nmajor;           // 1: tiles ordered N-major, so each XCD's contiguous run of tiles shares weight rows
+  unsigned* sem;        // split-K fix-up counters, one per (phase, tile) (nullptr: splitk_reduce_kernel follows)
+  int fuse;             // the fix-up's epilogue: 1 = standard, 2 = AAD
 };
 
 // ---------------------------------------------------------------------------
@@ -104,6 +106,67 @@ GHOST_DEV long out_pixel(const ConvArgs& a, long m, int py, int px) {
   const int r = (int)(m - (long)b * HW);
   const int qy = r / a.Wo, qx = r - qy * a.Wo;
   return ((long)b * (2 * a.Ho) + 2 * qy + py) * (2 * a.Wo) + 2 * qx + px;
+}
+
+// Split-K fix-up, run by every workgroup of a KEPI_SPLIT launch after its partial tile is stored (st_dev): the
+// last of a tile's nsplit workgroups to arrive (a counter per (phase, tile), zeroed per call and reset by that
+// workgroup) sums the tile's nsplit partials in split order from 0 — splitk_reduce_kernel's order, so the output
+// bytes are the same — and applies the epilogue.  Saves the reduction's launch (the small-M GEMMs of the
+// generator's 2x2..8x8 stages and the encoder's low-resolution convs each had one).  Only for tiles whose
+// partials fit `stage` (the kernel's own LDS, free after the K loop): the last arriver first pulls all of them
+// into LDS with one batch of independent device-scope loads per thread (a dependent load per split costs a
+// fabric round trip each, cdna_hip_programming.md §6 item 2), then sums from LDS.
+template <typename TO, int BM, int BN, int NTHR>
+GHOST_DEV void split_fixup(const ConvArgs& a, int tid, int tile_id, int m0, int n0, int par, float* stage) {
+  if (!last_arrival(a.sem + tile_id, (unsigned)a.nsplit)) return;
+  const int py = par >> 1, px = par & 1;
+  const int mrows = min(BM, a.M - m0);
+  const long sstride = (long)a.M * a.NT;
+  const float* pbase = a.partial + (long)par * a.nsplit * sstride + (long)m0 * a.NT + n0;
+  // stage[s][r][q] = partial of split s, tile row r, tile column q (q < BN: the whole tile width, inside NT)
+  const int per_split = mrows * BN, total = a.nsplit * per_split;
+  constexpr int U = 8;
+  for (int f0 = tid; f0 < total; f0 += U * NTHR) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int f = min(f0 + u * NTHR, total - 1);   // clamped, not skipped: every load issued before any use
+      const int sp = f / per_split, e = f - sp * per_split;
+      const int r = e / BN, q = e - r * BN;
+      v[u] = ld_dev(pbase + sp * sstride + (long)r * a.NT + q);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (f0 + u * NTHR < total) stage[f0 + u * NTHR] = v[u];
+  }
+  __syncthreads();
+  if (a.fuse == 1) {
+    const int ncol = min(BN, a.N - n0);
+    for (int i = tid; i < mrows * ncol; i += NTHR) {
+      const int r = i / ncol, q = i - r * ncol;
+      float v = 0.f;
+      for (int sp = 0; sp < a.nsplit; ++sp) v += stage[sp * per_split + r * BN + q];
+      const long op = out_pixel(a, m0 + r, py, px);
+      store_std<TO>(a, epi_std<TO>(a, v, n0 + q, op), n0 + q, op);
+    }
+  } else {
+    constexpr int CH = BN / 2;   // AAD channels per tile row: column pairs (gamma, beta) 16 apart
+    for (int i = tid; i < mrows * CH; i += NTHR) {
+      const int r = i / CH, cc = i - r * CH;
+      const long m = m0 + r;
+      const int q = (cc >> 4) * 32 + (cc & 15), ng = n0 + q;
+      const int c = (ng >> 5) * 16 + (ng & 15);
+      if (c >= a.C_aad) continue;
+      float ga = 0.f, ba = 0.f;
+      for (int sp = 0; sp < a.nsplit; ++sp) {
+        ga += stage[sp * per_split + r * BN + q];
+        ba += stage[sp * per_split + r * BN + q + 16];
+      }
+      ga += a.shift[ng];
+      ba += a.shift[ng + 16];
+      reinterpret_cast<TO*>(a.y)[m * a.ldy + c] = from_f<TO>(epi_aad<TO>(a, ga, ba, c, m));
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -309,7 +372,10 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
       if constexpr (EPI == KEPI_SPLIT) {
         float* dst = a.partial + (((long)par * a.nsplit + split) * a.M + m) * a.NT;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) dst[n0 + wn * WTN + j * 16 + lr] = acc[i][j][r];
+        for (int j = 0; j < TN; ++j) {
+          if (a.sem) st_dev(dst + n0 + wn * WTN + j * 16 + lr, acc[i][j][r]);
+          else dst[n0 + wn * WTN + j * 16 + lr] = acc[i][j][r];
+        }
       } else if constexpr (EPI == KEPI_STD) {
         const long op = out_pixel(a, m, py, px);
 #pragma unroll
@@ -332,6 +398,8 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(const ConvArgs a) {
       }
     }
   }
+  if constexpr (EPI == KEPI_SPLIT)
+    if (a.sem) split_fixup<TO, BM, BN, 256>(a, tid, par * gridDim.x + tile, m0, n0, par, reinterpret_cast<float*>(smem));
 }
 
 // split-K reduction + epilogue: one thread per (pixel, channel) [STD] or (pixel, AAD channel)
@@ -535,6 +603,28 @@ __global__ void __launch_bounds__(WSL ? 512 : 256) conv_glds_kernel(const ConvAr
       for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32<T>(af[i], bfv[j], acc[i][j]);
   }
 
+  if constexpr (EPI == KEPI_SPLIT) {
+    if (computes) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
+          if (m >= a.M) continue;
+          float* dst = a.partial + (((long)par * a.nsplit + split) * a.M + m) * a.NT;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if (a.sem) st_dev(dst + n0 + wn * WTN + j * 16 + lr, acc[i][j][r]);
+            else dst[n0 + wn * WTN + j * 16 + lr] = acc[i][j][r];
+          }
+        }
+      }
+    }
+    // (the DMA waves stay for the fix-up: its barriers count every wave, and they share its reduction)
+    if (a.sem)
+      split_fixup<TO, BM, BN, WSL ? 512 : 256>(a, tid, par * gridDim.x + tile, m0, n0, par, reinterpret_cast<float*>(lds));
+    return;
+  }
   if (!computes) return;
   // ---- epilogue (as v1) ----
 #pragma unroll
@@ -543,11 +633,7 @@ __global__ void __launch_bounds__(WSL ? 512 : 256) conv_glds_kernel(const ConvAr
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + wm * WTM + i * 16 + lq * 4 + r;
       if (m >= a.M) continue;
-      if constexpr (EPI == KEPI_SPLIT) {
-        float* dst = a.partial + (((long)par * a.nsplit + split) * a.M + m) * a.NT;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) dst[n0 + wn * WTN + j * 16 + lr] = acc[i][j][r];
-      } else if constexpr (EPI == KEPI_STD) {
+      if constexpr (EPI == KEPI_STD) {
         const long op = out_pixel(a, m, py, px);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -810,7 +896,7 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
       const bool ok = p.nsplit > 1 ? launch_glds<TI, KEPI_SPLIT>(a, p, s)
                                    : (d.epi == EPI_AAD ? launch_glds<TI, KEPI_AAD>(a, p, s) : launch_glds<TI, KEPI_STD>(a, p, s));
       if (ok) {
-        if (p.nsplit > 1) {
+        if (p.nsplit > 1 && !a.sem) {
           const int ncols = d.epi == EPI_AAD ? d.C_aad : d.N;
           const long total = (long)p.M * ncols;
           dim3 grid((unsigned)((total + 255) / 256), 1, p.npar);
@@ -825,7 +911,7 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
   }
   if (p.partial) {
     rc = p.fast ? dispatch_tile<TI, TO, KEPI_SPLIT, true>(a, p, s) : dispatch_tile<TI, TO, KEPI_SPLIT, false>(a, p, s);
-    if (rc) return rc;
+    if (rc || a.sem) return rc;
     const int ncols = d.epi == EPI_AAD ? d.C_aad : d.N;
     const long total = (long)p.M * ncols;
     dim3 grid((unsigned)((total + 255) / 256), 1, p.npar);
@@ -885,6 +971,28 @@ int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream
     partial = reinterpret_cast<float*>(ws);
   }
   ConvArgs a = make_args(d, p, partial);
+  // split-K fix-up in the GEMM (split_fixup) when the caller gave counters and a tile's partials are small enough
+  // for one workgroup to sum them (the last one to finish does it while the rest of the grid has drained):
+  // B = 1 and the generator's 2x2..8x8 stages; the large splits keep splitk_reduce_kernel over the whole chip
+  // (bf16 operands with an fp32 output keep it too: their reduction writes another type than the GEMM's)
+  // (the last arriver reads ~1 us per 16 KB of partials, cdna_hip_programming.md §6 item 2: a few tens of KB per
+  // tile; they are staged in the kernel's LDS, so never more than that holds)
+  static const int fuse_knob = GHOST_KNOB("GHOST_SPLIT_FUSE", 1);
+  static const long fuse_max = (long)GHOST_KNOB("GHOST_SPLIT_FUSE_KB", 32) << 10;
+  if (p.partial && p.nsplit > 1 && d.sem && fuse_knob && !(is16(d.ti) && d.to == GHOST_F32) &&
+      (long)p.nMt * p.nNt * p.npar <= d.nsem) {
+    const long tile_bytes = (long)p.nsplit * (p.M < p.BM ? p.M : p.BM) * p.BN * 4;
+    // LDS of the kernel that runs it: the smaller of conv_glds_kernel's ring and conv_igemm_kernel's two buffers
+    const int vec = is16(d.ti) ? 8 : 4, esz = is16(d.ti) ? 2 : 4;
+    static const int stages_knob = GHOST_KNOB("GHOST_CONV_STAGES", 3);
+    const long ring = (long)(p.stages > 0 ? p.stages : stages_knob) * (p.BM + p.BN) * 64;
+    const long bufs = 2L * (p.BM + p.BN) * (p.BK + vec) * esz;
+    const long lds = ring < bufs ? ring : bufs;
+    if (tile_bytes <= lds && (fuse_knob == 2 || tile_bytes <= fuse_max)) {
+      a.sem = d.sem;
+      a.fuse = d.epi == EPI_AAD ? 2 : 1;
+    }
+  }
   int rc;
   if (d.ti == GHOST_F32 && d.to == GHOST_F32) rc = dispatch_types<float, float>(d, a, p, stream);
   else if (d.ti == GHOST_BF16 && d.to == GHOST_BF16) rc = dispatch_types<bf16, bf16>(d, a, p, stream);

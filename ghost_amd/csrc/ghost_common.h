@@ -34,6 +34,30 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 enum GhostDType { GHOST_F32 = 0, GHOST_BF16 = 1, GHOST_F16 = 2, GHOST_U8 = 3 };
 
+// Last-arriver reductions (split-K fix-up, InstanceNorm final pass): the partials one workgroup hands to another
+// cross XCDs, whose L2s are not coherent with each other.  They are stored and re-read with device-scope
+// accesses (written through / re-fetched at the L2, per access) instead of agent-scope release / acquire fences,
+// which write back / invalidate the whole L2 of the issuing XCD: measured on the swap, a fence per workgroup made
+// the fused GEMMs 2-6x slower than the GEMM + reduction kernel pair they replace.
+GHOST_DEV void st_dev(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+GHOST_DEV float ld_dev(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// this workgroup's arrival at *cnt after its st_dev stores (every thread calls it; 1-D workgroups): true in the
+// last of n arrivals, which also resets the counter for the next launch on the stream
+GHOST_DEV bool last_arrival(unsigned* cnt, unsigned n) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's device-scope stores acknowledged
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == n - 1;
+    if (old == n - 1) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
 GHOST_DEV float to_f(float v) { return v; }
 GHOST_DEV float to_f(bf16 v) { return (float)v; }
 GHOST_DEV float to_f(_Float16 v) { return (float)v; }

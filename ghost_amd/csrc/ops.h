@@ -10,14 +10,16 @@ namespace ghost {
 // 1/sqrt(biased var + eps) over H*W, from shifted partial sums (no Sigma x^2 - n mu^2
 // cancellation) merged in fp64.  stat = [B][C][2].
 size_t in_stats_workspace_bytes(int B, int HW, int C);
+// sem (optional, nsem >= B words, zero on entry and left zero): the partial kernel's last workgroup per sample
+// merges that sample's partials (one launch instead of two; same sums in the same order)
 int in_stats(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, void* ws, size_t ws_bytes,
-             hipStream_t s);
+             hipStream_t s, unsigned* sem = nullptr, int nsem = 0);
 // the same statistics of upsample2x(x) ([B, 2H, 2W, C], values rounded to dt) without materialising
 // it: x is the [B, H, W, C] source; workspace = in_stats_workspace_bytes(B, 4HW, C)
 // true when in_stats_up2x takes the closed form over the source (cheaper than reading the upsample)
 bool in_stats_up2x_closed_form(int dt, int H, int W, int C, int ldx);
 int in_stats_up2x(int dt, const void* x, int ldx, int B, int H, int W, int C, float* stat, void* ws, size_t ws_bytes,
-                  hipStream_t s);
+                  hipStream_t s, unsigned* sem = nullptr, int nsem = 0);
 
 // statistics from the per-(tile, wave) partials a producer kernel wrote (ConvDesc::in_part): nrec
 // records of (mean, centred sum of squares) over 64 pixels per (sample, channel), merged in fp64 (Chan)

@@ -17,12 +17,54 @@ static constexpr float kInEps = 1e-5f;   // nn.InstanceNorm2d default (AADLayer.
 // grid (nchunk, ceil(C/64), B); a block reduces `chunk` pixels x 64 channels.
 // Shift K_c = x[b, pixel 0, c] makes the partial sums robust to |mean| >> std.
 // ---------------------------------------------------------------------------
+// mean / rstd of (sample b, channel c) from the fp64 sums of its chunks' shifted partials (K = pixel 0 of the
+// sample, also of a virtual upsample)
+GHOST_DEV void in_stats_store(float* __restrict__ stat, long i, double K, double S1, double S2, int HW) {
+  const double n = (double)HW;
+  const double md = S1 / n;
+  double var = S2 / n - md * md;
+  if (var < 0.0) var = 0.0;
+  stat[i * 2 + 0] = (float)(K + md);
+  stat[i * 2 + 1] = (float)(1.0 / sqrt(var + (double)kInEps));
+}
+
+// Fused final pass (sem != nullptr): the partial workgroups store with st_dev, and the last of sample b's
+// `arrivals` to finish merges the sample's partials — the sums of in_stats_final_kernel in its order, one launch per
+// statistics pass instead of two.  Each thread's chunk partials are loaded as one batch of independent device-scope
+// loads before any is summed (a dependent load per chunk is a fabric round trip each).
+template <typename T>
+GHOST_DEV void in_stats_fixup(const T* __restrict__ x, int ldx, long bstride, int HW, int C, int nchunk,
+                              const float* part, float* stat, unsigned* sem, int b, unsigned arrivals) {
+  if (!last_arrival(sem + b, arrivals)) return;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const double K = (double)to_f(x[(long)b * bstride * ldx + c]);
+    const float* o = part + ((long)b * nchunk * C + c) * 2;   // chunk k: o + 2 k C
+    double S1 = 0.0, S2 = 0.0;
+    for (int k0 = 0; k0 < nchunk; k0 += 16) {
+      float v1[16], v2[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const long k = min(k0 + j, nchunk - 1);   // clamped, not skipped: the whole batch in flight at once
+        v1[j] = ld_dev(o + k * C * 2);
+        v2[j] = ld_dev(o + k * C * 2 + 1);
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (k0 + j < nchunk) {
+          S1 += (double)v1[j];
+          S2 += (double)v2[j];
+        }
+    }
+    in_stats_store(stat, (long)b * C + c, K, S1, S2, HW);
+  }
+}
+
 // UP: x is the source of a virtual bilinear x2 upsample (u); the statistics are those of the
 // upsampled tensor as upsample2x would store it (values rounded to T), HW = 4 * u.H * u.W.
 template <typename T, bool UP>
 __global__ void __launch_bounds__(256)
 in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chunk, int nchunk, float* __restrict__ part,
-                        const Up2xSrc u) {
+                        const Up2xSrc u, float* stat, unsigned* sem) {
   constexpr int VEC = Vec16<T>::N;
   constexpr int TPP = 64 / VEC;   // threads per pixel (64 channels)
   constexpr int PPP = 256 / TPP;  // pixels per pass
@@ -69,10 +111,17 @@ in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chu
     for (int i = 0; i < PPP; ++i) { a += red[0][i][t]; q += red[1][i][t]; }
     if (c < C) {
       float* o = part + (((long)b * nchunk + ch) * C + c) * 2;
-      o[0] = a;
-      o[1] = q;
+      if (sem) {
+        st_dev(o, a);
+        st_dev(o + 1, q);
+      } else {
+        o[0] = a;
+        o[1] = q;
+      }
     }
   }
+  if (sem)
+    in_stats_fixup(x, ldx, UP ? (long)u.H * u.W : (long)HW, HW, C, nchunk, part, stat, sem, b, gridDim.x * gridDim.y);
 }
 
 // Statistics of upsample2x(x) without visiting the upsampled pixels.  The x2 bilinear upsample is
@@ -118,7 +167,7 @@ GHOST_DEV void up2x_tap_weights(float sc, int n, int s, float& wo, float& g0o, f
 template <typename T>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
 in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, float* __restrict__ part,
-                        const Up2xSrc u) {
+                        const Up2xSrc u, float* stat, unsigned* sem) {
   __shared__ float red[2][32][65];
   __shared__ float swx[3][128], swy[3][32];   // this workgroup's column / row tap-weight tables
   const int b = blockIdx.z, cg = blockIdx.y, ch = blockIdx.x;
@@ -195,10 +244,17 @@ in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, flo
     }
     if (c < C) {
       float* o = part + (((long)b * nchunk + ch) * C + c) * 2;
-      o[0] = a;
-      o[1] = s2;
+      if (sem) {
+        st_dev(o, a);
+        st_dev(o + 1, s2);
+      } else {
+        o[0] = a;
+        o[1] = s2;
+      }
     }
   }
+  if (sem)
+    in_stats_fixup(x, ldx, (long)u.H * u.W, 4 * u.H * u.W, C, nchunk, part, stat, sem, b, gridDim.x * gridDim.y);
 }
 
 template <typename T>
@@ -215,12 +271,7 @@ in_stats_final_kernel(const T* __restrict__ x, int ldx, long bstride, int B, int
     S1 += (double)o[0];
     S2 += (double)o[1];
   }
-  const double n = (double)HW;
-  const double md = S1 / n;
-  double var = S2 / n - md * md;
-  if (var < 0.0) var = 0.0;
-  stat[(long)i * 2 + 0] = (float)(K + md);
-  stat[(long)i * 2 + 1] = (float)(1.0 / sqrt(var + (double)kInEps));
+  in_stats_store(stat, i, K, S1, S2, HW);
 }
 
 // records [B][nrec][C][2] = (mean, centred sum of squares) over 64 pixels each.  Grid (C/16, B),
@@ -303,7 +354,7 @@ bool in_stats_up2x_closed_form(int dt, int H, int W, int C, int ldx) {
 
 template <typename T>
 static void in_stats_launch(const T* x, int ldx, int B, int HW, int C, float* stat, float* part, const Up2xSrc* up,
-                            hipStream_t s) {
+                            hipStream_t s, unsigned* sem) {
   int chunk, nchunk;
   stats_geometry(B, HW, C, chunk, nchunk);
   dim3 g1(nchunk, (C + 63) / 64, B);
@@ -313,45 +364,52 @@ static void in_stats_launch(const T* x, int ldx, int B, int HW, int C, float* st
     if (up && in_stats_up2x_closed_form(gdt<T>(), u.H, u.W, C, ldx)) {
       // closed form over the source: (H / 4) * (W / 128) records <= the HW / 512 reserved
       const int nr = u.H * u.W / 512;   // workgroups of 512 source pixels
-      hipLaunchKernelGGL(in_stats_up_quad_kernel<T>, dim3(nr, C / 64, B), dim3(256), 0, s, x, ldx, C, nr, part, u);
-      hipLaunchKernelGGL(in_stats_final_kernel<T>, g2, dim3(256), 0, s, x, ldx, (long)u.H * u.W, B, HW, C, nr, part,
-                         stat);
+      hipLaunchKernelGGL(in_stats_up_quad_kernel<T>, dim3(nr, C / 64, B), dim3(256), 0, s, x, ldx, C, nr, part, u, stat,
+                         sem);
+      if (!sem)
+        hipLaunchKernelGGL(in_stats_final_kernel<T>, g2, dim3(256), 0, s, x, ldx, (long)u.H * u.W, B, HW, C, nr, part,
+                           stat);
       return;
     }
   }
   if (up)
-    hipLaunchKernelGGL((in_stats_partial_kernel<T, true>), g1, dim3(256), 0, s, x, ldx, HW, C, chunk, nchunk, part, u);
+    hipLaunchKernelGGL((in_stats_partial_kernel<T, true>), g1, dim3(256), 0, s, x, ldx, HW, C, chunk, nchunk, part, u,
+                       stat, sem);
   else
-    hipLaunchKernelGGL((in_stats_partial_kernel<T, false>), g1, dim3(256), 0, s, x, ldx, HW, C, chunk, nchunk, part, u);
+    hipLaunchKernelGGL((in_stats_partial_kernel<T, false>), g1, dim3(256), 0, s, x, ldx, HW, C, chunk, nchunk, part, u,
+                       stat, sem);
+  if (sem) return;
   const long bstride = up ? (long)u.H * u.W : HW;
   hipLaunchKernelGGL(in_stats_final_kernel<T>, g2, dim3(256), 0, s, x, ldx, bstride, B, HW, C, nchunk, part, stat);
 }
 
 static int in_stats_any(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, void* ws, size_t ws_bytes,
-                        const Up2xSrc* up, hipStream_t s) {
+                        const Up2xSrc* up, hipStream_t s, unsigned* sem, int nsem) {
   if (C % 16 || ldx % 8 || (uintptr_t)x % 16) return -1;
   if (!ws || ws_bytes < in_stats_workspace_bytes(B, HW, C)) return -1;
   float* part = reinterpret_cast<float*>(ws);
+  static const int fuse_knob = GHOST_KNOB("GHOST_STATS_FUSE", 1);
+  if (!fuse_knob || B > nsem) sem = nullptr;   // one counter per sample
   if (dt == GHOST_F32)
-    in_stats_launch((const float*)x, ldx, B, HW, C, stat, part, up, s);
+    in_stats_launch((const float*)x, ldx, B, HW, C, stat, part, up, s, sem);
   else if (dt == GHOST_BF16)
-    in_stats_launch((const bf16*)x, ldx, B, HW, C, stat, part, up, s);
+    in_stats_launch((const bf16*)x, ldx, B, HW, C, stat, part, up, s, sem);
   else if (dt == GHOST_F16)
-    in_stats_launch((const _Float16*)x, ldx, B, HW, C, stat, part, up, s);
+    in_stats_launch((const _Float16*)x, ldx, B, HW, C, stat, part, up, s, sem);
   else
     return -1;
   return (int)hipGetLastError();
 }
 
 int in_stats(int dt, const void* x, int ldx, int B, int HW, int C, float* stat, void* ws, size_t ws_bytes,
-             hipStream_t s) {
-  return in_stats_any(dt, x, ldx, B, HW, C, stat, ws, ws_bytes, nullptr, s);
+             hipStream_t s, unsigned* sem, int nsem) {
+  return in_stats_any(dt, x, ldx, B, HW, C, stat, ws, ws_bytes, nullptr, s, sem, nsem);
 }
 
 int in_stats_up2x(int dt, const void* x, int ldx, int B, int H, int W, int C, float* stat, void* ws, size_t ws_bytes,
-                  hipStream_t s) {
+                  hipStream_t s, unsigned* sem, int nsem) {
   const Up2xSrc u = up2x_src(H, W);
-  return in_stats_any(dt, x, ldx, B, 4 * H * W, C, stat, ws, ws_bytes, &u, s);
+  return in_stats_any(dt, x, ldx, B, 4 * H * W, C, stat, ws, ws_bytes, &u, s, sem, nsem);
 }
 
 // ---------------------------------------------------------------------------

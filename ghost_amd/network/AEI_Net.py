@@ -130,7 +130,7 @@ class AADGenerator(nn.Module):
 
 
 # per-handle plan options (include/ghost_amd.h GHOST_AEI_OPT_*)
-OPTIONS = {"fuse_upsample": 0, "fuse_stats": 1, "two_streams": 2, "tap_partials": 3}
+OPTIONS = {"fuse_upsample": 0, "fuse_stats": 1, "two_streams": 2, "tap_partials": 3, "fuse_reduce": 4}
 
 
 class _Runtime:

@@ -117,6 +117,11 @@ int ghost_aei_swap_u8_indexed(ghost_aei* h, const uint8_t* crops, int64_t crop_b
  *                                    written and the narrow conv contracts it); 0: neither.  The partials
  *                                    are rounded to fp16 once (the extra rounding the bf16-storage
  *                                    emulation of oracle/aei_ref.py models).
+ *   GHOST_AEI_OPT_FUSE_REDUCE (1):   split-K GEMMs with small partial tiles and the InstanceNorm statistics
+ *                                    passes reduce their partials in the last workgroup to finish (arrival
+ *                                    counters in the workspace, zeroed once per call) instead of a second
+ *                                    kernel: the same sums in the same order, the same bytes, fewer launches
+ *                                    (0: the separate reduction kernels).
  * value is 0 or 1 (TAP_PARTIALS: 0..2).  A handle is not shared across threads without external
  * synchronisation. */
 enum {
@@ -124,7 +129,8 @@ enum {
   GHOST_AEI_OPT_FUSE_STATS = 1,
   GHOST_AEI_OPT_TWO_STREAMS = 2,
   GHOST_AEI_OPT_TAP_PARTIALS = 3,
-  GHOST_AEI_NOPT = 4
+  GHOST_AEI_OPT_FUSE_REDUCE = 4,
+  GHOST_AEI_NOPT = 5
 };
 int ghost_aei_set_option(ghost_aei* h, int option, int value);
 int ghost_aei_get_option(ghost_aei* h, int option, int* value);

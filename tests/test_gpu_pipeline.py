@@ -175,6 +175,33 @@ def test_two_stream_plan_is_bit_identical(lib, backbone, nb, B):
     assert torch.equal(res[0][2], res[1][2])
 
 
+@pytest.mark.parametrize("backbone,nb,dt,B", [("unet", 2, torch.bfloat16, 1), ("unet", 2, torch.bfloat16, 64),
+                                              ("linknet", 3, torch.float16, 8), ("unet", 2, None, 2),
+                                              ("unet", 1, torch.bfloat16, 3)])
+def test_fused_reductions_are_bit_identical(lib, backbone, nb, dt, B):
+    """GHOST_AEI_OPT_FUSE_REDUCE: split-K GEMMs summing their partials in the last workgroup of each tile, and
+    the InstanceNorm partial kernels merging per sample in their last workgroup, give the bytes of the separate
+    reduction kernels (forward outputs, attrs, the uint8 swap), call after call (the arrival counters are
+    reused by every launch of a stream and must be left at zero)."""
+    G, _ = model(backbone, nb, dt)
+    xt, z = aei_ref.make_inputs(B, 31)
+    crops = torch.from_numpy(aei_ref.make_u8_crops(B, 31)).to(DEV)
+    res = {}
+    for mode in (0, 1, 1):
+        G.set_option("fuse_reduce", mode)
+        Y, attr = G(xt.to(DEV), z.to(DEV))
+        u8 = G.swap_u8(crops, z.to(DEV))
+        torch.cuda.synchronize()
+        got = (Y.clone(), [a.clone() for a in attr], u8.clone())
+        if mode in res:
+            assert torch.equal(res[mode][0], got[0]) and torch.equal(res[mode][2], got[2])
+        res[mode] = got
+    assert G.get_option("fuse_reduce") == 1
+    assert torch.equal(res[0][0], res[1][0])
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+    assert torch.equal(res[0][2], res[1][2])
+
+
 def test_gather_pipeline_two_batches_in_flight(lib):
     """dp.GatherPipeline(streams=2) (bench.py's default): consecutive batches swapped on two pipeline streams
     at once (sharing one AEI_Net handle) give the bytes of one-at-a-time swaps, batch by batch, including a

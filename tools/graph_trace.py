@@ -89,8 +89,13 @@ def analyze(db):
         if k in per[1]:
             a, b = sum(per[0][k]) / len(per[0][k]), sum(per[1][k]) / len(per[1][k])
             diffs.append((b - a, a, b, len(per[0][k]), k))
-    for dd, a, b, n, k in sorted(diffs, reverse=True)[:15]:
-        print(f"  +{dd:8.1f} us  eager {a:8.1f} graphed {b:8.1f}  x{n}  {k}")
+    diffs.sort(reverse=True)
+    for row in (diffs[:15] + [None] + diffs[-15:] if len(diffs) > 30 else diffs):
+        if row is None:
+            print("  ...")
+            continue
+        dd, a, b, n, k = row
+        print(f"  {dd:+8.1f} us  eager {a:8.1f} graphed {b:8.1f}  x{n}  {k}")
     # gaps between consecutive kernels inside a call
     for name, ph in zip(("eager", "graphed"), phases):
         gaps = [(ph[i + 1][0] - ph[i][1]) / 1e3 for i in range(len(ph) - 1) if ph[i + 1][0] - ph[i][1] < 200e3]
