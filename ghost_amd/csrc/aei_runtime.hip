@@ -930,7 +930,8 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
   void* xin = c.alloc((size_t)B * 256 * 256 * 4 * es);
   if (!c.dry && c.ok()) {
     if (mode == M_SWAP)
-      c.check(crops_u8_to_input(io.crops, io.crop_bs, B, 256, 256, h->dt, xin, c.s, 4), "crops_u8_to_input");
+      c.check(crops_u8_to_input(io.crops, io.crop_bs, B, 256, 256, h->dt, xin, c.s, 4, c.sem_main,
+                                c.sem_main ? 2 * kSemWords : 0), "crops_u8_to_input");
     else
       c.check(input_to_nhwc(io.xt_dtype, io.xt, io.st, B, 3, 256, 256, h->dt, xin, c.s, 4), "input_to_nhwc");
   }
@@ -1099,10 +1100,13 @@ int run(ghost_aei* h, Mode mode, int B, const Io& io, void* ws, int64_t ws_bytes
   if (h->opt[GHOST_AEI_OPT_FUSE_REDUCE]) {
     // the counters start at zero (the workspace is the caller's memory); queued before every launch of the call,
     // which the up-path stream's launches follow through its events
+    // (a kernel, not hipMemsetAsync: a captured memset node left GraphedSwap's B = 8 one-chain replay with wrong
+    // bytes; a swap's crops conversion zeroes them in its own launch, see plan)
     unsigned* sem = (unsigned*)(c.base + main_bytes);
-    if (hipMemsetAsync(sem, 0, kSemBytes, c.s) != hipSuccess) return fail(GHOST_EINVAL, "counter reset failed");
     c.sem_main = sem;
     c.sem_up = sem + kSemWords;
+    if (mode != M_SWAP)
+      if (int rc = zero_words(sem, 2 * kSemWords, c.s)) return fail(rc, "counter reset failed");
   }
   if (dry.dual && ensure_up_stream(h, c.dev)) {
     c.s_up = h->up_path[c.dev].s;

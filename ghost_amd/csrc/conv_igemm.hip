@@ -978,7 +978,7 @@ int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream
   // (the last arriver reads ~1 us per 16 KB of partials, cdna_hip_programming.md §6 item 2: a few tens of KB per
   // tile; they are staged in the kernel's LDS, so never more than that holds)
   static const int fuse_knob = GHOST_KNOB("GHOST_SPLIT_FUSE", 1);
-  static const long fuse_max = (long)GHOST_KNOB("GHOST_SPLIT_FUSE_KB", 32) << 10;
+  static const long fuse_max = (long)GHOST_KNOB("GHOST_SPLIT_FUSE_KB", 128) << 10;
   if (p.partial && p.nsplit > 1 && d.sem && fuse_knob && !(is16(d.ti) && d.to == GHOST_F32) &&
       (long)p.nMt * p.nNt * p.npar <= d.nsem) {
     const long tile_bytes = (long)p.nsplit * (p.M < p.BM ? p.M : p.BM) * p.BN * 4;

@@ -49,8 +49,9 @@ int input_to_nhwc(int xdt, const void* x, const int64_t strides[4], int B, int C
 
 // uint8 BGR NHWC crops -> RGB NHWC in [-1,1]: (v/255 - 0.5)/0.5  (core.py:13-26)
 // ldy = 3, or 4 with a zero fourth channel
+// zero (optional): nzero words (a multiple of 4, 16-byte aligned) set to 0 by the same launch (zero_words' job)
 int crops_u8_to_input(const uint8_t* crops, int64_t batch_stride, int B, int H, int W, int dt, void* y,
-                      hipStream_t s, int ldy);
+                      hipStream_t s, int ldy, unsigned* zero = nullptr, int nzero = 0);
 
 // Y NHWC (3 channels, ld) -> uint8 BGR NHWC: ((Y*0.5+0.5)*255)[..., [2,1,0]].uint8  (faceshifter_run.py:20-21)
 int y_to_u8_bgr(int dt, const void* y, int ldy, int B, int H, int W, uint8_t* out, hipStream_t s);
@@ -63,6 +64,10 @@ int rows_to_f32(int xdt, const void* x, int64_t row_stride, int B, int n, float*
 // outside [0, n_rows) is clamped (memory-safe; the host wrapper validates indices)
 int gather_identity_rows(int nseg, const void* const* tab, const int64_t* row_bytes, void* const* out, int n_rows,
                          const int32_t* idx, int B, hipStream_t s);
+
+// p[0 .. nwords) = 0 (a kernel, not a memset: the arrival counters of the fused reductions, zeroed at the start of
+// every call, also inside a captured graph; nwords % 4 == 0, 16-byte aligned)
+int zero_words(unsigned* p, int nwords, hipStream_t s);
 
 // NHWC (ld) -> NCHW contiguous copy in the same dtype (attr export / tests)
 int nhwc_to_nchw(int dt, const void* x, int ldx, int B, int H, int W, int C, void* y, hipStream_t s);

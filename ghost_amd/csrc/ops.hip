@@ -857,8 +857,10 @@ int input_to_nhwc(int xdt, const void* x, const int64_t strides[4], int B, int C
 // encoder's first conv reads as aligned rows, conv_first.hip)
 template <typename T>
 __global__ void __launch_bounds__(256)
-crops_kernel(const uint8_t* __restrict__ crops, long bstride, int B, int H, int W, T* __restrict__ y, int ldy) {
+crops_kernel(const uint8_t* __restrict__ crops, long bstride, int B, int H, int W, T* __restrict__ y, int ldy,
+             u32x4* __restrict__ zero, int nzero16) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;   // one output pixel
+  if (idx < nzero16) zero[idx] = u32x4{0u, 0u, 0u, 0u};     // the call's reduction counters (zero_words' job)
   const long HW = (long)H * W;
   if (idx >= (long)B * HW) return;
   const int b = (int)(idx / HW);
@@ -874,17 +876,22 @@ crops_kernel(const uint8_t* __restrict__ crops, long bstride, int B, int H, int 
 }
 
 int crops_u8_to_input(const uint8_t* crops, int64_t batch_stride, int B, int H, int W, int dt, void* y, hipStream_t s,
-                      int ldy) {
+                      int ldy, unsigned* zero, int nzero) {
   if (ldy != 3 && ldy != 4) return -1;
+  if (zero && (nzero % 4 || (uintptr_t)zero % 16)) return -1;
   const long total = (long)B * H * W;
-  dim3 grid((unsigned)((total + 255) / 256));
+  const int nz16 = zero ? nzero / 4 : 0;
+  dim3 grid((unsigned)((std::max<long>(total, nz16) + 255) / 256));
+  u32x4* z = reinterpret_cast<u32x4*>(zero);
   if (dt == GHOST_F32)
-    hipLaunchKernelGGL(crops_kernel<float>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (float*)y, ldy);
+    hipLaunchKernelGGL(crops_kernel<float>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (float*)y, ldy,
+                       z, nz16);
   else if (dt == GHOST_BF16)
-    hipLaunchKernelGGL(crops_kernel<bf16>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (bf16*)y, ldy);
+    hipLaunchKernelGGL(crops_kernel<bf16>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W, (bf16*)y, ldy,
+                       z, nz16);
   else if (dt == GHOST_F16)   // transform_target_to_torch(half=True) of the reference: float16
     hipLaunchKernelGGL(crops_kernel<_Float16>, grid, dim3(256), 0, s, crops, (long)batch_stride, B, H, W,
-                       (_Float16*)y, ldy);
+                       (_Float16*)y, ldy, z, nz16);
   else
     return -1;
   return (int)hipGetLastError();
@@ -952,6 +959,18 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(GatherSegs g, int n_ro
   const uint4* __restrict__ src = g.tab[sg] + (long)r * n;
   uint4* __restrict__ dst = g.out[sg] + (long)b * n;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(256) zero_words_kernel(u32x4* __restrict__ p, int n16) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n16) p[i] = u32x4{0u, 0u, 0u, 0u};
+}
+
+int zero_words(unsigned* p, int nwords, hipStream_t s) {
+  if (!p || nwords <= 0 || nwords % 4 || (uintptr_t)p % 16) return -1;
+  const int n16 = nwords / 4;
+  hipLaunchKernelGGL(zero_words_kernel, dim3((n16 + 255) / 256), dim3(256), 0, s, reinterpret_cast<u32x4*>(p), n16);
+  return (int)hipGetLastError();
 }
 
 int gather_identity_rows(int nseg, const void* const* tab, const int64_t* row_bytes, void* const* out, int n_rows,

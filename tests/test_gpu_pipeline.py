@@ -175,15 +175,16 @@ def test_two_stream_plan_is_bit_identical(lib, backbone, nb, B):
     assert torch.equal(res[0][2], res[1][2])
 
 
-@pytest.mark.parametrize("backbone,nb,dt,B", [("unet", 2, torch.bfloat16, 1), ("unet", 2, torch.bfloat16, 64),
-                                              ("linknet", 3, torch.float16, 8), ("unet", 2, None, 2),
-                                              ("unet", 1, torch.bfloat16, 3)])
-def test_fused_reductions_are_bit_identical(lib, backbone, nb, dt, B):
+@pytest.mark.parametrize("backbone,nb,dt,B,ts", [("unet", 2, torch.bfloat16, 1, 1), ("unet", 2, torch.bfloat16, 64, 1),
+                                                 ("linknet", 3, torch.float16, 8, 1), ("unet", 2, None, 2, 1),
+                                                 ("unet", 1, torch.bfloat16, 3, 1), ("unet", 2, torch.bfloat16, 8, 0)])
+def test_fused_reductions_are_bit_identical(lib, backbone, nb, dt, B, ts):
     """GHOST_AEI_OPT_FUSE_REDUCE: split-K GEMMs summing their partials in the last workgroup of each tile, and
     the InstanceNorm partial kernels merging per sample in their last workgroup, give the bytes of the separate
     reduction kernels (forward outputs, attrs, the uint8 swap), call after call (the arrival counters are
     reused by every launch of a stream and must be left at zero)."""
     G, _ = model(backbone, nb, dt)
+    G.set_option("two_streams", ts)
     xt, z = aei_ref.make_inputs(B, 31)
     crops = torch.from_numpy(aei_ref.make_u8_crops(B, 31)).to(DEV)
     res = {}
