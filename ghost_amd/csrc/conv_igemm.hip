@@ -976,18 +976,22 @@ int conv_launch(const ConvDesc& d, void* ws, size_t ws_bytes, hipStream_t stream
   // B = 1 and the generator's 2x2..8x8 stages; the large splits keep splitk_reduce_kernel over the whole chip
   // (bf16 operands with an fp32 output keep it too: their reduction writes another type than the GEMM's)
   // (the last arriver reads ~1 us per 16 KB of partials, cdna_hip_programming.md §6 item 2: a few tens of KB per
-  // tile; they are staged in the kernel's LDS, so never more than that holds)
+  // tile; they are staged in the kernel's LDS, so never more than that holds.  Measured at B = 1 bf16: 32-40 KB
+  // 1.10-1.11 ms as without the fix-up, 128 KB — the deep ring's 4x4 / 8x8 GEMMs fused — 1.17-1.19 ms)
   static const int fuse_knob = GHOST_KNOB("GHOST_SPLIT_FUSE", 1);
-  static const long fuse_max = (long)GHOST_KNOB("GHOST_SPLIT_FUSE_KB", 128) << 10;
+  static const long fuse_max = (long)GHOST_KNOB("GHOST_SPLIT_FUSE_KB", 32) << 10;
   if (p.partial && p.nsplit > 1 && d.sem && fuse_knob && !(is16(d.ti) && d.to == GHOST_F32) &&
       (long)p.nMt * p.nNt * p.npar <= d.nsem) {
     const long tile_bytes = (long)p.nsplit * (p.M < p.BM ? p.M : p.BM) * p.BN * 4;
-    // LDS of the kernel that runs it: the smaller of conv_glds_kernel's ring and conv_igemm_kernel's two buffers
+    // LDS of the kernel that runs it: the deep ring (p.stages, always conv_glds_kernel: 16-bit, fast, 128 x 128)
+    // has stages x 16 KB; otherwise the smaller of conv_glds_kernel's 3-stage ring and conv_igemm_kernel's buffers
     const int vec = is16(d.ti) ? 8 : 4, esz = is16(d.ti) ? 2 : 4;
     static const int stages_knob = GHOST_KNOB("GHOST_CONV_STAGES", 3);
     const long ring = (long)(p.stages > 0 ? p.stages : stages_knob) * (p.BM + p.BN) * 64;
     const long bufs = 2L * (p.BM + p.BN) * (p.BK + vec) * esz;
-    const long lds = ring < bufs ? ring : bufs;
+    static const int use_v2 = GHOST_KNOB("GHOST_CONV_V2", 1);
+    const bool deep_glds = use_v2 && (p.stages == 8 || p.stages == 6 || p.stages == 4);   // launch_glds' instances
+    const long lds = deep_glds ? ring : (ring < bufs ? ring : bufs);
     if (tile_bytes <= lds && (fuse_knob == 2 || tile_bytes <= fuse_max)) {
       a.sem = d.sem;
       a.fuse = d.epi == EPI_AAD ? 2 : 1;
