@@ -436,6 +436,56 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a) {
   }
 }
 
+// the same reduction, four channels per thread: 16-byte slab loads (the scalar form read 4 B per lane and ran at
+// 0.4-1 TB/s on the B = 64 AAD / encoder reductions); per element the same ordered sum and the same epilogue
+template <typename TO, int EPI>
+__global__ void __launch_bounds__(256) splitk_reduce4_kernel(const ConvArgs a) {
+  const int par = blockIdx.z;
+  const int py = par >> 1, px = par & 1;
+  const int ncols = (EPI == KEPI_AAD) ? a.C_aad : a.N;
+  const int nq = ncols >> 2;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)a.M * nq) return;
+  const long m = idx / nq;
+  const int c = (int)(idx - m * nq) * 4;
+  const float* base = a.partial + ((long)par * a.nsplit * a.M + m) * a.NT;
+  const long sstride = (long)a.M * a.NT;
+  if constexpr (EPI == KEPI_STD) {
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int s = 0; s < a.nsplit; ++s) v += *reinterpret_cast<const f32x4*>(base + s * sstride + c);
+    const long op = out_pixel(a, m, py, px);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) store_std<TO>(a, epi_std<TO>(a, v[e], c + e, op), c + e, op);
+  } else {
+    const int ng = (c >> 4) * 32 + (c & 15);   // four consecutive channels: four consecutive gamma columns
+    f32x4 ga = f32x4{0.f, 0.f, 0.f, 0.f}, ba = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int s = 0; s < a.nsplit; ++s) {
+      ga += *reinterpret_cast<const f32x4*>(base + s * sstride + ng);
+      ba += *reinterpret_cast<const f32x4*>(base + s * sstride + ng + 16);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      reinterpret_cast<TO*>(a.y)[m * a.ldy + c + e] =
+          from_f<TO>(epi_aad<TO>(a, ga[e] + a.shift[ng + e], ba[e] + a.shift[ng + 16 + e], c + e, m));
+  }
+}
+
+// one reduction launch for a split-K GEMM's partials: the four-channel form when the columns allow it
+template <typename TO, int EPI>
+void launch_reduce(const ConvArgs& a, int ncols, int npar, hipStream_t s) {
+  static const int vec = GHOST_KNOB("GHOST_SPLITK_VEC", 1);
+  const long total = (long)a.M * ncols;
+  if (vec && ncols % 4 == 0 && a.NT % 4 == 0) {
+    dim3 grid((unsigned)((total / 4 + 255) / 256), 1, npar);
+    hipLaunchKernelGGL((splitk_reduce4_kernel<TO, EPI>), grid, dim3(256), 0, s, a);
+  } else {
+    dim3 grid((unsigned)((total + 255) / 256), 1, npar);
+    hipLaunchKernelGGL((splitk_reduce_kernel<TO, EPI>), grid, dim3(256), 0, s, a);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // v2: bf16 implicit GEMM staged by LDS-DMA (global_load_lds_dwordx4) through a STAGES-deep
 // ring with counted vmcnt waits and raw barriers (cdna_hip_programming.md §5 "Pipelining
@@ -897,13 +947,8 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
                                    : (d.epi == EPI_AAD ? launch_glds<TI, KEPI_AAD>(a, p, s) : launch_glds<TI, KEPI_STD>(a, p, s));
       if (ok) {
         if (p.nsplit > 1 && !a.sem) {
-          const int ncols = d.epi == EPI_AAD ? d.C_aad : d.N;
-          const long total = (long)p.M * ncols;
-          dim3 grid((unsigned)((total + 255) / 256), 1, p.npar);
-          if (d.epi == EPI_AAD)
-            hipLaunchKernelGGL((splitk_reduce_kernel<TO, KEPI_AAD>), grid, dim3(256), 0, s, a);
-          else
-            hipLaunchKernelGGL((splitk_reduce_kernel<TO, KEPI_STD>), grid, dim3(256), 0, s, a);
+          if (d.epi == EPI_AAD) launch_reduce<TO, KEPI_AAD>(a, d.C_aad, p.npar, s);
+          else launch_reduce<TO, KEPI_STD>(a, d.N, p.npar, s);
         }
         return 0;
       }
@@ -912,13 +957,8 @@ int dispatch_types(const ConvDesc& d, const ConvArgs& a, const Plan& p, hipStrea
   if (p.partial) {
     rc = p.fast ? dispatch_tile<TI, TO, KEPI_SPLIT, true>(a, p, s) : dispatch_tile<TI, TO, KEPI_SPLIT, false>(a, p, s);
     if (rc || a.sem) return rc;
-    const int ncols = d.epi == EPI_AAD ? d.C_aad : d.N;
-    const long total = (long)p.M * ncols;
-    dim3 grid((unsigned)((total + 255) / 256), 1, p.npar);
-    if (d.epi == EPI_AAD)
-      hipLaunchKernelGGL((splitk_reduce_kernel<TO, KEPI_AAD>), grid, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((splitk_reduce_kernel<TO, KEPI_STD>), grid, dim3(256), 0, s, a);
+    if (d.epi == EPI_AAD) launch_reduce<TO, KEPI_AAD>(a, d.C_aad, p.npar, s);
+    else launch_reduce<TO, KEPI_STD>(a, d.N, p.npar, s);
     return 0;
   }
   if (d.epi == EPI_AAD) {
