@@ -118,7 +118,8 @@ GHOST_DEV long out_pixel(const ConvArgs& a, long m, int py, int px) {
 // fabric round trip each, cdna_hip_programming.md §6 item 2), then sums from LDS.
 template <typename TO, int BM, int BN, int NTHR>
 GHOST_DEV void split_fixup(const ConvArgs& a, int tid, int tile_id, int m0, int n0, int par, float* stage) {
-  if (!last_arrival(a.sem + tile_id, (unsigned)a.nsplit)) return;
+  if (!last_arrival(a.sem + tile_id, (unsigned)a.nsplit, reinterpret_cast<int*>(stage))) return;
+  __syncthreads();   // every thread has read the flag (stage[0]) before the staging below overwrites it
   const int py = par >> 1, px = par & 1;
   const int mrows = min(BM, a.M - m0);
   const long sstride = (long)a.M * a.NT;

@@ -44,18 +44,20 @@ GHOST_DEV float ld_dev(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // this workgroup's arrival at *cnt after its st_dev stores (every thread calls it; 1-D workgroups): true in the
-// last of n arrivals, which also resets the counter for the next launch on the stream
-GHOST_DEV bool last_arrival(unsigned* cnt, unsigned n) {
-  __shared__ int s_last;
+// last of n arrivals, which also resets the counter for the next launch on the stream.  `flag` is a word of the
+// kernel's own LDS array, free at this point: a second __shared__ object beside an LDS-DMA ring makes hipcc wait
+// vmcnt(0) before the first LDS read of every K step (cdna_hip_programming.md §6 item 4a; measured here: the split
+// GEMMs' ring drained every step, +1.8 us per B = 1 GEMM).  The caller must not overwrite `flag` before a barrier.
+GHOST_DEV bool last_arrival(unsigned* cnt, unsigned n, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's device-scope stores acknowledged
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == n - 1;
+    *flag = old == n - 1;
     if (old == n - 1) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  return s_last != 0;
+  return *flag != 0;
 }
 
 GHOST_DEV float to_f(float v) { return v; }

@@ -34,8 +34,8 @@ GHOST_DEV void in_stats_store(float* __restrict__ stat, long i, double K, double
 // loads before any is summed (a dependent load per chunk is a fabric round trip each).
 template <typename T>
 GHOST_DEV void in_stats_fixup(const T* __restrict__ x, int ldx, long bstride, int HW, int C, int nchunk,
-                              const float* part, float* stat, unsigned* sem, int b, unsigned arrivals) {
-  if (!last_arrival(sem + b, arrivals)) return;
+                              const float* part, float* stat, unsigned* sem, int b, unsigned arrivals, int* flag) {
+  if (!last_arrival(sem + b, arrivals, flag)) return;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const double K = (double)to_f(x[(long)b * bstride * ldx + c]);
     const float* o = part + ((long)b * nchunk * C + c) * 2;   // chunk k: o + 2 k C
@@ -121,7 +121,8 @@ in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chu
     }
   }
   if (sem)
-    in_stats_fixup(x, ldx, UP ? (long)u.H * u.W : (long)HW, HW, C, nchunk, part, stat, sem, b, gridDim.x * gridDim.y);
+    in_stats_fixup(x, ldx, UP ? (long)u.H * u.W : (long)HW, HW, C, nchunk, part, stat, sem, b, gridDim.x * gridDim.y,
+                   reinterpret_cast<int*>(&red[0][0][0]));
 }
 
 // Statistics of upsample2x(x) without visiting the upsampled pixels.  The x2 bilinear upsample is
@@ -254,7 +255,8 @@ in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, flo
     }
   }
   if (sem)
-    in_stats_fixup(x, ldx, (long)u.H * u.W, 4 * u.H * u.W, C, nchunk, part, stat, sem, b, gridDim.x * gridDim.y);
+    in_stats_fixup(x, ldx, (long)u.H * u.W, 4 * u.H * u.W, C, nchunk, part, stat, sem, b, gridDim.x * gridDim.y,
+                   reinterpret_cast<int*>(&red[0][0][0]));
 }
 
 template <typename T>
