@@ -58,7 +58,7 @@ BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA spec
 AAD_BYTES_PER_FRAME = {"unet": 135.58e6, "linknet": 156.02e6, "resnet": 135.58e6}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -68,9 +68,9 @@ def parse():
     ap.add_argument("--num-blocks", type=int, default=2)
     ap.add_argument("--identities", type=int, default=1, help="source identities mixed in every batch (config 5: 4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--legs", default="config5_multi,d2h,fp16,config5,video,latency,arcface",
-                    help="side measurements (comma list of config5_multi (every N), d2h, fp16, config5, video, latency, "
-                         "arcface (N = 1 only); '' = none)")
+    ap.add_argument("--legs", default="config5_multi,per_batch_projection,d2h,fp16,config5,video,latency,arcface",
+                    help="side measurements (comma list of config5_multi (every N), per_batch_projection, d2h, fp16, "
+                         "config5, video, latency, arcface (N = 1 only); '' = none)")
     ap.add_argument("--c5-frames", type=int, default=240, help="video frames per GPU of the config5_multi leg")
     ap.add_argument("--video", type=int, default=900, help="frames of the config-3 video leg")
     ap.add_argument("--cpu-batches", default="1,64", help="CPU baseline batch sizes ('' = skip)")
@@ -81,7 +81,10 @@ def parse():
                     help="batches in flight on the GPU (dp.GatherPipeline streams; 1 = one batch at a time)")
     ap.add_argument("--opt", action="append", default=[],
                     help="AEI_Net plan option name=value (A/B runs), e.g. --opt fuse_stats=0")
-    return ap.parse_args()
+    # the launcher's CPU rehearsal (tests/test_dp_cpu.py): gloo ranks on the CPU with a stand-in swap, the same
+    # timed region / record / relay as the GPU run
+    ap.add_argument("--standin-cpu", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
 
 _MANGLED_TYPES = {"__bf16": "DF16b", "_Float16": "DF16_", "float": "f"}
@@ -309,6 +312,26 @@ def fp16_leg(dev, crops, z, steps, warmup, backbone, nb, nstreams=1):
     return {"workload": f"config 2 with a .half() module: batch={B} {backbone}/{nb} fp16 storage (fp32 accumulation), "
                         f"u8 in -> u8 out, {ns} batch(es) in flight",
             "dtype": "f16", "frames_per_s": round(B * steps / el, 1), "ms_per_batch": round(el * 1e3 / steps, 3)}
+
+
+def per_batch_projection_leg(G, crops, zs, idx, steps, warmup, nstreams):
+    """The headline step without the identity table: the literal faceshifter_batch work of
+    utils/inference/faceshifter_run.py:15-19 — the source embedding repeated over the batch (B rows, :15-16) and
+    every AADLayer's fc1/fc2 plus up1 projected from those rows in every batch (AEI_Net.swap_u8), same crops,
+    same batches in flight.  The bytes equal the headline's (tests/test_gpu_pipeline.py)."""
+    from ghost_amd.inference.dp import GatherPipeline
+    dev = crops.device
+    B = crops.shape[0]
+    zrows = zs.index_select(0, idx.long()).contiguous()
+
+    def swap(c, o):
+        return G.swap_u8(c, zrows, out=o)
+    pipe = GatherPipeline(swap, (B, 256, 256, 3), dev, depth=2, streams=max(1, nstreams))
+    el = timed_region(lambda: pipe.submit(crops), pipe.drain, steps, warmup, 1, dev)
+    return {"workload": f"config 2 with per-batch identity projections: batch={B}, z_id rows repeated over the batch "
+                        f"and fc1/fc2/up1 computed in every step (faceshifter_run.py:15-19), u8 in -> u8 out, "
+                        f"{pipe.nstreams} batch(es) in flight",
+            "frames_per_s": round(B * steps / el, 1), "ms_per_batch": round(el * 1e3 / steps, 3)}
 
 
 def d2h_leg(swap, crops, steps, nstreams=1):
@@ -692,10 +715,11 @@ def device_sync(dev: torch.device) -> None:
         torch.cuda.synchronize(dev)
 
 
-def timed_region(step, drain, steps, warmup, world, dev, before_timed=None) -> float:
+def timed_region(step, drain, steps, warmup, world, dev, before_timed=None, per_rank=None) -> float:
     """W untimed warm-up steps, then EXACTLY K timed steps bracketed by a barrier + device synchronize on
     both sides (every step's collective drained inside the region); returns the max over ranks of the
-    K steps' wall time (an all-reduce MAX over the group: RCCL on the GPU, gloo in the CPU test)."""
+    K steps' wall time (an all-gather of every rank's time over the group: RCCL on the GPU, gloo in the CPU
+    test).  per_rank: a list that receives every rank's own time, in rank order."""
     for _ in range(warmup):
         step()
     drain()
@@ -713,16 +737,23 @@ def timed_region(step, drain, steps, warmup, world, dev, before_timed=None) -> f
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    times = [el]
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        ts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(ts, t)
+        times = [float(x.item()) for x in ts]
+        el = max(times)
+    if per_rank is not None:
+        per_rank[:] = times
     return el
 
 
-def headline_record(world, B, steps, warmup, el, backbone, num_blocks, identities, dtype, nstreams) -> dict:
+def headline_record(world, B, steps, warmup, el, backbone, num_blocks, identities, dtype, nstreams,
+                    per_rank=None) -> dict:
     """The JSON line's headline fields: value = frames of ALL ranks / max-over-ranks time (weak scaling,
-    B frames per GPU per step)."""
+    B frames per GPU per step).  rccl_world = the process group's own size (dist.get_world_size(), 1 without a
+    group), per_rank_s = every rank's timed region."""
     frames = world * B * steps
     cfg = "config 5 (mixed identities)" if identities > 1 else ("config 4" if world > 1 else "config 2")
     return {
@@ -739,17 +770,117 @@ def headline_record(world, B, steps, warmup, el, backbone, num_blocks, identitie
                    "num_blocks": num_blocks, "identities": max(1, identities),
                    "parallelism": f"dp{world}", "batches_in_flight": nstreams,
                    "identity_projection": "fc1/fc2/up1 once per source identity (AEI_Net.identity_table, before the "
-                                          "timed region), gathered per sample by identity index in every step"},
+                                          "timed region), gathered per sample by identity index in every step; "
+                                          "legs.per_batch_projection: the literal per-batch projection"},
+        "rccl_world": dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1,
+        "per_rank_s": [round(t, 6) for t in (per_rank or [el])],
     }
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def launch_ranks(a, argv) -> int:
+    """``--gpus N`` (N > 1) with no outside launcher (no WORLD_SIZE in the environment): start N ranks of this same
+    command as child processes (subprocess.Popen, never exec; this process makes no GPU call at all), one per GPU,
+    with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set as torch.distributed.run sets
+    them.  Rank 0's stdout (the JSON line) is relayed line by line as it arrives; the other ranks' stdout goes to
+    stderr.  The first rank to fail ends the others (their exact PIDs); returns non-zero if any rank failed or
+    rank 0 printed no JSON line with n_gpus == N.  The reference's loop it spreads: utils/inference/core.py:72-74."""
+    import socket
+    import subprocess
+    import threading
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    me = os.path.abspath(__file__)
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", me] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(), text=True))
+    lines = []
+
+    def relay():
+        for ln in procs[0].stdout:
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+            lines.append(ln)
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    th.join(timeout=10)
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode), 0)
+    if rc:
+        print(f"bench.py: a rank exited with status {rc}", file=sys.stderr)
+        return rc if rc > 0 else 1
+    recs = []
+    for ln in lines:
+        try:
+            recs.append(json.loads(ln))
+        except ValueError:
+            pass
+    if not any(isinstance(x, dict) and x.get("n_gpus") == a.gpus for x in recs):
+        print(f"bench.py: rank 0 printed no JSON line with n_gpus = {a.gpus}", file=sys.stderr)
+        return 1
+    return 0
+
+
+def standin_main(a, world, rank):
+    """The launcher path on the CPU (tests/test_dp_cpu.py): gloo ranks, a deterministic stand-in for the swap on
+    small crops, GatherPipeline + timed_region + headline_record as the GPU run uses them."""
+    from ghost_amd.inference.dp import GatherPipeline
+    dev = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group("gloo")
+    B = a.batch
+
+    def swap(c, o):
+        o.copy_((255 - c).flip(-1))
+    pipe = GatherPipeline(swap, (B, 4, 4, 3), dev, depth=2)
+    crops = torch.full((B, 4, 4, 3), rank, dtype=torch.uint8)
+    per = []
+    el = timed_region(lambda: pipe.submit(crops), pipe.drain, a.steps, a.warmup, world, dev, per_rank=per)
+    if rank == 0:
+        res = headline_record(world, B, a.steps, a.warmup, el, a.backbone, a.num_blocks, a.identities, a.dtype, 1, per)
+        res["data"] = "synthetic (CPU stand-in swap, gloo)"
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        return launch_ranks(a, argv)             # N ranks of this command, no GPU call in this process
+    world = int(env_world or "1")
+    if env_world is not None and a.gpus != world:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if a.standin_cpu:
+        standin_main(a, world, rank)
+        return 0
+    if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -799,7 +930,8 @@ def main():
             # recorded on the launch stream around each of its launches)
             G.profile(1 << names.index("aad_dual_256"))
 
-    el = timed_region(step, pipe.drain, a.steps, a.warmup, world, dev, before_timed)
+    per_rank = []
+    el = timed_region(step, pipe.drain, a.steps, a.warmup, world, dev, before_timed, per_rank)
     iso = {}
     clock = {"timed": (0.0, 0), "isolated": (0.0, 0)}
     if prof:
@@ -830,7 +962,7 @@ def main():
         multi_legs["config5_multi"] = config5_multi_leg(dev, world, a.c5_frames)
     if rank == 0:
         res = headline_record(world, B, a.steps, a.warmup, el, a.backbone, a.num_blocks, a.identities, a.dtype,
-                              pipe.nstreams)
+                              pipe.nstreams, per_rank)
         if prof and classes["aad_dual_256"]["launches"]:
             c = classes["aad_dual_256"]
             per_launch_formula = c["bytes"] / c["launches"]
@@ -949,6 +1081,9 @@ def main():
         legs = [s for s in a.legs.split(",") if s] if world == 1 else []
         if legs or multi_legs:
             res["legs"] = dict(multi_legs)
+        if "per_batch_projection" in legs:
+            res["legs"]["per_batch_projection"] = per_batch_projection_leg(G, crops, zs, idx, a.steps, a.warmup,
+                                                                           pipe.nstreams)
         if "d2h" in legs:
             res["legs"]["d2h"] = d2h_leg(swap, crops, a.steps, pipe.nstreams)
         if "fp16" in legs:
@@ -975,4 +1110,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

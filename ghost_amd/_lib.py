@@ -48,7 +48,7 @@ _SIGS = {
     "ghost_aei_identity_table_bytes": (i64, [vp, i32]),
     "ghost_aei_identity_table_workspace_bytes": (i64, [vp, i32]),
     "ghost_aei_identity_table": (i32, [vp, vp, i32, i64, i32, vp, i64, vp, i64, vp]),
-    "ghost_aei_swap_u8_indexed": (i32, [vp, vp, i64, i32, vp, i32, vp, vp, vp, i64, vp]),
+    "ghost_aei_swap_u8_indexed": (i32, [vp, vp, i64, i32, vp, i32, i64, vp, vp, vp, i64, vp]),
     "ghost_aei_profile": (i32, [vp, i32]),
     "ghost_aei_profile_read": (i32, [vp, i32, C.POINTER(C.c_double), C.POINTER(i64), C.POINTER(C.c_double),
                                      C.POINTER(C.c_double)]),

@@ -917,7 +917,7 @@ void plan(Ctx& c, Mode mode, int B, Io io) {
     // table instead of the workspace (AADLayer.py:28-29 fc1/fc2 and AEI_Net.py:101 up1 on each source embedding once)
     float* z32 = (float*)c.alloc((size_t)B * h->c_id * sizeof(float));
     if (!c.dry && c.ok()) c.check(rows_to_f32(io.zid_dtype, io.zid, io.zid_rs, B, h->c_id, z32, c.s), "rows_to_f32");
-    generator_prologue(c, B, z32, (float*)io.table, (char*)io.table + table_idgb_bytes(h, B));
+    generator_prologue(c, B, z32, (float*)io.table, io.table ? (char*)io.table + table_idgb_bytes(h, B) : nullptr);
     return;
   }
   void* attr[8];
@@ -1005,6 +1005,8 @@ int64_t plan_bytes(ghost_aei* h, Mode mode, int B) {
   uintptr_t fake = 0x20000000;
   for (int k = 0; k < 8; ++k) io.attr[k] = (void*)(fake + k * 0x100000);
   io.y = (void*)(fake + 0x1000000);
+  // the table the real M_IDTABLE run writes (so the sizing pass allocates exactly what that run allocates)
+  if (mode == M_IDTABLE) io.table = (void*)(fake + 0x2000000);
   plan(c, mode, B, io);
   if (!c.ok()) return (int64_t)c.rc;
   const size_t scr = (c.scratch_need + 255) & ~size_t(255);
@@ -1264,11 +1266,14 @@ extern "C" int ghost_aei_identity_table(ghost_aei* h, const void* z_id, int zid_
 }
 
 extern "C" int ghost_aei_swap_u8_indexed(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_stride, int B,
-                                         const void* table, int n_ident, const int32_t* identity_index,
-                                         uint8_t* out_u8, void* ws, int64_t ws_bytes, void* stream) {
+                                         const void* table, int n_ident, int64_t table_bytes_,
+                                         const int32_t* identity_index, uint8_t* out_u8, void* ws, int64_t ws_bytes,
+                                         void* stream) {
   if (!crops || !table || !identity_index || !out_u8) return fail(GHOST_EINVAL, "null argument");
-  if (n_ident <= 0) return fail(GHOST_EINVAL, "n_ident must be positive");
+  if (!h || n_ident <= 0) return fail(GHOST_EINVAL, "n_ident must be positive");
   if ((uintptr_t)table % 256) return fail(GHOST_EINVAL, "identity table must be 256-byte aligned");
+  // the clamped gather reads rows [0, n_ident) only: a table of fewer rows is refused here, not read past its end
+  if (table_bytes_ < (int64_t)table_bytes(h, n_ident)) return fail(GHOST_EINVAL, "identity table too small for n_ident");
   Io io;
   io.crops = crops; io.crop_bs = crop_batch_stride;
   io.table = const_cast<void*>(table); io.n_ident = n_ident; io.idx = identity_index;

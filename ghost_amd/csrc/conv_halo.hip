@@ -465,6 +465,27 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       h_ok |= (ok ? 1u : 0u) << j;
     }
   };
+  // one DMA piece of this lane's wave: jj < HPW a halo piece, else weight piece jj - HPW (jj compile-time)
+  auto issue_piece = [&](unsigned char* buf, int cb, auto jt) {
+    constexpr int jj = decltype(jt)::value;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (jj < HPW) {
+      const int piece = wid + jj * NW;
+      if (piece < HPIECES && !(DBG & 2)) {
+        const T* __restrict__ xs = ax_ + dma_base + cb * 32;
+        const void* src = ((h_ok >> jj) & 1u) ? (const void*)(xs + h_off[jj]) : (const void*)g_halo_zero;
+        __builtin_amdgcn_global_load_lds(src, buf + piece * 1024, 16, 0, 0);
+      }
+    } else if constexpr (!RESW && !(DBG & 4)) {
+      constexpr int j = jj - HPW;
+      const int piece = wid + j * NW;
+      if (piece < WPIECES) {
+        const T* __restrict__ ws = aw_ + (long)dma_n0 * a.Kpad + cb * 288;
+        __builtin_amdgcn_global_load_lds(ws + w_off[j], buf + HALO_B + piece * 1024, 16, 0, 0);
+      }
+    }
+#endif
+  };
   auto issue = [&](unsigned char* buf, int cb) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const T* __restrict__ xs = ax_ + dma_base + cb * 32;
@@ -514,6 +535,16 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   const bool plain = !a.scale && !a.shift && a.slope == 1.f && !a.tanh_out;
   constexpr int NST = ((DBG & 48) || EPX) ? 0 : ((W16 || LDSW) ? 8 : 16) + (STATS ? 1 : 0);
   if (nmine == 0) return;
+  // (experiment, DBG & 512) the second-dispatched half of the workgroup (waves 4-7, the arbitration losers on each
+  // SIMD) at static priority 1 (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+  if constexpr ((DBG & 512) != 0) {
+    if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
+  // (experiment, DBG & 256) the next stage's DMA pieces issued two per tap after the first taps' MFMAs instead of
+  // all at the top of the stage (the top of a stage then holds only the wait, the barrier and tap 0's reads)
+  constexpr bool SPREAD = (DBG & 256) != 0;
+  constexpr int NPIECE = HPW + (RESW ? 0 : WPW);
+  constexpr int PPT = 2;
   Tile cur = tile_of(0);
   set_dma_tile(cur);
   issue(lds0, 0);
@@ -528,12 +559,14 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       __builtin_amdgcn_s_waitcnt(0x0F70);
     __builtin_amdgcn_s_waitcnt(0xC07F);     // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
+    const bool more = cb + 1 < NCB || k + 1 < nmine;   // a next stage to prefetch
     if constexpr (cb + 1 < NCB) {
-      issue(nbuf, cb + 1);
+      if constexpr (!SPREAD) issue(nbuf, cb + 1);
     } else if (k + 1 < nmine) {
       set_dma_tile(tile_of(k + 1));
-      issue(nbuf, 0);
+      if constexpr (!SPREAD) issue(nbuf, 0);
     }
+    constexpr int ncb_next = cb + 1 < NCB ? cb + 1 : 0;
     const unsigned char* wb = RESW ? wres + cb * WBLK_B : buf + HALO_B;
     // fragments of tap t + 1 are read while tap t's 16 MFMAs run (two register sets): the wave never
     // waits for its own LDS reads except at the first tap of a stage
@@ -569,6 +602,25 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             acc[j][i] = mfma16x16x32<T>(wf[tap & 1][j], pf[tap & 1][i], acc[j][i]);
+        if constexpr (SPREAD) {
+          if (more) {
+            pp_unroll(std::make_integer_sequence<int, PPT>{}, [&](auto qt) {
+              constexpr int q = decltype(qt)::value;
+              if (tap * PPT + q < NPIECE) {
+                // (tap is unrolled: the piece index folds to a constant)
+                switch (tap * PPT + q) {
+#define GHOST_SPREAD_CASE(N) case N: if constexpr (N < NPIECE) issue_piece(nbuf, ncb_next, std::integral_constant<int, N>{}); break;
+                  GHOST_SPREAD_CASE(0) GHOST_SPREAD_CASE(1) GHOST_SPREAD_CASE(2) GHOST_SPREAD_CASE(3)
+                  GHOST_SPREAD_CASE(4) GHOST_SPREAD_CASE(5) GHOST_SPREAD_CASE(6) GHOST_SPREAD_CASE(7)
+                  GHOST_SPREAD_CASE(8) GHOST_SPREAD_CASE(9) GHOST_SPREAD_CASE(10) GHOST_SPREAD_CASE(11)
+                  GHOST_SPREAD_CASE(12) GHOST_SPREAD_CASE(13) GHOST_SPREAD_CASE(14) GHOST_SPREAD_CASE(15)
+#undef GHOST_SPREAD_CASE
+                  default: break;
+                }
+              }
+            });
+          }
+        }
         // the software pipeline pinned (round 5): tap + 1's 8 fragment reads go out one per MFMA over the first half
         // of this tap's 16 MFMAs, which then run while they land.  Left to itself the scheduler sank the reads to
         // their first use, and every tap waited two or three times on LDS reads it had just issued.
@@ -1065,7 +1117,21 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   constexpr int NT = G::NW * 64;
 #ifdef GHOST_TUNING
   if constexpr (G::TW == 32) {
-    if (dbg && !a.in_part) {   // experiment variants (tuning builds only)
+    if (dbg >= 256) {   // scheduling experiments, with or without the InstanceNorm partials (tuning builds only)
+#define GHOST_PP_DBX(R, NB, V)                                                                                    \
+  if (resw == R && ncb == NB && dbg == V) {                                                                      \
+    if (a.in_part)                                                                                               \
+      hipLaunchKernelGGL((conv3x3_halo_pp_kernel<T, G, R, true, NB, V>), dim3((unsigned)g), dim3(NT), 0, s, a);  \
+    else                                                                                                         \
+      hipLaunchKernelGGL((conv3x3_halo_pp_kernel<T, G, R, false, NB, V>), dim3((unsigned)g), dim3(NT), 0, s, a); \
+    return (int)hipGetLastError();                                                                               \
+  }
+#define GHOST_PP_DBX3(R, NB) GHOST_PP_DBX(R, NB, 256) GHOST_PP_DBX(R, NB, 512) GHOST_PP_DBX(R, NB, 768)
+      GHOST_PP_DBX3(true, 2) GHOST_PP_DBX3(false, 4) GHOST_PP_DBX3(false, 8) GHOST_PP_DBX3(false, 16)
+#undef GHOST_PP_DBX3
+#undef GHOST_PP_DBX
+    }
+    if (dbg && dbg < 256 && !a.in_part) {   // experiment variants (tuning builds only)
 #define GHOST_PP_DBG(R, NB, V)                                                                               \
   if (resw == R && ncb == NB && dbg == V) {                                                                 \
     hipLaunchKernelGGL((conv3x3_halo_pp_kernel<T, G, R, false, NB, V>), dim3((unsigned)g), dim3(NT), 0, s, a); \

@@ -35,26 +35,41 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 enum GhostDType { GHOST_F32 = 0, GHOST_BF16 = 1, GHOST_F16 = 2, GHOST_U8 = 3 };
 
 // Last-arriver reductions (split-K fix-up, InstanceNorm final pass): the partials one workgroup hands to another
-// cross XCDs, whose L2s are not coherent with each other.  They are stored and re-read with device-scope
-// accesses (written through / re-fetched at the L2, per access) instead of agent-scope release / acquire fences,
-// which write back / invalidate the whole L2 of the issuing XCD: measured on the swap, a fence per workgroup made
-// the fused GEMMs 2-6x slower than the GEMM + reduction kernel pair they replace.
+// cross XCDs, whose L2s are not coherent with each other.  The hand-off is MI355X_MICROARCH.md's producer form
+// "{sc1 stores} -> every storing wave's s_waitcnt vmcnt(0) -> workgroup barrier -> one lane's agent-scope atomic
+// add" and its consumer form "the workgroup whose add came last -> ONE agent acquire -> s_waitcnt vmcnt(0) ->
+// __syncthreads() -> loads", which the guide validates at any number of workgroups per CU (its sc1-loads-only
+// variant without the acquire is validated at one workgroup per CU only, and in_stats_partial_kernel /
+// conv_igemm_kernel run several).  Only the last arriver pays the acquire (one L1 invalidate of its CU); a
+// release / acquire fence in EVERY producing workgroup (each writes back or invalidates its XCD's L2) made the
+// fused GEMMs 2-6x slower than the GEMM + reduction kernel pair they replace.
+// Every write of a handed-off partial MUST be st_dev (a write-through sc1 store), and every read of one ld_dev:
+// a plain store would sit in the producer XCD's L2, which the consumer's acquire does not reach.
+// The sc1 lowering of these accesses is the gfx94x / gfx950 memory model's; the library is built for gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "ghost_amd kernels target gfx950 only (last_arrival's hand-off relies on gfx950's sc1 write-through lowering)"
+#endif
 GHOST_DEV void st_dev(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 GHOST_DEV float ld_dev(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // this workgroup's arrival at *cnt after its st_dev stores (every thread calls it; 1-D workgroups): true in the
-// last of n arrivals, which also resets the counter for the next launch on the stream.  `flag` is a word of the
-// kernel's own LDS array, free at this point: a second __shared__ object beside an LDS-DMA ring makes hipcc wait
-// vmcnt(0) before the first LDS read of every K step (cdna_hip_programming.md §6 item 4a; measured here: the split
-// GEMMs' ring drained every step, +1.8 us per B = 1 GEMM).  The caller must not overwrite `flag` before a barrier.
+// last of n arrivals, which also resets the counter for the next launch on the stream and acquires the other
+// workgroups' partials for its CU before any thread reads them.  `flag` is a word of the kernel's own LDS array,
+// free at this point: a second __shared__ object beside an LDS-DMA ring makes hipcc wait vmcnt(0) before the first
+// LDS read of every K step (cdna_hip_programming.md §6 item 4a; measured here: the split GEMMs' ring drained every
+// step, +1.8 us per B = 1 GEMM).  The caller must not overwrite `flag` before a barrier.
 GHOST_DEV bool last_arrival(unsigned* cnt, unsigned n, int* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's device-scope stores acknowledged
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag = old == n - 1;
-    if (old == n - 1) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == n - 1) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // buffer_inv sc1: this CU's L1
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the invalidate has completed before the barrier
+    }
   }
   __syncthreads();
   return *flag != 0;

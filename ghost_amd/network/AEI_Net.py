@@ -184,6 +184,7 @@ class IdentityTable:
     def __init__(self, rt, buf: torch.Tensor, off: int, n: int, device: torch.device):
         self.rt, self.buf, self.n, self.device = rt, buf, n, device
         self.ptr = buf.data_ptr() + off
+        self.nbytes = buf.numel() - off       # what the native swap checks against the size n rows need
 
     def __len__(self):
         return self.n
@@ -440,7 +441,8 @@ class AEI_Net(PackedModule):
         ws = rt.workspace("swap", B, dev, stream)
         cstride = crops_u8.stride(0) if B > 1 else 256 * 256 * 3
         _lib.check(lib.ghost_aei_swap_u8_indexed(rt.h, crops_u8.data_ptr(), cstride, B, table.ptr, table.n,
-                                                 idx.data_ptr(), out.data_ptr(), ws.data_ptr(), ws.numel(), stream),
+                                                 table.nbytes, idx.data_ptr(), out.data_ptr(), ws.data_ptr(),
+                                                 ws.numel(), stream),
                    "AEI_Net.swap_u8_indexed")
         return out
 

@@ -88,15 +88,17 @@ int ghost_aei_swap_u8(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_str
  * ghost_aei_identity_table_workspace_bytes).  The table holds results of the handle's bound weights: rebuild it after
  * re-binding.  Rows are bit-identical to the projections a ghost_aei_swap_u8 of up to 64 frames computes.
  * ghost_aei_swap_u8_indexed = ghost_aei_swap_u8 with sample b's identity rows taken from table row
- * identity_index[b] (device int32 [B], values in [0, n_ident); an out-of-range value is clamped — memory-safe, not an
- * error: validate on the host).  Workspace: ghost_aei_swap_workspace_bytes. */
+ * identity_index[b] (device int32 [B], values in [0, n_ident); an out-of-range value is clamped to that range, not
+ * reported: validate on the host).  table_bytes: the table's size, checked against
+ * ghost_aei_identity_table_bytes(h, n_ident) (GHOST_EINVAL if smaller), so the clamped gather stays inside the table.
+ * Workspace: ghost_aei_swap_workspace_bytes. */
 int64_t ghost_aei_identity_table_bytes(ghost_aei* h, int n_ident);
 int64_t ghost_aei_identity_table_workspace_bytes(ghost_aei* h, int n_ident);
 int ghost_aei_identity_table(ghost_aei* h, const void* z_id, int zid_dtype, int64_t zid_row_stride, int n_ident,
                              void* table, int64_t table_bytes, void* ws, int64_t ws_bytes, void* stream);
 int ghost_aei_swap_u8_indexed(ghost_aei* h, const uint8_t* crops, int64_t crop_batch_stride, int B, const void* table,
-                              int n_ident, const int32_t* identity_index, uint8_t* out_u8, void* ws, int64_t ws_bytes,
-                              void* stream);
+                              int n_ident, int64_t table_bytes, const int32_t* identity_index, uint8_t* out_u8, void* ws,
+                              int64_t ws_bytes, void* stream);
 
 /* Per-handle plan options (defaults are the measured choices; every forward of the handle uses them):
  *   GHOST_AEI_OPT_FUSE_UPSAMPLE (1): AADBlk8's first AADLayer pair samples upsample2x(AADBlk7 output) on the fly
@@ -123,7 +125,10 @@ int ghost_aei_swap_u8_indexed(ghost_aei* h, const uint8_t* crops, int64_t crop_b
  *                                    kernel: the same sums in the same order, the same bytes, fewer launches
  *                                    (0: the separate reduction kernels).
  * value is 0 or 1 (TAP_PARTIALS: 0..2).  A handle is not shared across threads without external
- * synchronisation. */
+ * synchronisation.  Two-stream calls of ALL handles on one device share one up-path stream (below): while one
+ * call is being captured into a HIP graph (stream capture of the caller's stream), no other handle on that device
+ * may run a two-stream call from another thread — its up-path work would join the capture — so capture with
+ * GHOST_AEI_OPT_TWO_STREAMS = 0 (ghost_amd.inference.GraphedSwap's default) or serialise the calls. */
 enum {
   GHOST_AEI_OPT_FUSE_UPSAMPLE = 0,
   GHOST_AEI_OPT_FUSE_STATS = 1,
@@ -140,13 +145,15 @@ int ghost_aei_get_option(ghost_aei* h, int option, int* value);
  * NULL taps clears them. */
 int ghost_aei_set_taps(ghost_aei* h, void* const taps[8]);
 
-/* the handle's up-path stream on `device` (created by the first two-stream forward / swap there; NULL before, or
- * when the handle runs on one stream): diagnostics of hardware-queue sharing (tools/leg_probe.py) */
+/* the up-path stream on `device` as this handle uses it: ONE low-priority stream per device for the whole process,
+ * shared by every handle on that device, created by the first two-stream forward / swap there and never destroyed
+ * (valid until the process exits; NULL before this handle's first two-stream call there, or when stream creation
+ * failed and the handle runs on one stream).  Diagnostics of hardware-queue sharing (tools/leg_probe.py). */
 int ghost_aei_up_stream(ghost_aei* h, int device, void** stream);
 
 /* per-kernel-class device timing with HIP events (bench instrumentation).
  * class_mask bit i enables class i; classes: 0 AAD kernels (all stages), 1 the block-input AAD
- * kernel at 256x256 (through-upsample, aad_v4), 2 conv3x3 (all), 3 conv3x3 at 256x256, 4 IN stats + mask,
+ * kernel at 256x256 (through-upsample: aad_v5, aad_v3.hip), 2 conv3x3 (all), 3 conv3x3 at 256x256, 4 IN stats + mask,
  * 5 encoder, 6 upsample, 7 identity projections. */
 int ghost_aei_profile(ghost_aei* h, int class_mask);
 /* after the stream is synchronised: total ms, launches, algorithmic bytes and flops of class i */

@@ -546,3 +546,58 @@ def test_force_collective_needs_a_group():
     from ghost_amd.inference import dp
     with pytest.raises(RuntimeError, match="process group"):
         dp.GatherPipeline(lambda c, o: None, (2, 8, 8, 3), "cpu", force_collective=True)
+
+
+def _bench_cmd(*args):
+    import sys
+    return [sys.executable, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"),
+            *args]
+
+
+def _clean_env(**extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT")}
+    env.update(extra)
+    return env
+
+
+def test_bench_launcher_spawns_ranks_cpu():
+    """``python bench.py --gpus 2`` with no outside launcher starts 2 ranks itself (child
+    processes with RANK / WORLD_SIZE / MASTER_* set) and relays rank 0's one JSON line: n_gpus 2, the group's own
+    size in rccl_world, both ranks' timed regions, value = all ranks' frames / the slower rank's time.  Here on
+    gloo with the CPU stand-in swap (the GPU ranks run the same launcher, timed region and record)."""
+    import json
+    import subprocess
+    r = subprocess.run(_bench_cmd("--gpus", "2", "--standin-cpu", "--steps", "3", "--warmup", "1", "--batch", "2"),
+                       capture_output=True, text=True, env=_clean_env(), timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["n_gpus"] == 2 and rec["rccl_world"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["global_batch"] == 4 and rec["steps"] == 3 and rec["warmup"] == 1
+    assert len(rec["per_rank_s"]) == 2
+    el = max(rec["per_rank_s"])
+    assert abs(rec["value"] - 2 * 2 * 3 / el) <= 0.02 * rec["value"] + 0.01
+
+
+def test_bench_world_mismatch_exits_nonzero():
+    """--gpus N under an outside launcher that started a different number of ranks: refuse (exit 2) before any
+    device or group is touched."""
+    import subprocess
+    r = subprocess.run(_bench_cmd("--gpus", "2", "--standin-cpu", "--steps", "1", "--warmup", "0"),
+                       capture_output=True, text=True, env=_clean_env(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"),
+                       timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=1" in r.stderr and not r.stdout.strip()
+
+
+def test_bench_single_process_default_is_one_rank_cpu():
+    """No --gpus, no launcher: one rank, n_gpus 1, rccl_world 1 (the driver's default N = 1 run)."""
+    import json
+    import subprocess
+    r = subprocess.run(_bench_cmd("--standin-cpu", "--steps", "2", "--warmup", "1", "--batch", "2"),
+                       capture_output=True, text=True, env=_clean_env(), timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    assert rec["n_gpus"] == 1 and rec["rccl_world"] == 1 and len(rec["per_rank_s"]) == 1

@@ -156,10 +156,21 @@ def test_config5_linknet3_four_identities_bf16(lib):
     assert tg <= 1.3 * te + 1.0, (float(tg), float(te))
 
 
-@pytest.mark.parametrize("backbone,nb,B", [("unet", 2, 4), ("linknet", 3, 2)])
+def _up_stream(G):
+    """The up-path stream this module's handle has used on cuda:0 (NULL until its first two-stream call)."""
+    import ctypes as C
+    ptr = C.c_void_p()
+    G._rt.lib.ghost_aei_up_stream(G._rt.h, 0, C.byref(ptr))
+    return ptr.value
+
+
+@pytest.mark.parametrize("backbone,nb,B", [("unet", 2, 8), ("unet", 2, 64), ("linknet", 3, 8)])
 def test_two_stream_plan_is_bit_identical(lib, backbone, nb, B):
-    """GHOST_AEI_OPT_TWO_STREAMS: the encoder's up path and the identity projections on the handle's second
-    stream give the same bytes as the one-stream plan (forward outputs, attrs and the uint8 swap)."""
+    """GHOST_AEI_OPT_TWO_STREAMS: the encoder's up path and the identity projections on the shared up-path stream
+    give the same bytes as the one-stream plan (forward outputs, attrs and the uint8 swap).  B >= 8, where the plan
+    really splits (batches of fewer than 8 frames run on one stream whatever the option says): the handle has used
+    the up-path stream after the two-stream calls and not before (at B = 2 / 4 this test
+    compared the one-stream plan with itself)."""
     G, _ = model(backbone, nb, torch.bfloat16)
     xt, z = aei_ref.make_inputs(B, 23)
     crops = torch.from_numpy(aei_ref.make_u8_crops(B, 23)).to(DEV)
@@ -170,6 +181,7 @@ def test_two_stream_plan_is_bit_identical(lib, backbone, nb, B):
         u8 = G.swap_u8(crops, z.to(DEV))
         torch.cuda.synchronize()
         res[mode] = (Y.clone(), [a.clone() for a in attr], u8.clone())
+        assert bool(_up_stream(G)) == (mode == 1), mode
     assert torch.equal(res[0][0], res[1][0])
     assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
     assert torch.equal(res[0][2], res[1][2])
@@ -203,32 +215,46 @@ def test_fused_reductions_are_bit_identical(lib, backbone, nb, dt, B, ts):
     assert torch.equal(res[0][2], res[1][2])
 
 
-def test_gather_pipeline_two_batches_in_flight(lib):
-    """dp.GatherPipeline(streams=2) (bench.py's default): consecutive batches swapped on two pipeline streams
-    at once (sharing one AEI_Net handle) give the bytes of one-at-a-time swaps, batch by batch, including a
-    short last batch; results read on the caller's stream after the batch's stream."""
+@pytest.mark.parametrize("B,nb,indexed", [(4, 5, False), (8, 5, True), (64, 4, True), (64, 3, False)])
+def test_gather_pipeline_two_batches_in_flight(lib, B, nb, indexed):
+    """dp.GatherPipeline(streams=2) (bench.py's default): consecutive batches swapped on two pipeline streams at
+    once (sharing one AEI_Net handle and, at B >= 8, the process's up-path stream) give the bytes of one-at-a-time
+    swap_u8 calls, batch by batch, including a short last batch; results read on the caller's stream after the
+    batch's stream.  indexed: the headline configuration itself — swap_u8_indexed through the
+    identity table built before the loop (bench.py's step), against serial swap_u8 with the z row projected per
+    batch (faceshifter_run.py:15-19)."""
     from ghost_amd.inference.dp import GatherPipeline
     G, _ = model("unet", 2, torch.bfloat16)
-    B, nb = 4, 5
     crops = torch.from_numpy(aei_ref.make_u8_crops(B * nb - 1, 29)).to(DEV)
     _, z = aei_ref.make_inputs(1, 29)
     zd = z.to(DEV)
     ref = [G.swap_u8(crops[i:i + B], zd).clone() for i in range(0, crops.shape[0], B)]
-    pipe = GatherPipeline(lambda c, o: G.swap_u8(c, zd, out=o), (B, 256, 256, 3), DEV, depth=2, streams=2)
-    assert pipe.depth == 2 and pipe.nstreams == 2
-    got = []
-    pending = []
-    for i in range(0, crops.shape[0], B):
-        c = crops[i:i + B]
-        pending.append(pipe.submit(c, counts=[c.shape[0]] if c.shape[0] < B else None))
-        if len(pending) == 2:                  # read batch k once k + 1 is in flight
-            got.append(pipe.result(pending.pop(0)).clone())
-    got += [pipe.result(t).clone() for t in pending]
-    pipe.drain()
     torch.cuda.synchronize()
-    assert len(got) == len(ref)
-    for a, b in zip(got, ref):
-        assert torch.equal(a, b)
+    if indexed:
+        table = G.identity_table(zd)
+        idx = torch.zeros(B, dtype=torch.int32, device=DEV)
+
+        def swap(c, o):
+            return G.swap_u8_indexed(c, table, idx[:c.shape[0]], out=o)
+    else:
+        def swap(c, o):
+            return G.swap_u8(c, zd, out=o)
+    pipe = GatherPipeline(swap, (B, 256, 256, 3), DEV, depth=2, streams=2)
+    assert pipe.depth == 2 and pipe.nstreams == 2
+    for rep in range(2):                       # the second pass reuses both slots and both streams
+        got = []
+        pending = []
+        for i in range(0, crops.shape[0], B):
+            c = crops[i:i + B]
+            pending.append(pipe.submit(c, counts=[c.shape[0]] if c.shape[0] < B else None))
+            if len(pending) == 2:                  # read batch k once k + 1 is in flight
+                got.append(pipe.result(pending.pop(0)).clone())
+        got += [pipe.result(t).clone() for t in pending]
+        pipe.drain()
+        torch.cuda.synchronize()
+        assert len(got) == len(ref)
+        for k, (a, b) in enumerate(zip(got, ref)):
+            assert torch.equal(a, b), (rep, k)
 
 
 @pytest.mark.parametrize("dt,B", [(None, 1), (torch.bfloat16, 1), (torch.bfloat16, 4), (torch.float16, 2),
@@ -424,6 +450,27 @@ def test_identity_table_indexed_swap_is_bit_identical(lib, backbone, nb, dt, B, 
     assert torch.equal(got_dev, ref)
     with pytest.raises(IndexError):
         G.swap_u8_indexed(crops, table, torch.full((B,), nid))
+
+
+def test_indexed_swap_refuses_a_short_table(lib):
+    """the C ABI checks the table's size against n_ident (the clamped gather never reads past it)."""
+    import ctypes as C
+    G, _ = model("unet", 2, torch.bfloat16)
+    _, z = aei_ref.make_inputs(1, 45)
+    table = G.identity_table(z.to(DEV))
+    crops = torch.from_numpy(aei_ref.make_u8_crops(1, 45)).to(DEV)
+    idx = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out = torch.empty(1, 256, 256, 3, dtype=torch.uint8, device=DEV)
+    rt = G._rt
+    ws = rt.workspace("swap", 1, DEV, 0)
+    lib = rt.lib
+    rc = lib.ghost_aei_swap_u8_indexed(rt.h, crops.data_ptr(), 196608, 1, table.ptr, 2, table.nbytes, idx.data_ptr(),
+                                       out.data_ptr(), ws.data_ptr(), ws.numel(), None)
+    assert rc == -1 and b"too small" in lib.ghost_last_error()
+    rc = lib.ghost_aei_swap_u8_indexed(rt.h, crops.data_ptr(), 196608, 1, table.ptr, 1, table.nbytes, idx.data_ptr(),
+                                       out.data_ptr(), ws.data_ptr(), ws.numel(), None)
+    torch.cuda.synchronize()
+    assert rc == 0 and torch.equal(out, G.swap_u8_indexed(crops, table, idx))
 
 
 def test_identity_table_refuses_stale_weights(lib):
