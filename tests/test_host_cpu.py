@@ -6,6 +6,7 @@ packed layouts are validated by replaying the kernels' index arithmetic with tor
 CPU and comparing against torch's own conv ops.
 """
 import ctypes as C
+import os
 
 import pytest
 import torch
@@ -14,6 +15,8 @@ import torch.nn.functional as F
 from ghost_amd import _lib
 from ghost_amd.network import pack
 from oracle import aei_ref
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -232,3 +235,18 @@ def test_pack_invalidation_rules():
     assert G._pack_current(rt) and not G._pack_current(object())
     G.invalidate_pack()
     assert get() is not rt
+
+
+def test_host_code_under_address_sanitizer():
+    """SURVEY.md §5 (race detection / sanitizers): the native library's host code — handle creation, the plan's dry
+    run and bump allocator at every backbone / num_blocks / dtype / batch size, argument validation, the face-mask
+    polygon code — run under AddressSanitizer + UBSan (tools/asan_host.sh builds build/asan/host_main with
+    -Xarch_host -fsanitize=address,undefined; CPU only).  Skipped when that binary has not been built here."""
+    import subprocess
+    exe = os.path.join(REPO, "build", "asan", "host_main")
+    if not os.path.exists(exe):
+        pytest.skip("build/asan/host_main not built (bash tools/asan_host.sh)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "0 failed checks" in r.stdout and "ERROR: AddressSanitizer" not in r.stderr
