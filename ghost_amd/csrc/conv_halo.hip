@@ -535,16 +535,16 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   const bool plain = !a.scale && !a.shift && a.slope == 1.f && !a.tanh_out;
   constexpr int NST = ((DBG & 48) || EPX) ? 0 : ((W16 || LDSW) ? 8 : 16) + (STATS ? 1 : 0);
   if (nmine == 0) return;
-  // (experiment, DBG & 512) the second-dispatched half of the workgroup (waves 4-7, the arbitration losers on each
-  // SIMD) at static priority 1 (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-  if constexpr ((DBG & 512) != 0) {
-    if (wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  }
-  // (experiment, DBG & 256) the next stage's DMA pieces issued two per tap after the first taps' MFMAs instead of
-  // all at the top of the stage (the top of a stage then holds only the wait, the barrier and tap 0's reads)
-  constexpr bool SPREAD = (DBG & 256) != 0;
+  // Round 6: the next stage's DMA pieces (about ten per wave: its halo and weight pieces) go out two per tap, each
+  // pair after a tap's 16 MFMAs are issued, instead of all at the top of the stage.  At the top both waves of a SIMD
+  // issued theirs back to back after the barrier (60-185 cycles per piece, MI355X_MICROARCH.md) while the matrix
+  // pipe idled; spread, each piece issues in the shadow of MFMAs already in flight, and the top of a stage holds
+  // only the wait, the barrier and tap 0's fragment reads.  Same-box per-op A/B (B = 64, tools/ab_pp.sh,
+  // profiles/r06_ab_conv_spread.txt): 128x128 331 -> 315 us, 64x64 262 -> 250, 32x32 246 -> 233, 256x256 401 ->
+  // 389; one piece per tap or three measured no better.  (DBG & 4096: the old all-at-the-top issue, A/B only.)
+  constexpr bool SPREAD = (DBG & 4096) == 0;
   constexpr int NPIECE = HPW + (RESW ? 0 : WPW);
-  constexpr int PPT = 2;
+  constexpr int PPT = 2;   // pieces per tap
   Tile cur = tile_of(0);
   set_dma_tile(cur);
   issue(lds0, 0);
@@ -604,11 +604,13 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
             acc[j][i] = mfma16x16x32<T>(wf[tap & 1][j], pf[tap & 1][i], acc[j][i]);
         if constexpr (SPREAD) {
           if (more) {
-            pp_unroll(std::make_integer_sequence<int, PPT>{}, [&](auto qt) {
+            // tap t issues pieces [t PPT, (t + 1) PPT), the last tap also whatever is left
+            pp_unroll(std::make_integer_sequence<int, 16>{}, [&](auto qt) {
               constexpr int q = decltype(qt)::value;
-              if (tap * PPT + q < NPIECE) {
+              const int pc = tap * PPT + q;
+              if ((q < PPT || (tap == 8 && pc < NPIECE)) && pc < NPIECE) {
                 // (tap is unrolled: the piece index folds to a constant)
-                switch (tap * PPT + q) {
+                switch (pc) {
 #define GHOST_SPREAD_CASE(N) case N: if constexpr (N < NPIECE) issue_piece(nbuf, ncb_next, std::integral_constant<int, N>{}); break;
                   GHOST_SPREAD_CASE(0) GHOST_SPREAD_CASE(1) GHOST_SPREAD_CASE(2) GHOST_SPREAD_CASE(3)
                   GHOST_SPREAD_CASE(4) GHOST_SPREAD_CASE(5) GHOST_SPREAD_CASE(6) GHOST_SPREAD_CASE(7)
@@ -1117,7 +1119,7 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   constexpr int NT = G::NW * 64;
 #ifdef GHOST_TUNING
   if constexpr (G::TW == 32) {
-    if (dbg >= 256) {   // scheduling experiments, with or without the InstanceNorm partials (tuning builds only)
+    if (dbg >= 4096) {   // scheduling experiments, with or without the InstanceNorm partials (tuning builds only)
 #define GHOST_PP_DBX(R, NB, V)                                                                                    \
   if (resw == R && ncb == NB && dbg == V) {                                                                      \
     if (a.in_part)                                                                                               \
@@ -1126,25 +1128,9 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
       hipLaunchKernelGGL((conv3x3_halo_pp_kernel<T, G, R, false, NB, V>), dim3((unsigned)g), dim3(NT), 0, s, a); \
     return (int)hipGetLastError();                                                                               \
   }
-#define GHOST_PP_DBX3(R, NB) GHOST_PP_DBX(R, NB, 256) GHOST_PP_DBX(R, NB, 512) GHOST_PP_DBX(R, NB, 768)
-      GHOST_PP_DBX3(true, 2) GHOST_PP_DBX3(false, 4) GHOST_PP_DBX3(false, 8) GHOST_PP_DBX3(false, 16)
-#undef GHOST_PP_DBX3
+      GHOST_PP_DBX(true, 2, 4096) GHOST_PP_DBX(false, 4, 4096) GHOST_PP_DBX(false, 8, 4096)
+      GHOST_PP_DBX(false, 16, 4096) GHOST_PP_DBX(false, 32, 4096)
 #undef GHOST_PP_DBX
-    }
-    if (dbg && dbg < 256 && !a.in_part) {   // experiment variants (tuning builds only)
-#define GHOST_PP_DBG(R, NB, V)                                                                               \
-  if (resw == R && ncb == NB && dbg == V) {                                                                 \
-    hipLaunchKernelGGL((conv3x3_halo_pp_kernel<T, G, R, false, NB, V>), dim3((unsigned)g), dim3(NT), 0, s, a); \
-    return (int)hipGetLastError();                                                                          \
-  }
-      GHOST_PP_DBG(true, 2, 2) GHOST_PP_DBG(true, 2, 8) GHOST_PP_DBG(true, 2, 16) GHOST_PP_DBG(true, 2, 18)
-      GHOST_PP_DBG(true, 2, 26) GHOST_PP_DBG(true, 2, 24)
-      GHOST_PP_DBG(false, 4, 6) GHOST_PP_DBG(false, 4, 8) GHOST_PP_DBG(false, 4, 16) GHOST_PP_DBG(false, 4, 22)
-      GHOST_PP_DBG(false, 4, 54) GHOST_PP_DBG(false, 4, 118) GHOST_PP_DBG(false, 4, 38) GHOST_PP_DBG(false, 4, 64)
-      GHOST_PP_DBG(false, 4, 86)
-      GHOST_PP_DBG(false, 8, 6) GHOST_PP_DBG(false, 8, 8) GHOST_PP_DBG(false, 8, 16) GHOST_PP_DBG(false, 8, 22)
-      GHOST_PP_DBG(false, 8, 24) GHOST_PP_DBG(false, 8, 30) GHOST_PP_DBG(false, 8, 2) GHOST_PP_DBG(false, 8, 4)
-#undef GHOST_PP_DBG
     }
   }
 #endif
