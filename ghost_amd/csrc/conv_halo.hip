@@ -660,8 +660,16 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
       __builtin_amdgcn_s_barrier();         // every wave has read its last fragments of this stage
     }
+    // The epilogue in three compile-time forms, chosen once per tile (round 6): MODE 2 = plain (AAD_ResBlk's
+    // convs: no scale / shift / activation) without a residual, 1 = plain with the residual, 0 = the general
+    // epilogue (and every EPX tile).  Left as runtime tests inside the 16 (pixel, channel) fragment loop, the plain
+    // path still ran the residual unpacking, the scale / shift table reads and a scalar branch per fragment: at
+    // 256 x 256 (an epilogue every two stages) the epilogue was ~100 of the kernel's ~400 us (GHOST_HALO_DBG=32).
+    auto epi_body = [&](auto mt) {
+    constexpr int MODE = decltype(mt)::value;
+    const bool has_res = MODE == 1 || (MODE == 0 && ares_ != nullptr);
     uint2 rraw[4][4];
-    if (ares_) {
+    if (has_res) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int q = i * 16 + lr;
@@ -691,17 +699,17 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
       for (int j = 0; j < 4; ++j) {
         const int n = cur.n0 + j * 16 + lq * 4;
         float rv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (ares_) {
+        if (has_res) {
           const T* e = reinterpret_cast<const T*>(&rraw[i][j]);
 #pragma unroll
           for (int r = 0; r < 4; ++r) rv[r] = (float)e[r];
         }
         uint2 o;
         T* oe = reinterpret_cast<T*>(&o);
-        // the lane's 4 channels' tables as one 16-byte LDS read each (n % 4 == 0), not 4 scalar reads
-        const f32x4 tsc = *reinterpret_cast<const f32x4*>(s_sc + n);
-        const f32x4 tsh = *reinterpret_cast<const f32x4*>(s_sh + n);
         if constexpr (EPX) {
+          // the lane's 4 channels' tables as one 16-byte LDS read each (n % 4 == 0), not 4 scalar reads
+          const f32x4 tsc = *reinterpret_cast<const f32x4*>(s_sc + n);
+          const f32x4 tsh = *reinterpret_cast<const f32x4*>(s_sh + n);
           // same order as conv_igemm.hip epi_std
           const f32x4 tpr = *reinterpret_cast<const f32x4*>(s_ex + n);
           float v[4];
@@ -726,10 +734,12 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
           }
         } else {
         float v[4];
-        if (plain) {   // AAD_ResBlk's convs: no scale / shift / activation, at most the residual
+        if constexpr (MODE != 0) {   // AAD_ResBlk's convs: no scale / shift / activation, at most the residual
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = ares_ ? acc[j][i][r] + rv[r] : acc[j][i][r];
+          for (int r = 0; r < 4; ++r) v[r] = MODE == 1 ? acc[j][i][r] + rv[r] : acc[j][i][r];
         } else {
+          const f32x4 tsc = *reinterpret_cast<const f32x4*>(s_sc + n);
+          const f32x4 tsh = *reinterpret_cast<const f32x4*>(s_sh + n);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float t = fmaf(acc[j][i][r], tsc[r], tsh[r]);
@@ -761,21 +771,37 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
         // lanes lq and lq ^ 1 (lane ^ 16) hold channels 16 j + 4 lq .. +3 and the next four: each sends the
         // fragment its partner completes (even lanes keep j = 0, 2, odd lanes j = 1, 3), so every lane writes
         // two 16-byte pieces of 8 channels (8 stores per wave per tile instead of 16 of 8 bytes)
-        const bool odd = (lq & 1) != 0;
-        const uint2 sa = odd ? ov[0] : ov[1], sb = odd ? ov[2] : ov[3];
-        uint2 ga, gb;
-        ga.x = (unsigned)__shfl_xor((int)sa.x, 16, 64);
-        ga.y = (unsigned)__shfl_xor((int)sa.y, 16, 64);
-        gb.x = (unsigned)__shfl_xor((int)sb.x, 16, 64);
-        gb.y = (unsigned)__shfl_xor((int)sb.y, 16, 64);
-        const uint2 a0 = odd ? ga : ov[0], a1 = odd ? ov[1] : ga;
-        const uint2 b0 = odd ? gb : ov[2], b1 = odd ? ov[3] : gb;
+        // (round 6) one v_permlane16_swap per word pair does the exchange: it swaps the odd 16-lane rows of its first
+        // operand with the even rows of its second, which leaves (a0, a1) = (own ov[0], partner's ov[0]) in even rows
+        // and (partner's ov[1], own ov[1]) in odd rows — what the ds_bpermute + select form computed
+        uint2 a0, a1, b0, b1;
+        {
+          const auto x0 = __builtin_amdgcn_permlane16_swap(ov[0].x, ov[1].x, false, false);
+          const auto y0 = __builtin_amdgcn_permlane16_swap(ov[0].y, ov[1].y, false, false);
+          const auto x1 = __builtin_amdgcn_permlane16_swap(ov[2].x, ov[3].x, false, false);
+          const auto y1 = __builtin_amdgcn_permlane16_swap(ov[2].y, ov[3].y, false, false);
+          a0 = make_uint2(x0[0], y0[0]);
+          a1 = make_uint2(x0[1], y0[1]);
+          b0 = make_uint2(x1[0], y1[0]);
+          b1 = make_uint2(x1[1], y1[1]);
+        }
         // lane lq now holds chunk m = (lq >> 1) + 2 (lq & 1) of pixel q (a) and chunk 4 + m (b): the tile row's
         // 16 pixels q - lr .. +15 are consecutive, so store_rows16 writes them as 8 whole rows per store
         static_assert(G::TW % 16 == 0, "a pixel fragment lies in one tile row");
         const long p0 = pix - lr + (lr & 7);
         store_rows16<T>(ay_ + cur.n0, p0 * a.ldy, (p0 + 8) * a.ldy, lr, (lq >> 1) + 2 * (lq & 1),
                         u32x4{a0.x, a0.y, a1.x, a1.y}, u32x4{b0.x, b0.y, b1.x, b1.y});
+      }
+    }
+    };
+    if constexpr (EPX) {
+      epi_body(std::integral_constant<int, 0>{});
+    } else {
+      if (plain) {
+        if (ares_) epi_body(std::integral_constant<int, 1>{});
+        else epi_body(std::integral_constant<int, 2>{});
+      } else {
+        epi_body(std::integral_constant<int, 0>{});
       }
     }
     if constexpr (LDSW) {
@@ -1091,10 +1117,12 @@ static int num_cus() {
 }
 
 // the persistent kernel takes 16 x 16 tiles (HaloSmall) for images that are not a multiple of 16 x 32
-// (ArcFace 112 .. 14, overhanging tiles) — or, with GHOST_HALO_PP_SMALL=1, also the generator's
+// (ArcFace 112 .. 14, overhanging tiles) and, since round 6 (GHOST_HALO_PP_SMALL, default 1), the generator's
 // 16 x 16 stage (A/B knob)
 static bool pp_small(const ConvDesc& d) {
-  static const int force = GHOST_KNOB("GHOST_HALO_PP_SMALL", 0);
+  // round 6: also the generator's 16 x 16 stage (1024 -> 1024, B = 64: 252.6 / 256.5 -> 247.7 / 251.4 us per conv
+  // against the two-workgroup kernel since the spread DMA issue, profiles/r06_ab_conv_spread.txt)
+  static const int force = GHOST_KNOB("GHOST_HALO_PP_SMALL", 1);
   return !halo_exact_wide(d) && halo_small_ok(d) &&
          (force || d.Wi % HaloSmall::TW || d.Hi % HaloSmall::TH || d.prelu || d.y2 || d.res_first);
 }
@@ -1119,7 +1147,7 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   constexpr int NT = G::NW * 64;
 #ifdef GHOST_TUNING
   if constexpr (G::TW == 32) {
-    if (dbg >= 4096) {   // scheduling experiments, with or without the InstanceNorm partials (tuning builds only)
+    if (dbg) {   // experiment variants, with or without the InstanceNorm partials (tuning builds only)
 #define GHOST_PP_DBX(R, NB, V)                                                                                    \
   if (resw == R && ncb == NB && dbg == V) {                                                                      \
     if (a.in_part)                                                                                               \
@@ -1129,6 +1157,9 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
     return (int)hipGetLastError();                                                                               \
   }
       GHOST_PP_DBX(true, 2, 4096) GHOST_PP_DBX(false, 4, 4096) GHOST_PP_DBX(false, 8, 4096)
+      // where the 256 x 256 conv's time goes: 2 no halo DMA, 16 no output stores, 32 no epilogue, 34 neither
+      GHOST_PP_DBX(true, 2, 2) GHOST_PP_DBX(true, 2, 16) GHOST_PP_DBX(true, 2, 32) GHOST_PP_DBX(true, 2, 34)
+      GHOST_PP_DBX(true, 2, 8)
       GHOST_PP_DBX(false, 16, 4096) GHOST_PP_DBX(false, 32, 4096)
 #undef GHOST_PP_DBX
     }
