@@ -540,7 +540,7 @@ __global__ void __launch_bounds__(G::NW * 64) conv3x3_halo_pp_kernel(const HaloA
   // issued theirs back to back after the barrier (60-185 cycles per piece, MI355X_MICROARCH.md) while the matrix
   // pipe idled; spread, each piece issues in the shadow of MFMAs already in flight, and the top of a stage holds
   // only the wait, the barrier and tap 0's fragment reads.  Same-box per-op A/B (B = 64, tools/ab_pp.sh,
-  // profiles/r06_ab_conv_spread.txt): 128x128 331 -> 315 us, 64x64 262 -> 250, 32x32 246 -> 233, 256x256 401 ->
+  // profiles/r06_ab_kernels.txt): 128x128 331 -> 315 us, 64x64 262 -> 250, 32x32 246 -> 233, 256x256 401 ->
   // 389; one piece per tap or three measured no better.  (DBG & 4096: the old all-at-the-top issue, A/B only.)
   constexpr bool SPREAD = (DBG & 4096) == 0;
   constexpr int NPIECE = HPW + (RESW ? 0 : WPW);
@@ -1117,12 +1117,10 @@ static int num_cus() {
 }
 
 // the persistent kernel takes 16 x 16 tiles (HaloSmall) for images that are not a multiple of 16 x 32
-// (ArcFace 112 .. 14, overhanging tiles) and, since round 6 (GHOST_HALO_PP_SMALL, default 1), the generator's
-// 16 x 16 stage (A/B knob)
+// (ArcFace 112 .. 14, overhanging tiles) — or, with GHOST_HALO_PP_SMALL=1, also the generator's 16 x 16 stage (A/B knob;
+// its 1024 -> 1024 and cat 2048 -> 512 convs are outside the persistent kernel's N <= 512 / NCB <= 32 anyway)
 static bool pp_small(const ConvDesc& d) {
-  // round 6: also the generator's 16 x 16 stage (1024 -> 1024, B = 64: 252.6 / 256.5 -> 247.7 / 251.4 us per conv
-  // against the two-workgroup kernel since the spread DMA issue, profiles/r06_ab_conv_spread.txt)
-  static const int force = GHOST_KNOB("GHOST_HALO_PP_SMALL", 1);
+  static const int force = GHOST_KNOB("GHOST_HALO_PP_SMALL", 0);
   return !halo_exact_wide(d) && halo_small_ok(d) &&
          (force || d.Wi % HaloSmall::TW || d.Hi % HaloSmall::TH || d.prelu || d.y2 || d.res_first);
 }

@@ -765,6 +765,81 @@ upsample2x_rows_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int 
   }
 }
 
+// Round 6: 2 x 2 output quads.  With align_corners and an exact x2 scale, output rows 2q-1 and 2q (q >= 1) both
+// sample source rows (q-1, q), and output columns 2k-1 and 2k both sample source columns (k-1, k) (up2x_pairing_ok
+// checks both facts in fp32 on the host, as aad_v3.hip's v5_pairing_ok does for rows).  So a thread that owns the
+// quad {2q-1, 2q} x {2k-1, 2k} (one 16-byte chunk of channels) loads the 4 source chunks once and mixes its 4
+// outputs from them — up2x_mix on the same operands with each output's own weights, the rows kernel's values bit for
+// bit — 4 loads per 4 outputs instead of 4 per output (the rows kernel was bound by its L1 requests: the encoder's
+// z_attr8, 0.69 GB of HBM traffic, took 169 us).  The edge quads (q = 0: rows {0, 2H-1}; k = 0: columns
+// {0, 2W-1}) take each output's own taps.
+template <typename T, bool NT>
+__global__ void __launch_bounds__(256)
+upsample2x_quad_kernel(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy, const Up2xSrc u, int lg_nch) {
+  constexpr int VEC = Vec16<T>::N;
+  const int Wo = 2 * u.W, Ho = 2 * u.H;
+  const int i = blockIdx.x * 256 + threadIdx.x;   // (column pair k, chunk ci)
+  if (i >= (u.W << lg_nch)) return;
+  const int k = i >> lg_nch, ci = i - (k << lg_nch);
+  const int bq = blockIdx.y, b = bq / u.H, q = bq - b * u.H;
+  const int oy[2] = {q == 0 ? 0 : 2 * q - 1, q == 0 ? Ho - 1 : 2 * q};
+  const int ox[2] = {k == 0 ? 0 : 2 * k - 1, k == 0 ? Wo - 1 : 2 * k};
+  const T* xs = x + (long)b * u.H * u.W * ldx + ci * VEC;
+  T* ys = y + (long)b * Ho * Wo * ldy + ci * VEC;
+  auto put = [&](int oyy, int oxx, const float* o) {
+    T* d = ys + ((long)oyy * Wo + oxx) * ldy;
+    if constexpr (NT) store16_f_nt(d, o);
+    else store16_f(d, o);
+  };
+  if (q == 0 || k == 0) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        float o[VEC];
+        up2x_load16_f(xs, ldx, up2x_tap(u, oy[r], ox[c]), o);
+        put(oy[r], ox[c], o);
+      }
+    return;
+  }
+  Up2xTap t[2][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) t[r][c] = up2x_tap(u, oy[r], ox[c]);
+  // every output of the quad has the taps (q-1, q) x (k-1, k): the first output's offsets serve all four
+  float v00[VEC], v01[VEC], v10[VEC], v11[VEC];
+  load16_f(xs + (long)t[0][0].o00 * ldx, v00);
+  load16_f(xs + (long)t[0][0].o01 * ldx, v01);
+  load16_f(xs + (long)t[0][0].o10 * ldx, v10);
+  load16_f(xs + (long)t[0][0].o11 * ldx, v11);
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const Up2xTap& tt = t[r][c];
+      float o[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) o[e] = up2x_mix(tt.ly0, tt.ly1, tt.lx0, tt.lx1, v00[e], v01[e], v10[e], v11[e]);
+      put(oy[r], ox[c], o);
+    }
+}
+
+// both grids of a x2 upsample pair up (see upsample2x_quad_kernel), checked in the kernel's fp32 arithmetic
+static bool up2x_pairs(int n, float sc) {
+  auto f0 = [&](int o, float* fr) {
+    volatile float r = sc * (float)o;   // one fp32 multiply, as up2x_tap (no contraction)
+    const int v = (int)r;
+    if (fr) *fr = r - (float)v;
+    return v;
+  };
+  float a, z;
+  if (n < 2 || f0(0, &a) != 0 || a != 0.f || f0(2 * n - 1, &z) != n - 1 || z != 0.f) return false;
+  for (int q = 1; q < n; ++q)
+    if (f0(2 * q - 1, nullptr) != q - 1 || f0(2 * q, nullptr) != q - 1) return false;
+  return true;
+}
+
 int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, int W, int C, hipStream_t s) {
   const int vec = dt == GHOST_F32 ? 4 : 8;
   if (C % vec || ldx % vec || ldy % vec || (uintptr_t)x % 16 || (uintptr_t)y % 16) return -1;
@@ -782,6 +857,18 @@ int upsample2x(int dt, const void* x, int ldx, void* y, int ldy, int B, int H, i
     // has left L2 and the Infinity Cache) are written with non-temporal stores
     static const int nt_knob = GHOST_KNOB("GHOST_UP_NT", 1);
     const bool nt = nt_knob && (long)B * 4 * H * W * C * 2 >= (64L << 20);
+    static const int quad = GHOST_KNOB("GHOST_UP_QUAD", 1);
+    if (quad && up2x_pairs(H, u.sh) && up2x_pairs(W, u.sw)) {
+      const dim3 gq((unsigned)((W * nch + 255) / 256), (unsigned)(B * H));
+#define GHOST_UPQ(T)                                                                                           \
+      if (nt)                                                                                                    \
+        hipLaunchKernelGGL((upsample2x_quad_kernel<T, true>), gq, dim3(256), 0, s, (const T*)x, ldx, (T*)y, ldy, u, lg); \
+      else                                                                                                       \
+        hipLaunchKernelGGL((upsample2x_quad_kernel<T, false>), gq, dim3(256), 0, s, (const T*)x, ldx, (T*)y, ldy, u, lg);
+      if (dt == GHOST_BF16) { GHOST_UPQ(bf16) } else { GHOST_UPQ(_Float16) }
+#undef GHOST_UPQ
+      return (int)hipGetLastError();
+    }
 #define GHOST_UPR(T)                                                                                               \
     if (rows == 4)                                                                                                 \
       hipLaunchKernelGGL((upsample2x_rows_kernel<T, 4>), grid, dim3(256), 0, s, (const T*)x, ldx, (T*)y, ldy, u, lg); \
