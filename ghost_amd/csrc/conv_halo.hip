@@ -1138,7 +1138,11 @@ static int halo_pp_launch(const ConvDesc& d, hipStream_t s) {
   a.ntiles = d.B / G::IMG * a.tiles_x * a.tiles_y * a.nNt;
   static const int dbg = GHOST_KNOB("GHOST_HALO_DBG", 0);
   a.dbg = dbg;
-  const int g = a.ntiles < num_cus() ? a.ntiles : num_cus();
+  // (A/B knob, tuning build) the persistent grid as a share of the CUs: with two batches in flight the other
+  // batch's kernels can only use the CUs this kernel's 150 KB-LDS workgroups leave free
+  static const int pct = GHOST_KNOB("GHOST_PP_GRID_PCT", 100);
+  const int ncu = pct >= 100 ? num_cus() : (num_cus() * pct / 100 + 7) / 8 * 8;
+  const int g = a.ntiles < ncu ? a.ntiles : ncu;
   a.in_part = d.in_part;
   const bool resw = d.Cin <= 64 && d.N == 64;
   const int ncb = d.Cin / 32;

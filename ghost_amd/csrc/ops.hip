@@ -28,15 +28,21 @@ GHOST_DEV void in_stats_store(float* __restrict__ stat, long i, double K, double
   stat[i * 2 + 1] = (float)(1.0 / sqrt(var + (double)kInEps));
 }
 
-// Fused final pass (sem != nullptr): the partial workgroups store with st_dev, and the last of sample b's
-// `arrivals` to finish merges the sample's partials — the sums of in_stats_final_kernel in its order, one launch per
-// statistics pass instead of two.  Each thread's chunk partials are loaded as one batch of independent device-scope
-// loads before any is summed (a dependent load per chunk is a fabric round trip each).
+// Fused final pass (sem != nullptr): the partial workgroups store with st_dev, and the last of the `arrivals` chunk
+// workgroups of (sample b, 64-channel group cg) to finish merges that group's partials — the sums of
+// in_stats_final_kernel in its order, one launch per statistics pass instead of two.  Each thread's chunk partials are
+// loaded as one batch of independent device-scope loads before any is summed (a dependent load per chunk is a fabric
+// round trip each).  Round 6: one counter per (sample, channel group), sem[b * ncg + cg], instead of one per sample:
+// the sample's last arriver merged all C channels alone (C = 1024: 16 channels per thread behind one workgroup, the
+// 8 x 8 .. 32 x 32 stages' statistics 28-30 us against 10-12 for the two-kernel form); now each group's last
+// arriver merges its own 64.
 template <typename T>
 GHOST_DEV void in_stats_fixup(const T* __restrict__ x, int ldx, long bstride, int HW, int C, int nchunk,
-                              const float* part, float* stat, unsigned* sem, int b, unsigned arrivals, int* flag) {
-  if (!last_arrival(sem + b, arrivals, flag)) return;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+                              const float* part, float* stat, unsigned* sem, int b, int cg, int ncg, unsigned arrivals,
+                              int* flag) {
+  if (!last_arrival(sem + (long)b * ncg + cg, arrivals, flag)) return;
+  const int cend = min(C, cg * 64 + 64);
+  for (int c = cg * 64 + threadIdx.x; c < cend; c += blockDim.x) {
     const double K = (double)to_f(x[(long)b * bstride * ldx + c]);
     const float* o = part + ((long)b * nchunk * C + c) * 2;   // chunk k: o + 2 k C
     double S1 = 0.0, S2 = 0.0;
@@ -81,21 +87,33 @@ in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chu
   const int p0 = ch * chunk;
   const int p1 = min(HW, p0 + chunk);
   if (cok) {
-    for (int p = p0 + po; p < p1; p += PPP) {
-      float v[VEC];
-      if constexpr (UP) {
-        const int oy = p / (2 * u.W), ox = p - oy * (2 * u.W);
-        up2x_load16_f(xb + c0, ldx, up2x_tap(u, oy, ox), v);
+    // (round 6) four of the thread's pixels per iteration, every load issued before the first is used: one pixel
+    // per iteration waited a full load latency per pixel (the 16 x 16 stage's statistics, 256 pixels per workgroup:
+    // 28 us for 34 MB).  The sums run in the same pixel order as before, so the partials are bit for bit the same.
+    constexpr int U = 4;
+    for (int p = p0 + po; p < p1; p += U * PPP) {
+      float v[U][VEC];
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) v[e] = to_f(from_f<T>(v[e]));
-      } else {
-        load16_f(xb + (long)p * ldx + c0, v);
+      for (int uu = 0; uu < U; ++uu) {
+        const int pu = min(p + uu * PPP, p1 - 1);   // clamped, not skipped: all loads in flight at once
+        if constexpr (UP) {
+          const int oy = pu / (2 * u.W), ox = pu - oy * (2 * u.W);
+          up2x_load16_f(xb + c0, ldx, up2x_tap(u, oy, ox), v[uu]);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) v[uu][e] = to_f(from_f<T>(v[uu][e]));
+        } else {
+          load16_f(xb + (long)pu * ldx + c0, v[uu]);
+        }
       }
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) {
-        const float d = v[e] - K[e];
-        s1[e] += d;
-        s2[e] = fmaf(d, d, s2[e]);
+      for (int uu = 0; uu < U; ++uu) {
+        if (p + uu * PPP >= p1) break;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float d = v[uu][e] - K[e];
+          s1[e] += d;
+          s2[e] = fmaf(d, d, s2[e]);
+        }
       }
     }
   }
@@ -110,19 +128,25 @@ in_stats_partial_kernel(const T* __restrict__ x, int ldx, int HW, int C, int chu
     float a = 0.f, q = 0.f;
     for (int i = 0; i < PPP; ++i) { a += red[0][i][t]; q += red[1][i][t]; }
     if (c < C) {
-      float* o = part + (((long)b * nchunk + ch) * C + c) * 2;
-      if (sem) {
-        st_dev(o, a);
-        st_dev(o + 1, q);
+      if (nchunk == 1) {
+        // (round 6) one chunk: this workgroup saw every pixel of its channels, so it finishes them itself — the sums
+        // in_stats_final_kernel would form from its single record, with no partials, counter or second launch
+        in_stats_store(stat, (long)b * C + c, (double)to_f(xb[c]), (double)a, (double)q, HW);
       } else {
-        o[0] = a;
-        o[1] = q;
+        float* o = part + (((long)b * nchunk + ch) * C + c) * 2;
+        if (sem) {
+          st_dev(o, a);
+          st_dev(o + 1, q);
+        } else {
+          o[0] = a;
+          o[1] = q;
+        }
       }
     }
   }
-  if (sem)
-    in_stats_fixup(x, ldx, UP ? (long)u.H * u.W : (long)HW, HW, C, nchunk, part, stat, sem, b, gridDim.x * gridDim.y,
-                   reinterpret_cast<int*>(&red[0][0][0]));
+  if (sem && nchunk > 1)
+    in_stats_fixup(x, ldx, UP ? (long)u.H * u.W : (long)HW, HW, C, nchunk, part, stat, sem, b, cg, (int)gridDim.y,
+                   gridDim.x, reinterpret_cast<int*>(&red[0][0][0]));
 }
 
 // Statistics of upsample2x(x) without visiting the upsampled pixels.  The x2 bilinear upsample is
@@ -255,7 +279,7 @@ in_stats_up_quad_kernel(const T* __restrict__ x, int ldx, int C, int nchunk, flo
     }
   }
   if (sem)
-    in_stats_fixup(x, ldx, (long)u.H * u.W, 4 * u.H * u.W, C, nchunk, part, stat, sem, b, gridDim.x * gridDim.y,
+    in_stats_fixup(x, ldx, (long)u.H * u.W, 4 * u.H * u.W, C, nchunk, part, stat, sem, b, cg, (int)gridDim.y, gridDim.x,
                    reinterpret_cast<int*>(&red[0][0][0]));
 }
 
@@ -380,7 +404,7 @@ static void in_stats_launch(const T* x, int ldx, int B, int HW, int C, float* st
   else
     hipLaunchKernelGGL((in_stats_partial_kernel<T, false>), g1, dim3(256), 0, s, x, ldx, HW, C, chunk, nchunk, part, u,
                        stat, sem);
-  if (sem) return;
+  if (sem || nchunk == 1) return;   // the statistics are final (fused fix-up, or one chunk per workgroup)
   const long bstride = up ? (long)u.H * u.W : HW;
   hipLaunchKernelGGL(in_stats_final_kernel<T>, g2, dim3(256), 0, s, x, ldx, bstride, B, HW, C, nchunk, part, stat);
 }
@@ -391,7 +415,7 @@ static int in_stats_any(int dt, const void* x, int ldx, int B, int HW, int C, fl
   if (!ws || ws_bytes < in_stats_workspace_bytes(B, HW, C)) return -1;
   float* part = reinterpret_cast<float*>(ws);
   static const int fuse_knob = GHOST_KNOB("GHOST_STATS_FUSE", 1);
-  if (!fuse_knob || B > nsem) sem = nullptr;   // one counter per sample
+  if (!fuse_knob || (long)B * ((C + 63) / 64) > nsem) sem = nullptr;   // one counter per (sample, 64 channels)
   if (dt == GHOST_F32)
     in_stats_launch((const float*)x, ldx, B, HW, C, stat, part, up, s, sem);
   else if (dt == GHOST_BF16)

@@ -208,7 +208,7 @@ def stats_cases(lib, iters, dt=torch.bfloat16):
     B = 64
     st = torch.cuda.current_stream().cuda_stream
     ws = torch.empty(256 << 20, dtype=torch.uint8, device=DEV)
-    for C, n in [(64, 256), (128, 128)]:
+    for C, n in [(64, 256), (128, 128), (512, 32), (1024, 16)]:
         x = torch.randn(B, n, n, C, device=DEV).to(dt)
         stat = torch.empty(B, C, 2, device=DEV)
         us = timeit(lambda: _lib.check(lib.ghost_instnorm_stats_nhwc(_lib.gdtype(dt), x.data_ptr(), B, n * n, C, C,
