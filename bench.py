@@ -185,7 +185,8 @@ def rocprof_avg_us(kname):
 def aad_v4_min_bytes(B, ca8, nl, num_blocks, tap_partials):
     """Minimum HBM bytes of one aad_v4 launch (AADBlk8's block-input AADLayer pair at 256x256, bf16): the
     128x128x64 h_in source once, z_attr8 (ca8 channels) once, and each of the nl outputs as stored — 64 bf16
-    channels, or 32 fp16 tap partials for a layer that feeds the 3x3 conv to RGB through them
+    channels, or the 15 fp16 per pixel of row-summed tap partials (ghost_amd/csrc/tap_rows.h) for a layer that
+    feeds the 3x3 conv to RGB through them
     (GHOST_AEI_OPT_TAP_PARTIALS: nb >= 2 -> last_add_block's layer in mode 2; nb = 1 -> the h path's layer in
     modes 1 and 2, last_add_block's in mode 2).  Returns (bytes, layers writing partials, the kernel's ZPM mask)."""
     if num_blocks >= 2:
@@ -193,7 +194,7 @@ def aad_v4_min_bytes(B, ca8, nl, num_blocks, tap_partials):
     else:
         zpm = {0: 0, 1: 1, 2: 3}.get(tap_partials, 0)
     n_part = min(nl, bin(zpm).count("1"))
-    return B * (128 * 128 * 64 + 65536 * ca8 + (nl - n_part) * 65536 * 64 + n_part * 65536 * 32) * 2.0, n_part, zpm
+    return B * (128 * 128 * 64 + 65536 * ca8 + (nl - n_part) * 65536 * 64 + n_part * 65536 * 15) * 2.0, n_part, zpm
 
 
 def arcface_flops_per_face(layers=(3, 13, 30, 3)):
@@ -973,7 +974,7 @@ def main(argv=None):
             nl = max(1, round(per_launch_formula / (B * 65536 * (2 * 64 + ca8) * 2)))
             # minimum bytes of the fused kernel: h_in's 128x128 source once, z_attr8 once, nl outputs; an output
             # whose layer feeds AADBlk8's conv to 3 channels through tap partials (GHOST_AEI_OPT_TAP_PARTIALS) is
-            # 32 fp16 partial sums per pixel instead of 64 bf16 channels: nb >= 2 -> last_add_block's layer (mode
+            # 15 fp16 row-summed partials per pixel instead of 64 bf16 channels: nb >= 2 -> last_add_block's layer (mode
             # 2); nb = 1 -> the h path's layer (modes 1, 2) and last_add_block's (mode 2)
             zp = G.get_option("tap_partials") if a.dtype == "bf16" else 0
             per_launch_min, n_part, zpm = aad_v4_min_bytes(B, ca8, nl, a.num_blocks, zp)
@@ -1013,7 +1014,7 @@ def main(argv=None):
                 "live_clock_us": round(live_s * 1e6, 2), "launches_timed": clk_n if clocked else c["launches"],
                 "bytes_per_launch": per_launch_min,
                 "bytes_note": "achieved = minimum bytes of the fused kernel (128x128 h_in source + z_attr8 + outputs "
-                              "as stored: 64 bf16 channels, or 32 fp16 tap partials per pixel) / launch duration",
+                              "as stored: 64 bf16 channels, or 15 fp16 row-summed tap partials per pixel) / launch duration",
                 "fractions": {
                     "minimum_bytes": fr(per_launch_min, per_launch_s),
                     "physical_pmc": fr(tr["bytes_per_launch"], per_launch_s) if tr else None,

@@ -22,10 +22,11 @@ struct AadV3Desc {
   const float* idgb[2] = {nullptr, nullptr};
   void* out[2] = {nullptr, nullptr};
   int ldo[2] = {0, 0};
-  // tap partials (C = 64 only): a layer with zw[l] set writes, instead of its 64 channels, the 32 fp16
-  // values Z[p][t*3 + o] = sum_c zw[l][t*3 + o][c] * out_c(p) (t = ky*3 + kx, o < 3; rows >= 27 zero)
-  // of the 3x3 conv to 3 channels that is its only consumer (zw: bf16 rows of stride zwld, the narrow
-  // layout's K slice of this layer's channels); out[l] is then that [B*HW][32] fp16 buffer
+  // tap partials (C = 64 only): a layer with zw[l] set writes, instead of its 64 channels, its share of
+  // the 3x3 conv to 3 channels that is its only consumer, per-tap sums Z_t[o] = sum_c zw[l][t*3 + o][c] *
+  // out_c (t = ky*3 + kx) pre-summed along 8-column row segments (tap_rows.h: 15 fp16 per pixel; zw: bf16
+  // rows of stride zwld, the narrow layout's K slice of this layer's channels); out[l] is then that buffer,
+  // zr_image(HW) fp16 per sample, and the image width must be a multiple of 8
   const void* zw[2] = {nullptr, nullptr};
   int zwld = 0;
   // in-kernel clock of the launch (profiling; v4 / v5): aad_v3_clock_words(d) words of per-workgroup start

@@ -21,6 +21,7 @@
 
 #include "aad_v3.h"
 #include "ghost_common.h"
+#include "tap_rows.h"
 #include "up2x.h"
 
 namespace ghost {
@@ -53,10 +54,12 @@ struct AadV3ArgsT {
 
 static constexpr int kWaves = 8;
 
-// tap partials of one 16-pixel tile: xf[sh] = the bf16 outputs (channels 32 sh + 8 lq .. +7 of pixel lr, the
-// MFMA B-operand layout), W = the layer's 32 x 64 projection rows in LDS (64-element rows, see zw_idx); lane
-// ends with Z rows 16 rt + 4 lq .. +3 of pixel lr, stored as fp16 (8 bytes)
+// tap partials (tap_rows.h): MFMA row tile o, row 4 dy + dx holds the projection of tap (dy, dx) to channel o
+// (dy, dx < 3; the other rows zero), so a lane (pixel lr, lq = dy) ends with the three dx of each o; the lane
+// then sums its row neighbours inside the 8-column segment and stores fp16 row sums plus the segment-end
+// terms.  LDS holds only the 27 real rows, 9 o + 3 dy + dx, and one zero row that the others read.
 constexpr int ZLD = 64;
+constexpr int kZpRows = 28;
 // element offset of (row, k) in an unpadded image of 64-element (128-byte) rows with the 16-byte chunks XOR-
 // swizzled by row & 7: the ds_read_b128 of rows 16 rt + lr, chunk 4 ks + lq is conflict-free in every 16-lane
 // group (the +8-element padding it replaces was 2-way in half the groups and cost 1 KB per 64 rows)
@@ -79,52 +82,68 @@ template <int ZPM>
 GHOST_DEV constexpr int zp_slot(int l) { return l == 0 ? 0 : (ZPM & 1); }
 template <int ZPM>
 constexpr int zp_nlayers() { return (ZPM & 1) + ((ZPM >> 1) & 1); }
-template <typename T>
-GHOST_DEV void zp_store(const T* __restrict__ W, const v8_t<T> (&xf)[2], _Float16* __restrict__ zrow, int lr, int lq) {
-#pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const v8_t<T> wf = *reinterpret_cast<const v8_t<T>*>(&W[sw64(rt * 16 + lr, ks * 32 + lq * 8)]);
-      acc = mfma16x16x32<T>(wf, xf[ks], acc);
-    }
-    typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
-    const f16x4 h = {(_Float16)acc[0], (_Float16)acc[1], (_Float16)acc[2], (_Float16)acc[3]};
-    *reinterpret_cast<f16x4*>(zrow + rt * 16 + lq * 4) = h;
-  }
-}
 
-// the same, one K half at a time (K step ks = the half sh just computed): keeps 8 accumulator registers live
-// instead of both halves' T fragments
+// one K half (K step ks = the half sh just computed) into the three row tiles: 12 accumulator registers live
 template <typename T>
-GHOST_DEV void zp_mfma_half(const T* __restrict__ W, const v8_t<T>& xf, int ks, f32x4 (&acc)[2], int lr, int lq) {
+GHOST_DEV void zp_mfma_half(const T* __restrict__ W, const v8_t<T>& xf, int ks, f32x4 (&acc)[3], int lr, int lq) {
+  const int dy = lr >> 2, dx = lr & 3;
+  const bool real = dy < 3 && dx < 3;   // else the zero row 27
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
+  for (int rt = 0; rt < 3; ++rt) {
     asm volatile("" ::: "memory");   // the projection rows are re-read per use, not held across the tile loop
-    const v8_t<T> wf = *reinterpret_cast<const v8_t<T>*>(&W[sw64(rt * 16 + lr, ks * 32 + lq * 8)]);
+    const int row = real ? rt * 9 + dy * 3 + dx : 27;
+    const v8_t<T> wf = *reinterpret_cast<const v8_t<T>*>(&W[sw64(row, ks * 32 + lq * 8)]);
     acc[rt] = mfma16x16x32<T>(wf, xf, acc[rt]);
   }
 }
-GHOST_DEV void zp_store_acc(const f32x4 (&acc)[2], _Float16* __restrict__ zrow, int lq) {
+GHOST_DEV float zp_from_left(float v) {    // lane lr - 1's value (row_shr:1 within the 16-lane row)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true));
+}
+GHOST_DEV float zp_from_right(float v) {   // lane lr + 1's value (row_shl:1)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xf, 0xf, true));
+}
+// the lane's pixel p (in the image) at column lr & 7 of its segment; zimg = the image's buffer (tap_rows.h)
+GHOST_DEV void zp_store_acc(const f32x4 (&acc)[3], _Float16* __restrict__ zimg, long p, int HW, int lr, int lq) {
   typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+  const int col = lr & 7;
+  float R[3];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
-    const f16x4 h = {(_Float16)acc[rt][0], (_Float16)acc[rt][1], (_Float16)acc[rt][2], (_Float16)acc[rt][3]};
-    *reinterpret_cast<f16x4*>(zrow + rt * 16 + lq * 4) = h;
+  for (int o = 0; o < 3; ++o) {
+    const float l = zp_from_left(acc[o][0]), r = zp_from_right(acc[o][2]);
+    R[o] = ((col != 0 ? l : 0.f) + acc[o][1]) + (col != 7 ? r : 0.f);
+  }
+  if (lq < 3) {
+    *reinterpret_cast<f16x4*>(zimg + p * kZrR + lq * 4) = f16x4{(_Float16)R[0], (_Float16)R[1], (_Float16)R[2], 0};
+    _Float16* e = zimg + (long)HW * kZrR + (p >> 3) * kZrE + lq * 4;
+    if (col == 0)
+      *reinterpret_cast<f16x4*>(e) = f16x4{(_Float16)acc[0][2], (_Float16)acc[1][2], (_Float16)acc[2][2], 0};
+    if (col == 7)
+      *reinterpret_cast<f16x4*>(e + 12) = f16x4{(_Float16)acc[0][0], (_Float16)acc[1][0], (_Float16)acc[2][0], 0};
   }
 }
+// the same from both K halves' bf16 outputs (xf[sh] = channels 32 sh + 8 lq .. +7 of pixel lr)
+template <typename T>
+GHOST_DEV void zp_store(const T* __restrict__ W, const v8_t<T> (&xf)[2], _Float16* __restrict__ zimg, long p, int HW,
+                        int lr, int lq) {
+  f32x4 acc[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) zp_mfma_half(W, xf[ks], ks, acc, lr, lq);
+  zp_store_acc(acc, zimg, p, HW, lr, lq);
+}
 
+// projection row 9 o + 3 dy + dx <- the packed narrow-conv row (dy * 3 + dx) * 3 + o (pack_conv3x3_narrow)
 template <typename T, int L, int ZPM, int NT>
 GHOST_DEV void zp_stage_weights(const AadV3ArgsT<T>& a, T* s_wz, int tid) {
   if constexpr (ZPM != 0) {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
       if (!((ZPM >> l) & 1)) continue;
-      for (int idx = tid; idx < 32 * 8; idx += NT) {
+      for (int idx = tid; idx < kZpRows * 8; idx += NT) {
         const int row = idx >> 3, kc = idx & 7;
-        *reinterpret_cast<u32x4*>(&s_wz[sw64(zp_slot<ZPM>(l) * 32 + row, kc * 8)]) =
-            *reinterpret_cast<const u32x4*>(a.zw[l] + (long)row * a.zwld + kc * 8);
+        const int o = row / 9, t = row - o * 9;   // row 9 o + t, t = dy * 3 + dx
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (row < 27) v = *reinterpret_cast<const u32x4*>(a.zw[l] + (long)(t * 3 + o) * a.zwld + kc * 8);
+        *reinterpret_cast<u32x4*>(&s_wz[zp_slot<ZPM>(l) * kZpRows * ZLD + sw64(row, kc * 8)]) = v;   // as the reads
       }
     }
   }
@@ -147,7 +166,7 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
   __shared__ float s_k[L];                                        // sum_c wh * (-mu * rstd)
   __shared__ __attribute__((aligned(16))) float s_gi[L * C];
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
-  __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
+  __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * kZpRows * ZLD : 8];
 
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, lr = lane & 15, lq = lane >> 4;
   const int mrow = (lr & 3) == 3 ? 0 : (lr & 3);   // mask A row: part lr & 3 of the split (row 3 repeats hi)
@@ -316,7 +335,8 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
         }
       }
       if (ZPM && ((ZPM >> l) & 1))
-        zp_store(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, reinterpret_cast<_Float16*>(a.out[l]) + p * 32, lr, lq);
+        zp_store(s_wz + zp_slot<ZPM>(l) * kZpRows * ZLD, xf, reinterpret_cast<_Float16*>(a.out[l]) + b * zr_image(a.HW),
+                 p - (long)b * a.HW, a.HW, lr, lq);
     }
   }
 }
@@ -381,7 +401,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hA[kWaves * SLOT_B];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hB[kWaves * SLOT_B];
-  __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
+  __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * kZpRows * ZLD : 8];
 
   // wid through readfirstlane: tile indices and everything derived from them are wave-uniform (SGPRs),
   // so the per-tile address arithmetic runs on the scalar unit and the VALU keeps only lane offsets
@@ -533,7 +553,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
     for (int l = 0; l < L; ++l) {
       asm volatile("" ::: "memory");
       const T* W = s_w + l * 128 * WLD;
-      f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      f32x4 zacc[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int sh = 0; sh < 2; ++sh) {
         asm volatile("" ::: "memory");
@@ -580,12 +600,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))
           v8_t<T> xf;
 #pragma unroll
           for (int e = 0; e < 8; ++e) xf[e] = (T)o[e];
-          zp_mfma_half(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, sh, zacc, lr, lq);
+          zp_mfma_half(s_wz + zp_slot<ZPM>(l) * kZpRows * ZLD, xf, sh, zacc, lr, lq);
         } else {
           store16_f(a.out[l] + p0 * a.ldo[l] + (lr * a.ldo[l] + c0), o);
         }
       }
-      if (ZPM && ((ZPM >> l) & 1)) zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + (p0 + lr) * 32, lq);
+      if (ZPM && ((ZPM >> l) & 1))
+        zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + b * zr_image(a.HW), p0 + lr - (long)b * a.HW, a.HW,
+                     lr, lq);
     }
   };
 
@@ -692,7 +714,7 @@ GHOST_DEV void aad_v5_body(const AadV3ArgsT<T>& a) {
   __shared__ __attribute__((aligned(16))) float s_bi[L * C];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hA[NW * SLOT_B];
   __shared__ __attribute__((aligned(1024))) unsigned char s_hB[NBUF == 2 ? NW * SLOT_B : 16];
-  __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * 32 * ZLD : 8];
+  __shared__ __attribute__((aligned(16))) T s_wz[ZPM ? zp_nlayers<ZPM>() * kZpRows * ZLD : 8];
   // ASMW: each wave's z_attr tile (16 pixels x CA channels), single-buffered: read at the top of tile i, then
   // refilled with tile i+1's by DMA
   constexpr int ZSLOT_B = 16 * CA * 2;
@@ -978,7 +1000,7 @@ GHOST_DEV void aad_v5_body(const AadV3ArgsT<T>& a) {
     }
     // layer l's 32 channels (ct, sh) = hs2 of the lane's pixel: the GEMM rows, the blend, the store (or the tap
     // partials); h2[k] = hh of channels c0 + 2k, c0 + 2k + 1
-    auto layer_half = [&](const int l, const int hs2, const f32x2 (&h2)[4], f32x4 (&zacc)[2]) -> u32x4 {
+    auto layer_half = [&](const int l, const int hs2, const f32x2 (&h2)[4], f32x4 (&zacc)[3]) -> u32x4 {
       const int ct = hs2 >> 1, sh = hs2 & 1;
       const T* Wt = s_w + (l * CT + ct) * 128 * WLD;
       if constexpr (CT == 1) asm volatile("" ::: "memory");
@@ -1027,7 +1049,7 @@ GHOST_DEV void aad_v5_body(const AadV3ArgsT<T>& a) {
       if (ZPM && ((ZPM >> l) & 1)) {
         v8_t<T> xf;
         __builtin_memcpy(&xf, &ow, 16);
-        zp_mfma_half(s_wz + zp_slot<ZPM>(l) * 32 * ZLD, xf, sh, zacc, lr, lq);
+        zp_mfma_half(s_wz + zp_slot<ZPM>(l) * kZpRows * ZLD, xf, sh, zacc, lr, lq);
       }
       return ow;
     };
@@ -1043,7 +1065,7 @@ GHOST_DEV void aad_v5_body(const AadV3ArgsT<T>& a) {
 #pragma unroll
       for (int l = 0; l < L; ++l) {
         asm volatile("" ::: "memory");
-        f32x4 zacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+        f32x4 zacc[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
         u32x4 ow[2];
 #pragma unroll
         for (int sh = 0; sh < 2; ++sh) {
@@ -1054,7 +1076,7 @@ GHOST_DEV void aad_v5_body(const AadV3ArgsT<T>& a) {
 #ifdef GHOST_TUNING
           if (a.v5_flags & 8) continue;   // (tuning build, bit 3) no tap-partial stores: what they cost
 #endif
-          zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + pimg * 32 + p * 32, lq);
+          zp_store_acc(zacc, reinterpret_cast<_Float16*>(a.out[l]) + b * zr_image(a.HW), p, a.HW, lr, lq);
         } else {
           store_rows(l, 0, ow[0], ow[1]);
         }
@@ -1062,7 +1084,7 @@ GHOST_DEV void aad_v5_body(const AadV3ArgsT<T>& a) {
     } else {
       // C = 128: channel-tile-major, both layers per 64-channel tile, so a tile's hh (16 registers) is computed
       // once for both layers
-      f32x4 zacc[2];
+      f32x4 zacc[3];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         asm volatile("" ::: "memory");
@@ -1378,66 +1400,39 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// AADBlk8's output conv from the tap partials: an 8 x 32 output tile per workgroup; its 10 x 34 halo of
-// zh + zx (fp16 -> fp32, summed once per halo pixel) in LDS, then one output pixel per thread gathers
-// its nine taps: the gather and epilogue of conv3x3_narrow_kernel (conv_narrow.hip), whose LDS Z the
-// producers now write (tanh; BGR uint8 of faceshifter_run.py:20-21)
+// AADBlk8's output conv from the tap partials (tap_rows.h): one output pixel per thread sums the row sums of
+// the three source rows of both producers' buffers (zh: the h path, zx: last_add_block's x') plus the
+// segment-end terms at columns 8j - 1 / 8j, then tanh and the BGR uint8 copy of faceshifter_run.py:20-21.
+// Every row-sum slot is read by exactly one output pixel; a workgroup takes an 8 x 32 tile so the slots of
+// one 128-byte line are read by neighbouring rows of the same workgroup, and consecutive tiles share an XCD.
 // ---------------------------------------------------------------------------------------------
 namespace {
-constexpr int TS_TH = 16, TS_TW = 32, TS_HW = TS_TW + 2, TS_HP = (TS_TH + 2) * TS_HW, TS_LD = 29;
-constexpr int TS_ITEMS = TS_HP * 4, TS_PER = (TS_ITEMS + 511) / 512;   // (halo pixel, 16-byte chunk) per thread
+constexpr int TS_TH = 8, TS_TW = 32;
 }
 
 template <typename T>
-__global__ void __launch_bounds__(512) tap_sum3x3_kernel(const _Float16* __restrict__ zh, const _Float16* __restrict__ zx,
+__global__ void __launch_bounds__(256) tap_sum3x3_kernel(const _Float16* __restrict__ zh, const _Float16* __restrict__ zx,
                                                          int H, int W, T* __restrict__ y, int ldy,
                                                          uint8_t* __restrict__ u8) {
-  __shared__ float Z[TS_HP * TS_LD];
   const int tid = threadIdx.x;
-  const int tiles_x = W / TS_TW, tiles_y = H / TS_TH;
-  const int b = blockIdx.x / (tiles_x * tiles_y);
-  const int r = blockIdx.x - b * tiles_x * tiles_y;
-  const int y0 = (r / tiles_x) * TS_TH, x0 = (r % tiles_x) * TS_TW;
-  const long img = (long)b * H * W;
-  typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-  // halo pixel p, 16-byte chunk j (Z values 8j .. 8j+7; chunk 3 holds 24..31, of which 24..26 are used):
-  // every load of the thread issued before the first is used
-  f16x8 va[TS_PER], vc[TS_PER];
-#pragma unroll
-  for (int u = 0; u < TS_PER; ++u) {
-    const int i = tid + u * 512;
-    const int p = i >> 2, j = i & 3;
-    const int hy = p / TS_HW, hx = p - hy * TS_HW;
-    const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
-    const bool ok = i < TS_ITEMS && iy >= 0 && iy < H && ix >= 0 && ix < W;
-    const long q = (img + (long)(ok ? iy : 0) * W + (ok ? ix : 0)) * 32 + j * 8;
-    va[u] = ok ? *reinterpret_cast<const f16x8*>(zh + q) : f16x8{};
-    vc[u] = ok ? *reinterpret_cast<const f16x8*>(zx + q) : f16x8{};
-  }
-#pragma unroll
-  for (int u = 0; u < TS_PER; ++u) {
-    const int i = tid + u * 512;
-    if (i >= TS_ITEMS) break;
-    const int p = i >> 2, j = i & 3;
-    const int ne = j == 3 ? 3 : 8;
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      if (e < ne) Z[p * TS_LD + j * 8 + e] = (float)va[u][e] + (float)vc[u][e];
-  }
-  __syncthreads();
-  const int oy = tid / TS_TW, ox = tid - oy * TS_TW;
-  const long q = img + (long)(y0 + oy) * W + (x0 + ox);
+  const int tiles_x = W / TS_TW, tiles = tiles_x * (H / TS_TH);
+  // XCD-aware: workgroup id i runs on XCD i % 8; consecutive logical tiles go to one XCD (grid % 8 == 0)
+  const int nb = (int)gridDim.x;
+  const int bid = (nb & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3);
+  const int b = bid / tiles;
+  const int r = bid - b * tiles;
+  const int oy = (r / tiles_x) * TS_TH + tid / TS_TW, ox = (r % tiles_x) * TS_TW + (tid & (TS_TW - 1));
+  const long zi = (long)b * zr_image(H * W);
+  float s[3] = {0.f, 0.f, 0.f};
+  zr_gather(zh + zi, H, W, oy, ox, s);
+  zr_gather(zx + zi, H, W, oy, ox, s);
+  const long q = (long)b * H * W + (long)oy * W + ox;
 #pragma unroll
   for (int o = 0; o < 3; ++o) {
-    float s = 0.f;
-#pragma unroll
-    for (int ty = 0; ty < 3; ++ty)
-#pragma unroll
-      for (int tx = 0; tx < 3; ++tx) s += Z[((oy + ty) * TS_HW + ox + tx) * TS_LD + (ty * 3 + tx) * 3 + o];
-    s = tanhf(s);
-    y[q * ldy + o] = (T)s;
+    const float v = tanhf(s[o]);
+    y[q * ldy + o] = (T)v;
     if (u8) {
-      const float t = (s * 0.5f + 0.5f) * 255.0f;   // faceshifter_run.py:20-21
+      const float t = (v * 0.5f + 0.5f) * 255.0f;   // faceshifter_run.py:20-21
       u8[q * 3 + (2 - o)] = (uint8_t)(int)t;
     }
   }
@@ -1448,10 +1443,10 @@ int tap_sum3x3(int dt, const void* zh, const void* zx, int B, int H, int W, void
   if (H % TS_TH || W % TS_TW || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16 || !is16(dt)) return -1;
   const dim3 g((unsigned)(B * (H / TS_TH) * (W / TS_TW)));
   if (dt == GHOST_F16)
-    hipLaunchKernelGGL(tap_sum3x3_kernel<_Float16>, g, dim3(512), 0, s, (const _Float16*)zh, (const _Float16*)zx, H, W,
+    hipLaunchKernelGGL(tap_sum3x3_kernel<_Float16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, H, W,
                        (_Float16*)y, ldy, u8);
   else
-    hipLaunchKernelGGL(tap_sum3x3_kernel<bf16>, g, dim3(512), 0, s, (const _Float16*)zh, (const _Float16*)zx, H, W,
+    hipLaunchKernelGGL(tap_sum3x3_kernel<bf16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, H, W,
                        (bf16*)y, ldy, u8);
   return (int)hipGetLastError();
 }

@@ -24,6 +24,7 @@
 #include "conv_narrow.h"
 #include "ghost_common.h"
 #include "ops.h"
+#include "tap_rows.h"
 
 using namespace ghost;
 
@@ -503,7 +504,7 @@ struct AadOut {
   int id_off;
   void* out;
   int ldo;
-  const void* zw = nullptr;   // tap partials (aad_v3.h): out is then the [P][32] fp16 partial buffer
+  const void* zw = nullptr;   // tap partials (aad_v3.h): out is then the row-summed buffer of tap_rows.h
   int zwld = 0;
 };
 
@@ -737,8 +738,8 @@ void generator(Ctx& c, int B, const void* const attr[8], GenIn gin, void* y_out,
                        ? h->opt[GHOST_AEI_OPT_TAP_PARTIALS] : 0;
     const char* wn = zp ? (const char*)c.W(blk + ".conv" + std::to_string(nb - 1) + ".wn") : nullptr;
     const int wnld = rup(2 * cin, 32);
-    void* zh = zp ? c.alloc(P * 32 * 2) : nullptr;
-    void* zx = zp == 2 ? c.alloc(P * 32 * 2) : nullptr;
+    void* zh = zp ? c.alloc(P * kZrPerPixel * 2) : nullptr;   // row-summed partials (tap_rows.h)
+    void* zx = zp == 2 ? c.alloc(P * kZrPerPixel * 2) : nullptr;
     void* xq = zp == 1 ? c.alloc(P * cin * es) : nullptr;   // x' alone (the narrow conv contracts it)
     void* cat = (split && !zp) ? c.alloc(P * 2 * cin * es) : nullptr;
     const void* x = m;

@@ -9,6 +9,7 @@
 // Epilogue: optional residual, tanh, and the BGR uint8 copy of faceshifter_run.py:20-21.
 #include "conv_narrow.h"
 #include "ghost_common.h"
+#include "tap_rows.h"
 
 namespace ghost {
 
@@ -26,7 +27,7 @@ struct NarrowArgs {
   const void* res;
   void* y;
   uint8_t* u8;
-  const _Float16* zadd;   // optional [B*H*W][32] fp16 tap partials of other input channels, added to Z
+  const _Float16* zadd;   // optional tap partials of other input channels (tap_rows.h), added to the sums
   int H, W, Cin, ldx, Kpad, ldy, ldres, NO, tanh_out;
 };
 
@@ -128,29 +129,19 @@ __global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const NarrowArgs a)
     }
   }
   __syncthreads();
-  if (a.zadd) {   // tap partials of the channels a producer already contracted (AADBlk8's h path, aad_v3.h)
-    for (int i = tid; i < HP * 4; i += 256) {
-      const int p = i >> 2, j = i & 3;
-      const int hy = p / HW_, hx = p - hy * HW_;
-      const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
-      if (iy < 0 || iy >= a.H || ix < 0 || ix >= a.W) continue;
-      typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
-      const f16x8 z = *reinterpret_cast<const f16x8*>(a.zadd + (img + (long)iy * a.W + ix) * 32 + j * 8);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Z[p * ZLD + j * 8 + e] += (float)z[e];
-    }
-    __syncthreads();
-  }
-
   // gather: one output pixel per thread
   const int oy = tid / TW, ox = tid - oy * TW;
   const long q = img + (long)(y0 + oy) * a.W + (x0 + ox);
+  // tap partials of the channels a producer already contracted (AADBlk8's h path; row sums, tap_rows.h)
+  float zs[3] = {0.f, 0.f, 0.f};
+  if (a.zadd) zr_gather(a.zadd + (long)b * zr_image(a.H * a.W), a.H, a.W, y0 + oy, x0 + ox, zs);
   for (int o = 0; o < a.NO; ++o) {
     float s = 0.f;
 #pragma unroll
     for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
       for (int tx = 0; tx < 3; ++tx) s += Z[((oy + ty) * HW_ + ox + tx) * ZLD + (ty * 3 + tx) * a.NO + o];
+    s += zs[o < 3 ? o : 0];
     if (a.res) s += to_f(reinterpret_cast<const T*>(a.res)[q * a.ldres + o]);
     if (a.tanh_out) s = tanhf(s);
     reinterpret_cast<T*>(a.y)[q * a.ldy + o] = from_f<T>(s);
@@ -170,7 +161,7 @@ int conv3x3_narrow(int dt, const void* x, int B, int H, int W, int Cin, int ldx,
                    const void* res, int ldres, int tanh_out, void* y, int ldy, uint8_t* u8, hipStream_t s,
                    const void* zadd) {
   if (!conv3x3_narrow_supported(dt, H, W, Cin, ldx, NO) || (uintptr_t)x % 16 || (uintptr_t)w_narrow % 16) return -1;
-  if (zadd && (uintptr_t)zadd % 16) return -1;
+  if (zadd && ((uintptr_t)zadd % 16 || NO != 3 || W % 8)) return -1;
   NarrowArgs a{x, w_narrow, res, y, u8, (const _Float16*)zadd, H, W, Cin, ldx, Kpad, ldy, ldres, NO, tanh_out};
   dim3 grid((unsigned)(B * (H / TH) * (W / TW)));
 #define GHOST_NARROW(T)                                                   \

@@ -112,13 +112,14 @@ int ghost_aei_swap_u8_indexed(ghost_aei* h, const uint8_t* crops, int64_t crop_b
  *                                    ordering seen by the caller is unchanged (0: one stream; batches of
  *                                    fewer than 8 frames always run on one stream).  Same results.
  *   GHOST_AEI_OPT_TAP_PARTIALS (2):  bf16, C = 64 output block (AADBlk8): the 3x3 conv to 3 channels is
- *                                    contracted in its producers: each AADLayer that feeds it writes the 27
- *                                    per-tap partial sums of its channels (fp16, 32 per pixel) instead of its
- *                                    64 bf16 channels, and a gather kernel sums the nine taps (+ tanh, uint8).
+ *                                    contracted in its producers: each AADLayer that feeds it writes the
+ *                                    per-tap partial sums of its channels, pre-summed along 8-pixel row
+ *                                    segments (fp16, 15 per pixel) instead of its 64 bf16 channels, and a
+ *                                    gather kernel sums three rows of them (+ tanh, uint8).
  *                                    2: both the h path and last_add_block's x'; 1: the h path only (x' is
  *                                    written and the narrow conv contracts it); 0: neither.  The partials
- *                                    are rounded to fp16 once (the extra rounding the bf16-storage
- *                                    emulation of oracle/aei_ref.py models).
+ *                                    are rounded to fp16 once per row sum (the extra rounding the
+ *                                    bf16-storage emulation of oracle/aei_ref.py models).
  *   GHOST_AEI_OPT_FUSE_REDUCE (1):   split-K GEMMs with small partial tiles and the InstanceNorm statistics
  *                                    passes reduce their partials in the last workgroup to finish (arrival
  *                                    counters in the workspace, zeroed once per call) instead of a second

@@ -418,17 +418,30 @@ def up1_bf16_storage(z_id, p):
 
 
 def _tap_conv3x3(a, w, round16):
-    """conv2d(a, w, padding=1) for 3 output channels as the runtime's tap-partial path computes it: per tap
-    (ky, kx) the partial sum Z_t = sum_c w[:, c, ky, kx] * a_c at every source pixel (fp32 over bf16
-    operands), stored in fp16 when round16, then out[q] = sum_t Z_t[q + (ky - 1, kx - 1)] (zero outside)."""
+    """conv2d(a, w, padding=1) for 3 output channels as the runtime's tap-partial path computes it
+    (ghost_amd/csrc/tap_rows.h): per tap (dy, dx) the partial sum Z = sum_c w[:, c, dy, dx] * a_c at every
+    source pixel (fp32 over bf16 operands).  round16 False: out = sum over taps, unrounded (the narrow conv's
+    own channels).  round16 True: the producer's fp16 row sums inside 8-column segments,
+    R_dy(x) = (Z_{dy,0}(x-1) + Z_{dy,1}(x)) + Z_{dy,2}(x+1) (neighbours across a segment end left out), plus the
+    fp16 segment-end terms at columns 8j - 1 (Z_{dy,2} of column 8j) and 8j (Z_{dy,0} of column 8j - 1);
+    out(y, x) = sum_dy of those at source row y + dy - 1 (zero outside)."""
     H, W = a.shape[-2:]
+    z = [[torch.einsum("bchw,oc->bohw", a, w[:, :, dy, dx]) for dx in range(3)] for dy in range(3)]
     out = torch.zeros(a.shape[0], w.shape[0], H, W)
-    for ky in range(3):
-        for kx in range(3):
-            zt = torch.einsum("bchw,oc->bohw", a, w[:, :, ky, kx])
-            if round16:
-                zt = zt.half().float()
-            out = out + F.pad(zt, (1, 1, 1, 1))[:, :, ky:ky + H, kx:kx + W]
+    if not round16:
+        for dy in range(3):
+            for dx in range(3):
+                out = out + F.pad(z[dy][dx], (1, 1, 1, 1))[:, :, dy:dy + H, dx:dx + W]
+        return out
+    col = torch.arange(W) % 8
+    for dy in range(3):
+        from_left = F.pad(z[dy][0], (1, 0))[..., :W]     # Z_{dy,0}(x - 1), zero at x = 0
+        from_right = F.pad(z[dy][2], (0, 1))[..., 1:]    # Z_{dy,2}(x + 1), zero at x = W - 1
+        zero = torch.zeros(())
+        r = ((torch.where(col != 0, from_left, zero) + z[dy][1]) + torch.where(col != 7, from_right, zero))
+        ends = torch.where(col == 7, from_right.half().float(), torch.where(col == 0, from_left.half().float(), zero))
+        c = r.half().float() + ends
+        out = out + F.pad(c, (0, 0, 1, 1))[:, :, dy:dy + H, :]
     return out
 
 

@@ -176,12 +176,12 @@ def test_product_refuses_cpu_tensors():
 
 
 def test_bench_roofline_bytes_follow_the_stored_outputs():
-    """bench.py's minimum bytes of the aad_v4 launch: a tap-partial output is 32 fp16 per pixel, not 64 bf16."""
+    """bench.py's minimum bytes of the aad_v4 launch: a tap-partial output is 15 fp16 per pixel, not 64 bf16."""
     import bench
     full, n0, z0 = bench.aad_v4_min_bytes(64, 64, 2, 2, 0)
     assert (n0, z0) == (0, 0) and full == 64 * (128 * 128 * 64 + 65536 * 64 * 3) * 2.0 == 1744830464.0
     part, n2, z2 = bench.aad_v4_min_bytes(64, 64, 2, 2, 2)
-    assert (n2, z2) == (1, 2) and full - part == 64 * 65536 * 32 * 2.0
+    assert (n2, z2) == (1, 2) and full - part == 64 * 65536 * (64 - 15) * 2.0
     assert bench.aad_v4_min_bytes(64, 64, 2, 2, 1)[1:] == (0, 0)          # mode 1: partials in the later layer
     assert bench.aad_v4_min_bytes(64, 32, 2, 1, 2)[1:] == (2, 3)          # nb = 1: both layers feed the RGB conv
     assert bench.aad_v4_min_bytes(64, 32, 2, 1, 1)[1:] == (1, 1)
