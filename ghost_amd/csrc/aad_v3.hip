@@ -55,11 +55,12 @@ struct AadV3ArgsT {
 static constexpr int kWaves = 8;
 
 // tap partials (tap_rows.h): MFMA row tile o, row 4 dy + dx holds the projection of tap (dy, dx) to channel o
-// (dy, dx < 3; the other rows zero), so a lane (pixel lr, lq = dy) ends with the three dx of each o; the lane
-// then sums its row neighbours inside the 8-column segment and stores fp16 row sums plus the segment-end
-// terms.  LDS holds only the 27 real rows, 9 o + 3 dy + dx, and one zero row that the others read.
+// (dy, dx < 3), so a lane (pixel lr, lq = dy) ends with the three dx of each o; the lane then sums its row
+// neighbours inside the 8-column segment and stores fp16 row sums plus the segment-end terms.  LDS holds the
+// 27 real rows, 9 o + 3 dy + dx; the A rows with dy or dx = 3 re-read a real row of their 8-lane group (the
+// same address: a broadcast, no bank conflict) and produce values nothing stores.
 constexpr int ZLD = 64;
-constexpr int kZpRows = 28;
+constexpr int kZpRows = 27;
 // element offset of (row, k) in an unpadded image of 64-element (128-byte) rows with the 16-byte chunks XOR-
 // swizzled by row & 7: the ds_read_b128 of rows 16 rt + lr, chunk 4 ks + lq is conflict-free in every 16-lane
 // group (the +8-element padding it replaces was 2-way in half the groups and cost 1 KB per 64 rows)
@@ -86,12 +87,11 @@ constexpr int zp_nlayers() { return (ZPM & 1) + ((ZPM >> 1) & 1); }
 // one K half (K step ks = the half sh just computed) into the three row tiles: 12 accumulator registers live
 template <typename T>
 GHOST_DEV void zp_mfma_half(const T* __restrict__ W, const v8_t<T>& xf, int ks, f32x4 (&acc)[3], int lr, int lq) {
-  const int dy = lr >> 2, dx = lr & 3;
-  const bool real = dy < 3 && dx < 3;   // else the zero row 27
+  const int dy = min(lr >> 2, 2), dx = min(lr & 3, 2);
 #pragma unroll
   for (int rt = 0; rt < 3; ++rt) {
     asm volatile("" ::: "memory");   // the projection rows are re-read per use, not held across the tile loop
-    const int row = real ? rt * 9 + dy * 3 + dx : 27;
+    const int row = rt * 9 + dy * 3 + dx;
     const v8_t<T> wf = *reinterpret_cast<const v8_t<T>*>(&W[sw64(row, ks * 32 + lq * 8)]);
     acc[rt] = mfma16x16x32<T>(wf, xf, acc[rt]);
   }
@@ -141,8 +141,7 @@ GHOST_DEV void zp_stage_weights(const AadV3ArgsT<T>& a, T* s_wz, int tid) {
       for (int idx = tid; idx < kZpRows * 8; idx += NT) {
         const int row = idx >> 3, kc = idx & 7;
         const int o = row / 9, t = row - o * 9;   // row 9 o + t, t = dy * 3 + dx
-        u32x4 v = {0u, 0u, 0u, 0u};
-        if (row < 27) v = *reinterpret_cast<const u32x4*>(a.zw[l] + (long)(t * 3 + o) * a.zwld + kc * 8);
+        const u32x4 v = *reinterpret_cast<const u32x4*>(a.zw[l] + (long)(t * 3 + o) * a.zwld + kc * 8);
         *reinterpret_cast<u32x4*>(&s_wz[zp_slot<ZPM>(l) * kZpRows * ZLD + sw64(row, kc * 8)]) = v;   // as the reads
       }
     }
@@ -346,6 +345,12 @@ GHOST_DEV void aad_v3_body(const AadV3ArgsT<T>& a) {
 template <typename T, int C, int CA, int L, bool UP, int ZPM = 0>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) aad_v3_kernel(const AadV3ArgsT<T> a) {
   aad_v3_body<T, C, CA, L, UP, kWaves, ZPM>(a);
+}
+// one layer writing tap partials (AADBlk8's h path): held to 6 waves per SIMD (<= 80 VGPRs; the compiler's
+// own allocation is 86, 5 waves), three 512-thread workgroups per CU for this streaming pass
+template <typename T, int CA>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6, 8))) aad_v3_zp1_kernel(const AadV3ArgsT<T> a) {
+  aad_v3_body<T, 64, CA, 1, false, kWaves, 1>(a);
 }
 template <typename T, int C, int CA, int L, bool UP>
 __global__ void __launch_bounds__(512) aad_v3_wide_kernel(const AadV3ArgsT<T> a) {
@@ -1357,12 +1362,19 @@ static int aad_v3_t(const AadV3Desc& d, hipStream_t s) {
   }
   }
   if (zpm) {   // the non-upsampled forms with tap partials (AADBlk8's last add_block; fuse_upsample off)
+    if (d.C == 64 && d.L == 1 && !up && zpm == 1 && (d.Ca == 64 || d.Ca == 32)) {
+      if (d.Ca == 64)
+        hipLaunchKernelGGL((aad_v3_zp1_kernel<T, 64>), grid, dim3(kWaves * 64), 0, s, a);
+      else
+        hipLaunchKernelGGL((aad_v3_zp1_kernel<T, 32>), grid, dim3(kWaves * 64), 0, s, a);
+      return (int)hipGetLastError();
+    }
 #define GHOST_V3Z(ca, l, zm)                                                                     \
     if (d.C == 64 && d.Ca == ca && d.L == l && !up && zpm == zm) {                               \
       hipLaunchKernelGGL((aad_v3_kernel<T, 64, ca, l, false, zm>), grid, dim3(kWaves * 64), 0, s, a); \
       return (int)hipGetLastError();                                                             \
     }
-    GHOST_V3Z(64, 1, 1) GHOST_V3Z(32, 1, 1) GHOST_V3Z(64, 2, 1) GHOST_V3Z(32, 2, 1) GHOST_V3Z(64, 2, 2)
+    GHOST_V3Z(64, 2, 1) GHOST_V3Z(32, 2, 1) GHOST_V3Z(64, 2, 2)
     GHOST_V3Z(32, 2, 2) GHOST_V3Z(64, 2, 3) GHOST_V3Z(32, 2, 3)
 #undef GHOST_V3Z
     return -1;
