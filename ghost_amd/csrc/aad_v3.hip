@@ -1412,53 +1412,95 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// AADBlk8's output conv from the tap partials (tap_rows.h): one output pixel per thread sums the row sums of
-// the three source rows of both producers' buffers (zh: the h path, zx: last_add_block's x') plus the
-// segment-end terms at columns 8j - 1 / 8j, then tanh and the BGR uint8 copy of faceshifter_run.py:20-21.
-// Every row-sum slot is read by exactly one output pixel; a workgroup takes an 8 x 32 tile so the slots of
-// one 128-byte line are read by neighbouring rows of the same workgroup, and consecutive tiles share an XCD.
+// AADBlk8's output conv from the tap partials (tap_rows.h): each thread takes four consecutive output pixels,
+// sums the row sums of the three source rows of both producers' buffers (zh: the h path, zx: last_add_block's
+// x') plus the segment-end terms at columns 8j - 1 / 8j, then tanh, and stores the 4 x 3 outputs and their BGR
+// uint8 copy (faceshifter_run.py:20-21) as whole dwords.  Every row-sum slot is read by exactly one output
+// pixel; consecutive 1024-pixel blocks share an XCD, so the three output rows that read one source row meet it
+// in the same L2.
 // ---------------------------------------------------------------------------------------------
-namespace {
-constexpr int TS_TH = 8, TS_TW = 32;
+GHOST_DEV void zr_gather4(const _Float16* __restrict__ z, int H, int W, int y, int x0, float (&s)[4][3]) {
+  typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+  const _Float16* __restrict__ e = z + (long)H * W * kZrR;
+  const bool first = (x0 & 7) == 0 && x0 > 0, last = (x0 & 7) == 4 && x0 + 4 < W;   // pixel 0 / pixel 3 at a segment end
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int yy = y + dy - 1;
+    if (yy < 0 || yy >= H) continue;
+    const long ps = (long)yy * W + x0;
+    f16x4 r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = *reinterpret_cast<const f16x4*>(z + (ps + k) * kZrR + dy * 4);
+    f16x4 cf = {0, 0, 0, 0}, cl = {0, 0, 0, 0};
+    if (first) cf = *reinterpret_cast<const f16x4*>(e + ((ps - 1) >> 3) * kZrE + 12 + dy * 4);   // previous E_right
+    if (last) cl = *reinterpret_cast<const f16x4*>(e + ((ps + 4) >> 3) * kZrE + dy * 4);         // next E_left
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      s[0][o] += (float)r[0][o] + (float)cf[o];
+      s[1][o] += (float)r[1][o];
+      s[2][o] += (float)r[2][o];
+      s[3][o] += (float)r[3][o] + (float)cl[o];
+    }
+  }
 }
 
 template <typename T>
 __global__ void __launch_bounds__(256) tap_sum3x3_kernel(const _Float16* __restrict__ zh, const _Float16* __restrict__ zx,
-                                                         int H, int W, T* __restrict__ y, int ldy,
+                                                         int B, int H, int W, T* __restrict__ y, int ldy,
                                                          uint8_t* __restrict__ u8) {
-  const int tid = threadIdx.x;
-  const int tiles_x = W / TS_TW, tiles = tiles_x * (H / TS_TH);
-  // XCD-aware: workgroup id i runs on XCD i % 8; consecutive logical tiles go to one XCD (grid % 8 == 0)
+  // XCD-aware: workgroup id i runs on XCD i % 8; consecutive logical blocks go to one XCD (grid % 8 == 0)
   const int nb = (int)gridDim.x;
   const int bid = (nb & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3);
-  const int b = bid / tiles;
-  const int r = bid - b * tiles;
-  const int oy = (r / tiles_x) * TS_TH + tid / TS_TW, ox = (r % tiles_x) * TS_TW + (tid & (TS_TW - 1));
+  const long g = (long)bid * 256 + threadIdx.x;   // group of 4 pixels
+  const int gpr = W / 4;
+  const long rowg = g / gpr;
+  if (rowg >= (long)B * H) return;
+  const int b = (int)(rowg / H), oy = (int)(rowg - (long)b * H), ox = (int)(g - rowg * gpr) * 4;
   const long zi = (long)b * zr_image(H * W);
-  float s[3] = {0.f, 0.f, 0.f};
-  zr_gather(zh + zi, H, W, oy, ox, s);
-  zr_gather(zx + zi, H, W, oy, ox, s);
-  const long q = (long)b * H * W + (long)oy * W + ox;
+  float s[4][3] = {};
+  zr_gather4(zh + zi, H, W, oy, ox, s);
+  zr_gather4(zx + zi, H, W, oy, ox, s);
+  const long q = rowg * W + ox;   // first output pixel
+  float v[12];
+  uint32_t c[3] = {0u, 0u, 0u};
 #pragma unroll
-  for (int o = 0; o < 3; ++o) {
-    const float v = tanhf(s[o]);
-    y[q * ldy + o] = (T)v;
-    if (u8) {
-      const float t = (v * 0.5f + 0.5f) * 255.0f;   // faceshifter_run.py:20-21
-      u8[q * 3 + (2 - o)] = (uint8_t)(int)t;
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      v[k * 3 + o] = tanhf(s[k][o]);
+      const float t = (v[k * 3 + o] * 0.5f + 0.5f) * 255.0f;   // faceshifter_run.py:20-21
+      const int bi = k * 3 + (2 - o);                            // BGR
+      c[bi >> 2] |= (uint32_t)(uint8_t)(int)t << ((bi & 3) * 8);
     }
+  if (ldy == 3) {   // 12 contiguous values: three 8-byte stores
+    typedef __attribute__((ext_vector_type(4))) T t4;
+    t4* yp = reinterpret_cast<t4*>(y + q * 3);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) yp[j] = t4{(T)v[4 * j], (T)v[4 * j + 1], (T)v[4 * j + 2], (T)v[4 * j + 3]};
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int o = 0; o < 3; ++o) y[(q + k) * ldy + o] = (T)v[k * 3 + o];
+  }
+  if (u8) {
+    uint32_t* up = reinterpret_cast<uint32_t*>(u8 + q * 3);   // 12 bytes at a multiple of 12: dword aligned
+#pragma unroll
+    for (int j = 0; j < 3; ++j) up[j] = c[j];
   }
 }
 
 int tap_sum3x3(int dt, const void* zh, const void* zx, int B, int H, int W, void* y, int ldy, uint8_t* u8,
                hipStream_t s) {
-  if (H % TS_TH || W % TS_TW || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16 || !is16(dt)) return -1;
-  const dim3 g((unsigned)(B * (H / TS_TH) * (W / TS_TW)));
+  if (W % 8 || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16 || (uintptr_t)y % 8 || (uintptr_t)u8 % 4 ||
+      !is16(dt))
+    return -1;
+  const dim3 g((unsigned)(((long)B * H * W / 4 + 255) / 256));
   if (dt == GHOST_F16)
-    hipLaunchKernelGGL(tap_sum3x3_kernel<_Float16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, H, W,
-                       (_Float16*)y, ldy, u8);
+    hipLaunchKernelGGL(tap_sum3x3_kernel<_Float16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, B, H,
+                       W, (_Float16*)y, ldy, u8);
   else
-    hipLaunchKernelGGL(tap_sum3x3_kernel<bf16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, H, W,
+    hipLaunchKernelGGL(tap_sum3x3_kernel<bf16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, B, H, W,
                        (bf16*)y, ldy, u8);
   return (int)hipGetLastError();
 }
