@@ -1447,7 +1447,7 @@ GHOST_DEV void zr_gather4(const _Float16* __restrict__ z, int H, int W, int y, i
 template <typename T>
 __global__ void __launch_bounds__(256) tap_sum3x3_kernel(const _Float16* __restrict__ zh, const _Float16* __restrict__ zx,
                                                          int B, int H, int W, T* __restrict__ y, int ldy,
-                                                         uint8_t* __restrict__ u8) {
+                                                         uint8_t* __restrict__ u8, int vec) {
   // XCD-aware: workgroup id i runs on XCD i % 8; consecutive logical blocks go to one XCD (grid % 8 == 0)
   const int nb = (int)gridDim.x;
   const int bid = (nb & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3);
@@ -1472,7 +1472,7 @@ __global__ void __launch_bounds__(256) tap_sum3x3_kernel(const _Float16* __restr
       const int bi = k * 3 + (2 - o);                            // BGR
       c[bi >> 2] |= (uint32_t)(uint8_t)(int)t << ((bi & 3) * 8);
     }
-  if (ldy == 3) {   // 12 contiguous values: three 8-byte stores
+  if (vec & 1) {   // ldy = 3, y 8-byte aligned: 12 contiguous values in three 8-byte stores
     typedef __attribute__((ext_vector_type(4))) T t4;
     t4* yp = reinterpret_cast<t4*>(y + q * 3);
 #pragma unroll
@@ -1483,25 +1483,28 @@ __global__ void __launch_bounds__(256) tap_sum3x3_kernel(const _Float16* __restr
 #pragma unroll
       for (int o = 0; o < 3; ++o) y[(q + k) * ldy + o] = (T)v[k * 3 + o];
   }
-  if (u8) {
-    uint32_t* up = reinterpret_cast<uint32_t*>(u8 + q * 3);   // 12 bytes at a multiple of 12: dword aligned
+  if (u8 && (vec & 2)) {
+    uint32_t* up = reinterpret_cast<uint32_t*>(u8 + q * 3);   // 12 bytes at a multiple of 12 from a dword base
 #pragma unroll
     for (int j = 0; j < 3; ++j) up[j] = c[j];
+  } else if (u8) {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) u8[q * 3 + j] = (uint8_t)(c[j >> 2] >> ((j & 3) * 8));
   }
 }
 
 int tap_sum3x3(int dt, const void* zh, const void* zx, int B, int H, int W, void* y, int ldy, uint8_t* u8,
                hipStream_t s) {
-  if (W % 8 || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16 || (uintptr_t)y % 8 || (uintptr_t)u8 % 4 ||
-      !is16(dt))
-    return -1;
+  if (W % 8 || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16 || !is16(dt)) return -1;
   const dim3 g((unsigned)(((long)B * H * W / 4 + 255) / 256));
+  // whole-dword stores where the caller's buffers allow them (an out= view may start anywhere)
+  const int vec = (ldy == 3 && (uintptr_t)y % 8 == 0 ? 1 : 0) | ((uintptr_t)u8 % 4 == 0 ? 2 : 0);
   if (dt == GHOST_F16)
     hipLaunchKernelGGL(tap_sum3x3_kernel<_Float16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, B, H,
-                       W, (_Float16*)y, ldy, u8);
+                       W, (_Float16*)y, ldy, u8, vec);
   else
     hipLaunchKernelGGL(tap_sum3x3_kernel<bf16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, B, H, W,
-                       (bf16*)y, ldy, u8);
+                       (bf16*)y, ldy, u8, vec);
   return (int)hipGetLastError();
 }
 

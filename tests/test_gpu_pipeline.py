@@ -215,6 +215,34 @@ def test_fused_reductions_are_bit_identical(lib, backbone, nb, dt, B, ts):
     assert torch.equal(res[0][2], res[1][2])
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_swap_into_unaligned_output_views(lib, dt):
+    """The RGB conv's gather (tap_sum3x3 over the row-summed tap partials) stores whole dwords only where the
+    caller's buffer allows: a uint8 out= view starting 1 byte into its storage gets the same bytes as a fresh
+    tensor, and forward's out_u8 likewise."""
+    G, _ = model("unet", 2, dt)
+    B = 3
+    xt, z = aei_ref.make_inputs(B, 37)
+    crops = torch.from_numpy(aei_ref.make_u8_crops(B, 37)).to(DEV)
+    ref = G.swap_u8(crops, z.to(DEV)).clone()
+    n = B * 256 * 256 * 3
+    for off in (1, 2, 4):
+        buf = torch.full((n + 8,), 7, dtype=torch.uint8, device=DEV)
+        view = buf[off:off + n].view(B, 256, 256, 3)
+        got = G.swap_u8(crops, z.to(DEV), out=view)
+        torch.cuda.synchronize()
+        assert got.data_ptr() == view.data_ptr()
+        assert torch.equal(got, ref), off
+        assert bool((buf[:off] == 7).all()) and bool((buf[off + n:] == 7).all()), off   # nothing outside the view
+    o0 = torch.empty(B, 256, 256, 3, dtype=torch.uint8, device=DEV)
+    Y0, _ = G(xt.to(DEV), z.to(DEV), out_u8=o0)
+    buf = torch.zeros(n + 4, dtype=torch.uint8, device=DEV)
+    o1 = buf[3:3 + n].view(B, 256, 256, 3)
+    Y1, _ = G(xt.to(DEV), z.to(DEV), out_u8=o1)
+    torch.cuda.synchronize()
+    assert torch.equal(Y0, Y1) and torch.equal(o0, o1)
+
+
 @pytest.mark.parametrize("B,nb,indexed", [(4, 5, False), (8, 5, True), (64, 4, True), (64, 3, False)])
 def test_gather_pipeline_two_batches_in_flight(lib, B, nb, indexed):
     """dp.GatherPipeline(streams=2) (bench.py's default): consecutive batches swapped on two pipeline streams at
