@@ -1445,6 +1445,9 @@ GHOST_DEV void zr_gather4(const _Float16* __restrict__ z, int H, int W, int y, i
 }
 
 template <typename T>
+GHOST_DEV void tap_out4(const float (&s)[4][3], long q, T* __restrict__ y, int ldy, uint8_t* __restrict__ u8, int vec);
+
+template <typename T>
 __global__ void __launch_bounds__(256) tap_sum3x3_kernel(const _Float16* __restrict__ zh, const _Float16* __restrict__ zx,
                                                          int B, int H, int W, T* __restrict__ y, int ldy,
                                                          uint8_t* __restrict__ u8, int vec) {
@@ -1460,7 +1463,13 @@ __global__ void __launch_bounds__(256) tap_sum3x3_kernel(const _Float16* __restr
   float s[4][3] = {};
   zr_gather4(zh + zi, H, W, oy, ox, s);
   zr_gather4(zx + zi, H, W, oy, ox, s);
-  const long q = rowg * W + ox;   // first output pixel
+  tap_out4(s, rowg * W + ox, y, ldy, u8, vec);
+}
+
+// four output pixels of one row from their sums: tanh, the 12 values, their BGR uint8 copy
+// (faceshifter_run.py:20-21), as whole dwords where the caller's buffers allow them (vec)
+template <typename T>
+GHOST_DEV void tap_out4(const float (&s)[4][3], long q, T* __restrict__ y, int ldy, uint8_t* __restrict__ u8, int vec) {
   float v[12];
   uint32_t c[3] = {0u, 0u, 0u};
 #pragma unroll
@@ -1493,12 +1502,105 @@ __global__ void __launch_bounds__(256) tap_sum3x3_kernel(const _Float16* __restr
   }
 }
 
+// one source row's contribution to the three output rows it feeds, for four pixels of one buffer: slot dy of
+// row s lands on output row s - dy + 1, so up[dy] += R_dy (+ the segment-end terms at pixels 0 / 3)
+GHOST_DEV void zr_row4(const _Float16* __restrict__ z, int H, int W, int s, int x0, float (&o2)[4][3],
+                       float (&o1)[4][3], float (&o0)[4][3]) {
+  typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+  typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+  const long ps = (long)s * W + x0;
+  f16x8_t r[6];   // the four pixels' R records: 48 fp16, 96 contiguous bytes
+#pragma unroll
+  for (int j = 0; j < 6; ++j) r[j] = *reinterpret_cast<const f16x8_t*>(z + ps * kZrR + j * 8);
+  const _Float16* __restrict__ e = z + (long)H * W * kZrR;
+  const bool first = (x0 & 7) == 0 && x0 > 0, last = (x0 & 7) == 4 && x0 + 4 < W;
+  f16x8_t ef = {}, el = {};
+  f16x4 ef2 = {}, el2 = {};
+  if (first) {   // the previous segment's E_right, dy = 0..2
+    const _Float16* q = e + ((ps - 1) >> 3) * kZrE + 12;
+    ef = *reinterpret_cast<const f16x8_t*>(q);
+    ef2 = *reinterpret_cast<const f16x4*>(q + 8);
+  }
+  if (last) {    // the next segment's E_left
+    const _Float16* q = e + ((ps + 4) >> 3) * kZrE;
+    el = *reinterpret_cast<const f16x8_t*>(q);
+    el2 = *reinterpret_cast<const f16x4*>(q + 8);
+  }
+  auto rv = [&](int k, int dy, int o) { const int i = k * 12 + dy * 4 + o; return (float)r[i >> 3][i & 7]; };
+  auto ev = [&](const f16x8_t& a, const f16x4& a2, int dy, int o) {
+    const int i = dy * 4 + o;
+    return i < 8 ? (float)a[i] : (float)a2[i - 8];
+  };
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    o2[0][o] += rv(0, 2, o) + ev(ef, ef2, 2, o);
+    o1[0][o] += rv(0, 1, o) + ev(ef, ef2, 1, o);
+    o0[0][o] += rv(0, 0, o) + ev(ef, ef2, 0, o);
+#pragma unroll
+    for (int k = 1; k < 3; ++k) {
+      o2[k][o] += rv(k, 2, o);
+      o1[k][o] += rv(k, 1, o);
+      o0[k][o] += rv(k, 0, o);
+    }
+    o2[3][o] += rv(3, 2, o) + ev(el, el2, 2, o);
+    o1[3][o] += rv(3, 1, o) + ev(el, el2, 1, o);
+    o0[3][o] += rv(3, 0, o) + ev(el, el2, 0, o);
+  }
+}
+
+// strips of TS_SR output rows per thread (four pixels wide): the thread walks source rows y0 - 1 .. y0 + SR
+// once, each feeding the three output rows around it, so a row-sum record is read (SR + 2) / SR times instead
+// of the three 8-byte pieces of it being fetched by three output rows' threads (PMC: 1.6x the minimum bytes)
+constexpr int TS_SR = 8;
+template <typename T>
+__global__ void __launch_bounds__(256) tap_sum3x3_strip_kernel(const _Float16* __restrict__ zh,
+                                                               const _Float16* __restrict__ zx, int B, int H, int W,
+                                                               T* __restrict__ y, int ldy, uint8_t* __restrict__ u8,
+                                                               int vec) {
+  const int nb = (int)gridDim.x;
+  const int bid = (nb & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3);
+  const long g = (long)bid * 256 + threadIdx.x;   // (sample, strip, 4-pixel column group)
+  const int gpr = W / 4, strips = H / TS_SR;
+  const long sg = g / gpr;
+  if (sg >= (long)B * strips) return;
+  const int b = (int)(sg / strips), y0 = (int)(sg - (long)b * strips) * TS_SR, ox = (int)(g - sg * gpr) * 4;
+  const long zi = (long)b * zr_image(H * W);
+  // o2: the output row that source row s completes (s - 1), o1: row s, o0: row s + 1
+  float a2[4][3] = {}, a1[4][3] = {}, a0[4][3] = {};
+  for (int sr = y0 - 1; sr <= y0 + TS_SR; ++sr) {
+    if (sr >= 0 && sr < H) {
+      zr_row4(zh + zi, H, W, sr, ox, a2, a1, a0);
+      zr_row4(zx + zi, H, W, sr, ox, a2, a1, a0);
+    }
+    if (sr - 1 >= y0) tap_out4(a2, ((long)b * H + sr - 1) * W + ox, y, ldy, u8, vec);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int o = 0; o < 3; ++o) {
+        a2[k][o] = a1[k][o];
+        a1[k][o] = a0[k][o];
+        a0[k][o] = 0.f;
+      }
+  }
+}
+
 int tap_sum3x3(int dt, const void* zh, const void* zx, int B, int H, int W, void* y, int ldy, uint8_t* u8,
                hipStream_t s) {
   if (W % 8 || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16 || !is16(dt)) return -1;
-  const dim3 g((unsigned)(((long)B * H * W / 4 + 255) / 256));
   // whole-dword stores where the caller's buffers allow them (an out= view may start anywhere)
   const int vec = (ldy == 3 && (uintptr_t)y % 8 == 0 ? 1 : 0) | ((uintptr_t)u8 % 4 == 0 ? 2 : 0);
+  static const int strip = GHOST_KNOB("GHOST_TAPSUM_STRIP", 1);
+  if (strip && H % TS_SR == 0) {
+    const dim3 gs((unsigned)(((long)B * (H / TS_SR) * (W / 4) + 255) / 256));
+    if (dt == GHOST_F16)
+      hipLaunchKernelGGL(tap_sum3x3_strip_kernel<_Float16>, gs, dim3(256), 0, s, (const _Float16*)zh,
+                         (const _Float16*)zx, B, H, W, (_Float16*)y, ldy, u8, vec);
+    else
+      hipLaunchKernelGGL(tap_sum3x3_strip_kernel<bf16>, gs, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx,
+                         B, H, W, (bf16*)y, ldy, u8, vec);
+    return (int)hipGetLastError();
+  }
+  const dim3 g((unsigned)(((long)B * H * W / 4 + 255) / 256));
   if (dt == GHOST_F16)
     hipLaunchKernelGGL(tap_sum3x3_kernel<_Float16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, B, H,
                        W, (_Float16*)y, ldy, u8, vec);
