@@ -1412,60 +1412,11 @@ int aad_v3(const AadV3Desc& d, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// AADBlk8's output conv from the tap partials (tap_rows.h): each thread takes four consecutive output pixels,
-// sums the row sums of the three source rows of both producers' buffers (zh: the h path, zx: last_add_block's
-// x') plus the segment-end terms at columns 8j - 1 / 8j, then tanh, and stores the 4 x 3 outputs and their BGR
-// uint8 copy (faceshifter_run.py:20-21) as whole dwords.  Every row-sum slot is read by exactly one output
-// pixel; consecutive 1024-pixel blocks share an XCD, so the three output rows that read one source row meet it
-// in the same L2.
+// AADBlk8's output conv from the tap partials (tap_rows.h): output (y, x) is the sum over both producers'
+// buffers (zh: the h path, zx: last_add_block's x') of the row sums R_dy of source row y + dy - 1, plus the
+// segment-end terms at columns 8j - 1 / 8j; then tanh, and the BGR uint8 copy of faceshifter_run.py:20-21.
+// A thread takes four pixels of an 8-row strip (tap_sum3x3_strip_kernel); consecutive blocks share an XCD.
 // ---------------------------------------------------------------------------------------------
-GHOST_DEV void zr_gather4(const _Float16* __restrict__ z, int H, int W, int y, int x0, float (&s)[4][3]) {
-  typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
-  const _Float16* __restrict__ e = z + (long)H * W * kZrR;
-  const bool first = (x0 & 7) == 0 && x0 > 0, last = (x0 & 7) == 4 && x0 + 4 < W;   // pixel 0 / pixel 3 at a segment end
-#pragma unroll
-  for (int dy = 0; dy < 3; ++dy) {
-    const int yy = y + dy - 1;
-    if (yy < 0 || yy >= H) continue;
-    const long ps = (long)yy * W + x0;
-    f16x4 r[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r[k] = *reinterpret_cast<const f16x4*>(z + (ps + k) * kZrR + dy * 4);
-    f16x4 cf = {0, 0, 0, 0}, cl = {0, 0, 0, 0};
-    if (first) cf = *reinterpret_cast<const f16x4*>(e + ((ps - 1) >> 3) * kZrE + 12 + dy * 4);   // previous E_right
-    if (last) cl = *reinterpret_cast<const f16x4*>(e + ((ps + 4) >> 3) * kZrE + dy * 4);         // next E_left
-#pragma unroll
-    for (int o = 0; o < 3; ++o) {
-      s[0][o] += (float)r[0][o] + (float)cf[o];
-      s[1][o] += (float)r[1][o];
-      s[2][o] += (float)r[2][o];
-      s[3][o] += (float)r[3][o] + (float)cl[o];
-    }
-  }
-}
-
-template <typename T>
-GHOST_DEV void tap_out4(const float (&s)[4][3], long q, T* __restrict__ y, int ldy, uint8_t* __restrict__ u8, int vec);
-
-template <typename T>
-__global__ void __launch_bounds__(256) tap_sum3x3_kernel(const _Float16* __restrict__ zh, const _Float16* __restrict__ zx,
-                                                         int B, int H, int W, T* __restrict__ y, int ldy,
-                                                         uint8_t* __restrict__ u8, int vec) {
-  // XCD-aware: workgroup id i runs on XCD i % 8; consecutive logical blocks go to one XCD (grid % 8 == 0)
-  const int nb = (int)gridDim.x;
-  const int bid = (nb & 7) ? (int)blockIdx.x : (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3);
-  const long g = (long)bid * 256 + threadIdx.x;   // group of 4 pixels
-  const int gpr = W / 4;
-  const long rowg = g / gpr;
-  if (rowg >= (long)B * H) return;
-  const int b = (int)(rowg / H), oy = (int)(rowg - (long)b * H), ox = (int)(g - rowg * gpr) * 4;
-  const long zi = (long)b * zr_image(H * W);
-  float s[4][3] = {};
-  zr_gather4(zh + zi, H, W, oy, ox, s);
-  zr_gather4(zx + zi, H, W, oy, ox, s);
-  tap_out4(s, rowg * W + ox, y, ldy, u8, vec);
-}
-
 // four output pixels of one row from their sums: tanh, the 12 values, their BGR uint8 copy
 // (faceshifter_run.py:20-21), as whole dwords where the caller's buffers allow them (vec)
 template <typename T>
@@ -1586,27 +1537,16 @@ __global__ void __launch_bounds__(256) tap_sum3x3_strip_kernel(const _Float16* _
 
 int tap_sum3x3(int dt, const void* zh, const void* zx, int B, int H, int W, void* y, int ldy, uint8_t* u8,
                hipStream_t s) {
-  if (W % 8 || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16 || !is16(dt)) return -1;
+  if (W % 8 || H % TS_SR || ldy < 3 || (uintptr_t)zh % 16 || (uintptr_t)zx % 16 || !is16(dt)) return -1;
   // whole-dword stores where the caller's buffers allow them (an out= view may start anywhere)
   const int vec = (ldy == 3 && (uintptr_t)y % 8 == 0 ? 1 : 0) | ((uintptr_t)u8 % 4 == 0 ? 2 : 0);
-  static const int strip = GHOST_KNOB("GHOST_TAPSUM_STRIP", 1);
-  if (strip && H % TS_SR == 0) {
-    const dim3 gs((unsigned)(((long)B * (H / TS_SR) * (W / 4) + 255) / 256));
-    if (dt == GHOST_F16)
-      hipLaunchKernelGGL(tap_sum3x3_strip_kernel<_Float16>, gs, dim3(256), 0, s, (const _Float16*)zh,
-                         (const _Float16*)zx, B, H, W, (_Float16*)y, ldy, u8, vec);
-    else
-      hipLaunchKernelGGL(tap_sum3x3_strip_kernel<bf16>, gs, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx,
-                         B, H, W, (bf16*)y, ldy, u8, vec);
-    return (int)hipGetLastError();
-  }
-  const dim3 g((unsigned)(((long)B * H * W / 4 + 255) / 256));
+  const dim3 gs((unsigned)(((long)B * (H / TS_SR) * (W / 4) + 255) / 256));
   if (dt == GHOST_F16)
-    hipLaunchKernelGGL(tap_sum3x3_kernel<_Float16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, B, H,
-                       W, (_Float16*)y, ldy, u8, vec);
+    hipLaunchKernelGGL(tap_sum3x3_strip_kernel<_Float16>, gs, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx,
+                       B, H, W, (_Float16*)y, ldy, u8, vec);
   else
-    hipLaunchKernelGGL(tap_sum3x3_kernel<bf16>, g, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, B, H, W,
-                       (bf16*)y, ldy, u8, vec);
+    hipLaunchKernelGGL(tap_sum3x3_strip_kernel<bf16>, gs, dim3(256), 0, s, (const _Float16*)zh, (const _Float16*)zx, B,
+                       H, W, (bf16*)y, ldy, u8, vec);
   return (int)hipGetLastError();
 }
 
